@@ -1,0 +1,46 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, 'audio-to-motion-generation_amd')
+for p in (REPO, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+GOLDEN = os.path.join(REPO, 'tests', 'golden')
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (runs through the HIP C-ABI)')
+    config.addinivalue_line('markers', 'slow: long CPU test')
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def golden_keys():
+    with open(os.path.join(GOLDEN, 'state_dict_keys.json')) as f:
+        return json.load(f)
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    den = max(np.abs(b).max(), 1e-30) if b.size else 1.0
+    return float(np.abs(a - b).max() / den) if b.size else 0.0
+
+
+@pytest.fixture(scope='session')
+def g_state():
+    from oracle import weights
+    return weights.make_state_dict(golden_keys()['G'], seed=1234)
+
+
+@pytest.fixture(scope='session')
+def d_state():
+    from oracle import weights
+    return weights.make_state_dict(golden_keys()['D'], seed=1235)

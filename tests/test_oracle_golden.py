@@ -1,0 +1,115 @@
+"""Pin the CPU oracle against golden vectors produced by running the reference itself
+(oracle/make_fixtures.py).  CPU only."""
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, rel_err
+
+
+def test_mel_build_config():
+    from oracle import mel
+    z = golden('mel.npz')
+    for w, ref in zip(z['mel_build_wave'], z['mel_build_out']):
+        out = mel.log_mel(w, **mel.BUILD_CFG)
+        assert out.shape == (64, 128)
+        assert rel_err(out, ref) < 1e-12
+    m = mel.mel_matrix(128, 1025, 16000, 125.0, 7500.0)
+    assert np.array_equal(m, z['mel_build_matrix'])
+
+
+def test_mel_other_configs_and_edges():
+    from oracle import mel
+    z = golden('mel.npz')
+    out = mel.log_mel(z['mel_repr_wave'], sample_rate=16000, log_offset=0.01, window_secs=0.025,
+                      hop_secs=0.010, num_mel_bins=64, lower_hz=125, upper_hz=7500)
+    assert rel_err(out, z['mel_repr_out']) < 1e-12
+    assert rel_err(mel.log_mel(z['mel_default_wave']), z['mel_default_out']) < 1e-12
+    assert rel_err(mel.log_mel(z['mel_oneframe_wave'], **mel.BUILD_CFG), z['mel_oneframe_out']) < 1e-12
+    assert mel.log_mel(z['mel_oneframe_wave'][:2047], **mel.BUILD_CFG).shape == z['mel_empty_out'].shape
+    cases = [dict(lower_hz=-1.0), dict(lower_hz=8000.0, upper_hz=7000.0), dict(upper_hz=9000.0)]
+    for kw, msg in zip(cases, z['mel_errors']):
+        args = {**dict(lower_hz=125.0, upper_hz=7500.0), **kw}
+        with pytest.raises(ValueError) as e:
+            mel.mel_matrix(8, 33, 16000, **args)
+        assert str(e.value) == msg
+
+
+def test_losses_oracle():
+    from oracle import model
+    z = golden('losses.npz')
+    gen, real = torch.from_numpy(z['gen']), torch.from_numpy(z['real'])
+    assert model.HAND_TRIPLES == [tuple(t) for t in z['hand_triples'].tolist()]
+    assert model.BODY_TRIPLES == [tuple(t) for t in z['body_triples'].tolist()]
+    assert rel_err(model.bone_length_loss(real, gen), z['bone']) < 1e-6
+    assert rel_err(model.hand_angle_loss(gen), z['hand']) < 1e-6
+    assert rel_err(model.body_angle_loss(gen), z['body']) < 1e-6
+    assert rel_err(model.angle_loss(gen), z['angle']) < 1e-6
+
+
+def test_generator_eval_oracle(g_state):
+    from oracle import model
+    z = golden('g_eval_b2t64.npz')
+    with torch.no_grad():
+        out, losses = model.generator(g_state, torch.from_numpy(z['audio']),
+                                      real_pose=torch.from_numpy(z['real_pose']))
+    assert rel_err(out, z['pose']) < 1e-5
+    assert rel_err(losses[0], z['bone']) < 1e-5
+    assert rel_err(losses[1], z['angle']) < 1e-5
+
+
+def test_discriminator_eval_oracle(d_state):
+    from oracle import model
+    z = golden('g_eval_b2t64.npz')
+    rm = torch.diff(torch.from_numpy(z['real_pose']), dim=1)
+    with torch.no_grad():
+        out = model.discriminator(d_state, rm)
+    assert rel_err(out, z['d_real']) < 1e-5
+
+
+@pytest.mark.slow
+def test_generator_longform_oracle(g_state):
+    from oracle import model
+    z = golden('g_eval_b1t480.npz')
+    with torch.no_grad():
+        out, losses = model.generator(g_state, torch.from_numpy(z['audio']))
+    assert rel_err(out, z['pose']) < 1e-5
+    assert rel_err(losses[0], z['angle']) < 1e-5
+
+
+def bn_cancelled(name):
+    """Parameters whose true gradient is exactly zero, so computed grads are rounding noise:
+    conv biases that feed a train-mode BatchNorm (the batch mean removes them) and
+    SelfAttention key biases (q.b is constant over the keys the softmax runs over)."""
+    return name.endswith(('.conv.bias', '.conv_transpose.bias', '.key_conv.bias')) or \
+        re.fullmatch(r'conv[123](\.\d)?\.(0|4|9)\.bias', name) is not None
+
+
+def test_train_step_oracle(g_state, d_state):
+    """One G-step + D-step in train mode (BN batch stats, p=0): losses and grads."""
+    from oracle import model
+    z = golden('g_eval_b2t64.npz')
+    t = golden('train_step_b2t64.npz')
+    gs = {k: v.clone().requires_grad_(v.is_floating_point() and 'running' not in k) for k, v in g_state.items()}
+    ds = {k: v.clone().requires_grad_(v.is_floating_point() and 'running' not in k) for k, v in d_state.items()}
+    audio, pose = torch.from_numpy(z['audio']), torch.from_numpy(z['real_pose'])
+    fake, internal = model.generator(gs, audio, real_pose=pose, train=True)
+    fd = model.discriminator(ds, torch.diff(fake, dim=1), train=True)
+    l1, sm, jk = model.motion_terms(pose, fake)
+    adv = torch.nn.functional.mse_loss(fd, torch.full((2, 4), 0.93))
+    loss = l1 + adv + 0.1 * sm + 0.05 * jk + internal[0] + internal[1]
+    assert rel_err(fake.detach(), t['fake_pose']) < 1e-4
+    assert rel_err(loss.detach(), t['G_loss']) < 1e-5
+    loss.backward()
+    names = list(t['gG_names'])
+    for i, n in enumerate(names):
+        if bn_cancelled(n):
+            continue
+        g = gs[n].grad.double().reshape(-1).numpy()
+        ix = t['gG_idx'][i]
+        ok = ix >= 0
+        ref = t['gG_val'][i][ok]
+        scale = max(np.sqrt(t['gG_sumsq'][i] / max(g.size, 1)), np.abs(ref).max(), 1e-12)
+        assert np.abs(g[ix[ok]] - ref).max() / scale < 2e-3, n
