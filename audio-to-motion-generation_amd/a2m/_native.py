@@ -1,0 +1,92 @@
+"""ctypes binding of liba2m_hip.so (C-ABI declared in include/a2m.h).
+
+The library is REQUIRED: there is no CPU or eager-PyTorch fallback.  Importing a2m on a
+machine without the built library raises immediately (build it with
+`make -C audio-to-motion-generation_amd` or `python -c "import __graft_entry__ as g; g.build()"`).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('A2M_LIB', os.path.join(_HERE, 'liba2m_hip.so'))
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+F64 = ctypes.c_double
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/a2m.h
+SIGNATURES = {
+    'a2m_last_error': (ctypes.c_char_p, []),
+    'a2m_version': (ctypes.c_int, []),
+    'a2m_logmel_num_frames': (I64, [I64, I32, I32]),
+    'a2m_logmel_geometry': (ctypes.c_int, [I32, F64, F64, ctypes.POINTER(I32), ctypes.POINTER(I32),
+                                           ctypes.POINTER(I32)]),
+    'a2m_logmel_plan_bytes': (SZ, [I32, F64, F64, I32, F64, F64]),
+    'a2m_logmel_plan_build': (ctypes.c_int, [I32, F64, F64, I32, F64, F64, P, SZ]),
+    'a2m_logmel_f32': (ctypes.c_int, [P, I64, I64, I64, I32, I32, I32, I32, P, F32, P, P]),
+    'a2m_conv1d_fwd_f32': (ctypes.c_int, [P, I64, I64, I64, I32, I32, I32, P, P, I32, I32, I32, I32,
+                                          P, P, P, P, F32, I32, F32, P, I64, I64, I64, P, SZ, P]),
+    'a2m_convt1d_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, I32, I32, I32, I32, I32,
+                                           P, P, P, P, F32, I32, F32, P, I64, I64, P, SZ, P]),
+    'a2m_conv2d_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, I32,
+                                          P, P, P, P, F32, I32, F32, P, I32, I32, I32, I32, P, SZ, P]),
+    'a2m_mean_time_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P]),
+    'a2m_repeat_time_f32': (ctypes.c_int, [P, I32, I32, I32, P, I64, I64, P]),
+    'a2m_interp_time_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, I32, P]),
+    'a2m_self_attention_fwd_f32': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, P, P, P, P, P,
+                                                  I64, P, P, P, SZ, P]),
+    'a2m_self_attention_ws_bytes': (SZ, [I32, I32, I32]),
+    'a2m_channel_attention_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, P, P, I32, P, P, P, P, P]),
+    'a2m_layernorm_fwd_f32': (ctypes.c_int, [P, I32, I32, P, P, F32, P, I32, I64, I64, I64, P, P, P]),
+    'a2m_graph_layer_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32, P, P,
+                                               P, P, SZ, P]),
+    'a2m_pose_losses_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, P, P, SZ, P]),
+}
+
+A2M_EINVAL, A2M_EHIP, A2M_EWS = -1, -2, -3
+
+
+class A2MError(RuntimeError):
+    pass
+
+
+class WorkspaceTooSmall(A2MError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f'a2m: native library not found at {LIB_PATH}; build it first '
+                          f'(make -C audio-to-motion-generation_amd)')
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error():
+    return lib.a2m_last_error().decode()
+
+
+def check(rc, value_error=False):
+    """Raise on a non-zero status (ValueError where the reference raises ValueError)."""
+    if rc == 0:
+        return
+    msg = last_error()
+    if rc == A2M_EWS:
+        raise WorkspaceTooSmall(msg)
+    if rc == A2M_EINVAL and value_error:
+        raise ValueError(msg)
+    raise A2MError(f'a2m error {rc}: {msg}')
+
+
+def exported_symbols():
+    return list(SIGNATURES)

@@ -1,0 +1,224 @@
+"""Drop-in SelfAttention_G / SelfAttention_D (real_motion_model.py) on the MI355X HIP path.
+
+Same constructors, forward signatures, return values and state_dict keys as the reference:
+  SelfAttention_G(time_steps=64, in_channels=256, out_channels=256, out_feats=104, p=0.2)
+      .forward(audio [B,T,128], real_pose=None) -> (pose [B,T,104], [bone?, angle])
+  SelfAttention_D(in_channels=104, out_channels=64, n_downsampling=2, p=0.3, groups=1, aux_classes=10)
+      .forward(motion [B,T-1,104], audio=None, aux_labels=None) -> ([B,4], [aux?])
+"""
+import torch
+import torch.nn as nn
+
+from . import functional as F
+from . import skeleton as S
+from .graph_layers import GATConv, GraphConv
+from .model_layers import (AudioEncoder, ChannelAttention, ConvNormRelu, ResBlock, SelfAttention,
+                           UNet1D, _autograd, _grad_path)
+
+
+class _GraphTopology(nn.Module):
+    """Edge-index templates (persistent buffers, reference keys) + the in-neighbour CSR the
+    fused HIP kernel reads (non-persistent)."""
+
+    def _register_topology(self):
+        self.register_buffer('body_edge_index_template', S.edge_index(0, S.NUM_BODY))
+        self.register_buffer('hand_edge_index_template', S.edge_index(10, S.NUM_HAND))
+        for part, n in (('body', S.NUM_BODY), ('hand', S.NUM_HAND)):
+            ptr, idx = S.in_neighbour_csr(getattr(self, f'{part}_edge_index_template'), n)
+            self.register_buffer(f'_{part}_nbr_ptr', ptr, persistent=False)
+            self.register_buffer(f'_{part}_nbr_idx', idx, persistent=False)
+
+    def topology(self, part):
+        return getattr(self, f'_{part}_nbr_ptr'), getattr(self, f'_{part}_nbr_idx')
+
+
+class SelfAttention_G(_GraphTopology):
+    def __init__(self, time_steps=64, in_channels=256, out_channels=256, out_feats=104, p=0.2):
+        super().__init__()
+        self.audio_encoder = AudioEncoder(output_feats=time_steps, p=p)
+        self.unet = UNet1D(input_channels=in_channels, output_channels=out_channels, p=p)
+        self.body_feats = 20
+        self.hand_feats = out_feats - self.body_feats
+        self.num_body_joints, self.num_hand_joints, self.joint_feat_dim = S.NUM_BODY, S.NUM_HAND, S.FEAT
+        self.skeleton = S.Skeleton2D()
+        self.parents = S.PARENTS
+        self.joint_names = S.JOINT_NAMES
+        self.joint_subset = list(range(out_feats // 2))
+        self.hand_triples = S.triples(10, S.NUM_HAND)
+        self.body_triples = S.triples(0, S.NUM_BODY)
+        self.body_edge_index = S.edge_index(0, S.NUM_BODY)
+        self.hand_edge_index = S.edge_index(10, S.NUM_HAND)
+        self._register_topology()
+        C, J = out_channels, self.joint_feat_dim
+        for part, nj in (('body', S.NUM_BODY), ('hand', S.NUM_HAND)):
+            if part == 'body':
+                pre = [ResBlock(C, type='1d', p=p), ConvNormRelu(C, C, type='1d', leaky=True, p=p),
+                       ChannelAttention(C), SelfAttention(C)]
+                post = [ResBlock(C, type='1d', p=p), ConvNormRelu(C, C, type='1d', leaky=True, p=p),
+                        SelfAttention(C)]
+            else:
+                pre = [ResBlock(C, type='1d', p=p), ConvNormRelu(C, C, type='1d', leaky=True, p=p),
+                       SelfAttention(C), ChannelAttention(C)]
+                post = [ResBlock(C, type='1d', p=p), ConvNormRelu(C, C, type='1d', leaky=True, p=p),
+                        SelfAttention(C), ChannelAttention(C)]
+            setattr(self, f'{part}_decoder_pre', nn.Sequential(*pre))
+            setattr(self, f'{part}_proj_in', nn.Linear(C, nj * J))
+            for L in range(1, 6):
+                layer = GATConv(J, J, heads=4, concat=False) if L % 2 == 1 else GraphConv(J, J)
+                setattr(self, f'{part}_gcn{L}', layer)
+            setattr(self, f'{part}_layer_norms', nn.ModuleList([nn.LayerNorm(J) for _ in range(5)]))
+            setattr(self, f'{part}_relu', nn.LeakyReLU(0.2))
+            setattr(self, f'{part}_dropout', nn.Dropout(p=p))
+            setattr(self, f'{part}_proj_out', nn.Linear(nj * J, C))
+            setattr(self, f'{part}_norm', nn.LayerNorm(C))
+            setattr(self, f'{part}_decoder_post', nn.Sequential(*post))
+            setattr(self, f'{part}_logits', nn.Conv1d(C, self.body_feats if part == 'body' else self.hand_feats, 1))
+
+    # ------------------------------------------------------------------ eval-mode fused path
+    def _graph_stack(self, part, x, out_bct):
+        """proj_in -> 5 x fused {GNN, LN64, LeakyReLU, +res} -> proj_out -> LN -> [B,C,T]."""
+        B, C, T = x.shape
+        nj = getattr(self, f'num_{part}_joints')
+        pin, pout = getattr(self, f'{part}_proj_in'), getattr(self, f'{part}_proj_out')
+        h = torch.empty(B, T, nj * 64, device=x.device)
+        F.conv1d(x, pin.weight, pin.bias, out=h.permute(0, 2, 1))
+        a, b = h.view(B * T * nj, 64), torch.empty(B * T * nj, 64, device=x.device)
+        ptr, idx = self.topology(part)
+        lns = getattr(self, f'{part}_layer_norms')
+        for L in range(5):
+            g = getattr(self, f'{part}_gcn{L + 1}')
+            if L % 2 == 0:
+                F.graph_layer(a, nj, 0, ptr, idx, g.lin.weight, None, g.att_src, g.att_dst, g.bias,
+                              lns[L].weight, lns[L].bias, out=b)
+            else:
+                F.graph_layer(a, nj, 1, ptr, idx, g.lin_rel.weight, g.lin_root.weight, None, None,
+                              g.lin_rel.bias, lns[L].weight, lns[L].bias, out=b)
+            a, b = b, a
+        rows = torch.empty(B, T, C, device=x.device)
+        F.conv1d(a.view(B, T, nj * 64).permute(0, 2, 1), pout.weight, pout.bias, out=rows.permute(0, 2, 1))
+        nrm = getattr(self, f'{part}_norm')
+        return F.layernorm_to_bct(rows.view(B * T, C), nrm.weight, nrm.bias, T, eps=nrm.eps, out=out_bct)
+
+    def _branch(self, part, feats, pose_out, f0):
+        x = getattr(self, f'{part}_decoder_pre')(feats)
+        x = self._graph_stack(part, x, None)
+        x = getattr(self, f'{part}_decoder_post')(x)
+        lg = getattr(self, f'{part}_logits')
+        nf = lg.weight.shape[0]
+        F.conv1d(x, lg.weight, lg.bias, out=pose_out[:, :, f0:f0 + nf].permute(0, 2, 1))
+
+    def forward(self, audio, real_pose=None):
+        if _grad_path(self, audio):
+            return _autograd().generator_forward(self, audio, real_pose)
+        B, T, _ = audio.shape
+        feats = self.unet(self.audio_encoder(audio))
+        out = torch.empty(B, T, self.body_feats + self.hand_feats, device=audio.device)
+        self._branch('body', feats, out, 0)
+        self._branch('hand', feats, out, self.body_feats)
+        losses = F.pose_losses(out, real_pose)
+        internal = [losses[0]] if real_pose is not None else []
+        internal.append(losses[1])
+        return out, internal
+
+    # ------------------------------------------------------------------ reference loss API
+    def compute_bone_length_loss(self, real_pose, gen_pose):
+        return F.pose_losses(gen_pose.contiguous(), real_pose.contiguous())[0]
+
+    def compute_comprehensive_angle_loss(self, gen_pose):
+        return F.pose_losses(gen_pose.contiguous())[1]
+
+
+class SelfAttention_D(_GraphTopology):
+    def __init__(self, in_channels=104, out_channels=64, n_downsampling=2, p=0.3, groups=1, aux_classes=10, **kwargs):
+        super().__init__()
+        assert groups == 1
+        self.n_downsampling, self.groups, self.p = n_downsampling, groups, p
+        self.skeleton = S.Skeleton2D()
+        self.num_body_joints, self.num_hand_joints, self.joint_feat_dim = S.NUM_BODY, S.NUM_HAND, S.FEAT
+        self.body_edge_index = S.edge_index(0, S.NUM_BODY)
+        self.hand_edge_index = S.edge_index(10, S.NUM_HAND)
+        self._register_topology()
+
+        def block(ci, co, k, s, pad=1):
+            return [nn.Conv1d(ci, co, k, s, pad), nn.BatchNorm1d(co), nn.LeakyReLU(0.2), nn.Dropout(p)]
+
+        oc = out_channels
+        self.conv1 = nn.Sequential(*block(in_channels, oc, 4, 2), *block(oc, oc, 4, 1))
+        self.conv2 = nn.ModuleList()
+        cur = oc
+        for n in range(1, n_downsampling + 1):
+            mul = min(2 ** n, 16)
+            self.conv2.append(nn.Sequential(*block(cur, cur * mul, 4, 2), *block(cur * mul, cur * mul, 4, 1)))
+            cur *= mul
+        self.conv3 = nn.Sequential(*block(cur, cur * 2, 4, 1), *block(cur * 2, cur * 4, 4, 1),
+                                   SelfAttention(cur * 4), *block(cur * 4, cur * 4, 3, 1))
+        J = self.joint_feat_dim
+        self.body_proj = nn.Linear(cur * 4 // 2, S.NUM_BODY * J)
+        self.hand_proj = nn.Linear(cur * 4 // 2, S.NUM_HAND * J)
+        self.body_gat = GATConv(J, J, heads=4, concat=False)
+        self.hand_gat = GATConv(J, J, heads=4, concat=False)
+        self.body_graph_out = nn.Linear(S.NUM_BODY * J, cur * 2)
+        self.hand_graph_out = nn.Linear(S.NUM_HAND * J, cur * 2)
+        self.audio_fusion = nn.Conv1d(256, cur * 4, kernel_size=1)
+        out_shape = kwargs.get('out_shape', 1)
+        self.logits = nn.Conv1d(cur * 4 * 2, out_shape, kernel_size=3, stride=1, padding=1)
+        self.aux_classifier = nn.Sequential(nn.Linear(cur * 4, 512), nn.LeakyReLU(0.2), nn.Dropout(p),
+                                            nn.Linear(512, aux_classes))
+        self.aux_loss_fn = nn.CrossEntropyLoss()
+        self.cur = cur
+
+    def conv_blocks(self):
+        """(conv, bn) pairs of the trunk in order, with the SelfAttention position marked."""
+        seqs = [self.conv1] + list(self.conv2) + [self.conv3]
+        out = []
+        for sq in seqs:
+            mods = list(sq)
+            for i, m in enumerate(mods):
+                if isinstance(m, nn.Conv1d):
+                    out.append((m, mods[i + 1]))
+                elif isinstance(m, SelfAttention):
+                    out.append(m)
+        return out
+
+    def forward(self, x, audio=None, aux_labels=None):
+        if audio is not None or aux_labels is not None:
+            raise NotImplementedError('audio fusion / aux classifier are off the training path '
+                                      '(version5_model_train.py never passes them)')
+        if _grad_path(self, x):
+            return _autograd().discriminator_forward(self, x), []
+        h = x.transpose(-1, -2)
+        if h.shape[2] < 4:
+            h = torch.nn.functional.pad(h, (0, 4 - h.shape[2] % 4)).contiguous()
+        blocks = self.conv_blocks()
+        B = x.shape[0]
+        for i, blk in enumerate(blocks):
+            if isinstance(blk, SelfAttention):
+                h = blk(h)
+                continue
+            conv, bn = blk
+            last = i == len(blocks) - 1
+            Tin = h.shape[2]
+            Tout = (Tin + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
+            out = None
+            if last:  # write straight into the first half of the logits' concat buffer
+                cat = torch.empty(B, 2 * conv.out_channels, Tout, device=x.device)
+                out = cat[:, :conv.out_channels]
+            h = F.conv1d(h, conv.weight, conv.bias, conv.stride[0], conv.padding[0],
+                         bn=(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps),
+                         act=F.ACT_LRELU, out=out)
+        C, T = h.shape[1], h.shape[2]
+        g = torch.empty(B, 2 * self.cur * 2, device=x.device)
+        for k, (part, nj) in enumerate((('body', S.NUM_BODY), ('hand', S.NUM_HAND))):
+            half = h[:, k * C // 2:(k + 1) * C // 2]
+            pooled = F.mean_time(half)
+            proj = getattr(self, f'{part}_proj')
+            z = F.linear(pooled, proj.weight, proj.bias).view(B * nj, 64)
+            gat = getattr(self, f'{part}_gat')
+            ptr, idx = self.topology(part)
+            z2 = F.graph_layer(z, nj, 0, ptr, idx, gat.lin.weight, None, gat.att_src, gat.att_dst,
+                               gat.bias, None, None, norm_res=False)
+            go = getattr(self, f'{part}_graph_out')
+            F.linear(z2.view(B, nj * 64), go.weight, go.bias, out=g[:, k * self.cur * 2:(k + 1) * self.cur * 2])
+        F.repeat_time(g, cat[:, C:])
+        lg = F.conv1d(cat, self.logits.weight, self.logits.bias, 1, 1)
+        return lg.transpose(-1, -2).squeeze(-1), []

@@ -1,0 +1,110 @@
+// Internal helpers shared by the a2m HIP translation units (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/a2m.h"
+
+namespace a2m {
+
+void set_error(const char* fmt, ...);
+
+#define A2M_CHECK_ARG(cond, ...)                      \
+  do {                                                \
+    if (!(cond)) {                                    \
+      ::a2m::set_error(__VA_ARGS__);                  \
+      return A2M_EINVAL;                              \
+    }                                                 \
+  } while (0)
+
+#define A2M_CHECK_HIP(expr)                                                     \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      ::a2m::set_error("%s failed: %s", #expr, hipGetErrorString(_e));          \
+      return A2M_EHIP;                                                          \
+    }                                                                           \
+  } while (0)
+
+#define A2M_LAUNCH_CHECK()                                                      \
+  do {                                                                          \
+    hipError_t _e = hipGetLastError();                                          \
+    if (_e != hipSuccess) {                                                     \
+      ::a2m::set_error("kernel launch failed: %s", hipGetErrorString(_e));      \
+      return A2M_EHIP;                                                          \
+    }                                                                           \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------------------
+// Implicit-GEMM operand description.  Element (r, k) of an operand viewed as [R][K]:
+//   r = (r0*R1 + r1)*R2 + r2          k = (k0*K1 + k1)*K2 + k2
+//   h = r1*ar1 + k1*bk1 + ch          w = r2*ar2 + k2*bk2 + cw
+//   valid iff h, w >= 0, h % divh == 0, w % divw == 0, h/divh < Lh, w/divw < Lw
+//   value = base[z*bstride + r0*sr0 + k0*sk0 + (h/divh)*sh + (w/divw)*sw]   (0 if invalid)
+// This one form covers dense row/col-major matrices, conv1d/conv2d im2col (forward),
+// transposed-conv / dgrad gathers (div = stride) and wgrad operands.
+// ---------------------------------------------------------------------------------------
+struct Gather {
+  const float* base;
+  int64_t bstride;
+  int sr0, sk0, sh, sw;
+  int R1, R2, K1, K2;
+  int ar1, ar2, bk1, bk2, ch, cw;
+  int divh, divw, Lh, Lw;
+  int kcontig;  // 1: consecutive k are (usually) adjacent in memory -> k-major thread map
+};
+
+inline Gather dense_rk(const float* p, int ld, int64_t bstride = 0) {  // [R][K] row-major, ld >= K
+  Gather g{};
+  g.base = p; g.bstride = bstride; g.sr0 = ld; g.sk0 = 1;
+  g.R1 = g.R2 = g.K1 = g.K2 = 1; g.divh = g.divw = 1; g.Lh = g.Lw = 1; g.kcontig = 1;
+  return g;
+}
+inline Gather dense_kr(const float* p, int ld, int64_t bstride = 0) {  // [K][R] (r contiguous)
+  Gather g = dense_rk(p, 1, bstride);
+  g.sr0 = 1; g.sk0 = ld; g.kcontig = 0;
+  return g;
+}
+
+// Output / epilogue: C[m][n] -> out[z*bstride + n0*so0 + n1*so1 + n2*so2 + m*som],
+// n = (n0*N1 + n1)*N2 + n2.  v = acc (+bias[m]); BN-eval affine; activation;
+// v = v*gamma[0] (if gamma); v += res1[addr] + res2[addr] (same addressing as out).
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_SIGMOID = 3 };
+
+struct Epilogue {
+  float* out;
+  int64_t bstride;
+  int so0, so1, so2, som;
+  int N1, N2;
+  const float* bias;
+  const float* bn_w; const float* bn_b; const float* bn_rm; const float* bn_rv;
+  float bn_eps;
+  int act;
+  float slope;
+  const float* gamma;
+  const float* res1; const float* res2;
+  int accumulate;  // 1: out += v
+};
+
+inline Epilogue epi_dense(float* out, int ldn, int64_t bstride = 0) {  // out[m][n], ld = ldn
+  Epilogue e{};
+  e.out = out; e.bstride = bstride; e.so0 = 1; e.so1 = 0; e.so2 = 0; e.som = ldn;
+  e.N1 = e.N2 = 1; e.bn_eps = 1e-5f; e.slope = 0.2f;
+  return e;
+}
+
+// Runs C = A . B^T-style implicit GEMM: C[m][n] = sum_k A(m,k) * B(n,k), over `batch`
+// independent problems (grid z), with optional split-K through workspace `ws`.
+int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int K, int batch,
+         void* ws, size_t ws_bytes, hipStream_t stream, int force_split = 0);
+size_t gemm_ws_bytes(int M, int N, int K, int batch);
+
+}  // namespace a2m

@@ -1,0 +1,393 @@
+// Implicit-GEMM engine on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32, exact f32 FMA chain).
+//
+// C[m][n] = sum_k A(m,k) * B(n,k) with A, B described by a2m::Gather (dense matrices,
+// conv im2col, transposed-conv / dgrad gathers, wgrad operands) and a fused epilogue
+// (bias, BatchNorm-eval affine, activation, gamma scale, residual adds, strided store).
+//
+// Tiling: 256 threads = 4 waves in a 2x2 layout, block tile BM x BN (128x128 or 64x64),
+// BK = 16.  Both operands are staged in LDS as [row][k] with a 20-float (80 B) row pitch:
+// a wave64 lane (i = lane&31, h = lane>>5) reads its 8 k-values of row i as two
+// ds_read_b128 (conflict-free at this pitch) and feeds MFMA sub-step s with k = 8h + s --
+// the MFMA's k slot assignment is free as long as A and B agree.  Global loads for tile
+// k+1 are issued into registers before the MFMAs of tile k; LDS is double-buffered so one
+// barrier per K-step suffices.  Split-K writes fp32 partial slabs to a workspace that a
+// second kernel reduces in a fixed order (bitwise reproducible) and runs the epilogue on.
+#include "a2m_internal.h"
+
+namespace a2m {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 16;
+constexpr int LDK = BK + 4;
+
+struct GemmArgs {
+  Gather A, B;
+  Epilogue E;
+  int M, N, K;
+  int splits, kchunk;
+  float* partial;
+};
+
+struct RowInfo {
+  int base, h, w;
+  bool valid;
+};
+
+__device__ __forceinline__ RowInfo row_info(const Gather& g, int r, int R) {
+  RowInfo ri;
+  ri.valid = r < R;
+  int rr = ri.valid ? r : 0;
+  int r2 = rr % g.R2;
+  int t = rr / g.R2;
+  int r1 = t % g.R1;
+  int r0 = t / g.R1;
+  ri.base = r0 * g.sr0;
+  ri.h = r1 * g.ar1 + g.ch;
+  ri.w = r2 * g.ar2 + g.cw;
+  return ri;
+}
+
+struct KPos {
+  int k, k0, k1, k2;
+};
+
+__device__ __forceinline__ KPos kpos(const Gather& g, int k) {
+  KPos p;
+  p.k = k;
+  p.k2 = k % g.K2;
+  int t = k / g.K2;
+  p.k1 = t % g.K1;
+  p.k0 = t / g.K1;
+  return p;
+}
+
+__device__ __forceinline__ void kinc(const Gather& g, KPos& p) {
+  ++p.k;
+  if (++p.k2 == g.K2) {
+    p.k2 = 0;
+    if (++p.k1 == g.K1) {
+      p.k1 = 0;
+      ++p.k0;
+    }
+  }
+}
+
+__device__ __forceinline__ float gather_elem(const Gather& g, const float* base, const RowInfo& ri,
+                                             const KPos& p, int K) {
+  int h = ri.h + p.k1 * g.bk1;
+  int w = ri.w + p.k2 * g.bk2;
+  bool v = ri.valid && p.k < K && h >= 0 && w >= 0;
+  if (g.divh > 1) {
+    v = v && (h % g.divh) == 0;
+    h /= g.divh;
+  }
+  if (g.divw > 1) {
+    v = v && (w % g.divw) == 0;
+    w /= g.divw;
+  }
+  v = v && h < g.Lh && w < g.Lw;
+  return v ? base[ri.base + p.k0 * g.sk0 + h * g.sh + w * g.sw] : 0.f;
+}
+
+// MODE 0: dense k-contiguous, float4 loads.  MODE 1: k-contiguous gather (scalar).
+// MODE 2: row-contiguous gather (consecutive lanes -> consecutive rows).
+template <int BR, int MODE>
+struct TileLoader {
+  static constexpr int NPASS = BR / 64;             // k-major maps: 64 rows x 4 quads / pass
+  static constexpr int KPT = BK * BR / 256;         // row-major map: k per thread
+  static constexpr int NREG = BK * BR / 256;        // floats per thread
+  const Gather* g;
+  const float* base;
+  int K;
+  RowInfo ri[MODE == 2 ? 1 : NPASS];
+  int lrow[MODE == 2 ? 1 : NPASS];
+  int kq;  // k offset of this thread inside the tile
+  float r[NREG];
+
+  __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid) {
+    g = &gg;
+    base = gg.base + (int64_t)z * gg.bstride;
+    K = KK;
+    if (MODE == 2) {
+      lrow[0] = tid % BR;
+      kq = (tid / BR) * KPT;
+      ri[0] = row_info(gg, row0 + lrow[0], R);
+    } else {
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p) {
+        lrow[p] = tid / 4 + p * 64;
+        ri[p] = row_info(gg, row0 + lrow[p], R);
+      }
+      kq = (tid % 4) * 4;
+    }
+  }
+
+  __device__ __forceinline__ void load(int k0) {
+    if (MODE == 0) {
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p) {
+        int k = k0 + kq;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ri[p].valid && k < K) v = *reinterpret_cast<const float4*>(base + ri[p].base + k);
+        r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
+      }
+    } else if (MODE == 1) {
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p) {
+        KPos kp = kpos(*g, k0 + kq);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          r[p * 4 + j] = gather_elem(*g, base, ri[p], kp, K);
+          kinc(*g, kp);
+        }
+      }
+    } else {
+      KPos kp = kpos(*g, k0 + kq);
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        r[j] = gather_elem(*g, base, ri[0], kp, K);
+        kinc(*g, kp);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(float* lds) const {
+    if (MODE == 2) {
+      float* dst = lds + lrow[0] * LDK + kq;
+#pragma unroll
+      for (int j = 0; j < KPT; j += 4)
+        *reinterpret_cast<float4*>(dst + j) = make_float4(r[j], r[j + 1], r[j + 2], r[j + 3]);
+    } else {
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p)
+        *reinterpret_cast<float4*>(lds + lrow[p] * LDK + kq) =
+            make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
+    }
+  }
+};
+
+__device__ __forceinline__ int64_t epi_addr(const Epilogue& E, int m, int n) {
+  int n2 = n % E.N2;
+  int t = n / E.N2;
+  int n1 = t % E.N1;
+  int n0 = t / E.N1;
+  return (int64_t)n0 * E.so0 + (int64_t)n1 * E.so1 + (int64_t)n2 * E.so2 + (int64_t)m * E.som;
+}
+
+__device__ __forceinline__ float epi_value(const Epilogue& E, float v, int m) {
+  if (E.bias) v += E.bias[m];
+  if (E.bn_w) v = (v - E.bn_rm[m]) * (E.bn_w[m] / sqrtf(E.bn_rv[m] + E.bn_eps)) + E.bn_b[m];
+  if (E.act == ACT_RELU) v = v > 0.f ? v : 0.f;
+  else if (E.act == ACT_LRELU) v = v > 0.f ? v : v * E.slope;
+  else if (E.act == ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+  if (E.gamma) v *= E.gamma[0];
+  return v;
+}
+
+__device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int m, int64_t a) {
+  int64_t off = (int64_t)z * E.bstride + a;
+  v = epi_value(E, v, m);
+  if (E.res1) v += E.res1[off];
+  if (E.res2) v += E.res2[off];
+  if (E.accumulate) v += E.out[off];
+  E.out[off] = v;
+}
+
+template <int BM, int BN, int MA, int MB>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const int zz = blockIdx.z;
+  const int batch = zz / args.splits, split = zz % args.splits;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = split * args.kchunk;
+  const int kend = min(args.K, kbeg + args.kchunk);
+
+  TileLoader<BM, MA> la;
+  TileLoader<BN, MB> lb;
+  la.init(args.A, batch, m0, args.M, args.K, tid);
+  lb.init(args.B, batch, n0, args.N, args.K, tid);
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
+
+  if (kbeg < kend) {
+    la.load(kbeg);
+    lb.load(kbeg);
+    la.store(lds);
+    lb.store(lds + BM * LDK);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int k = kbeg; k < kend; k += BK) {
+    const bool has_next = k + BK < kend;
+    if (has_next) {
+      la.load(k + BK);
+      lb.load(k + BK);
+    }
+    const float* As = lds + cur * (BM + BN) * LDK;
+    const float* Bs = As + BM * LDK;
+    float af[TM][8], bf[TN][8];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const float* p = As + (wm * (BM / 2) + t * 32 + li) * LDK + lh * 8;
+      float4 v0 = *reinterpret_cast<const float4*>(p);
+      float4 v1 = *reinterpret_cast<const float4*>(p + 4);
+      af[t][0] = v0.x; af[t][1] = v0.y; af[t][2] = v0.z; af[t][3] = v0.w;
+      af[t][4] = v1.x; af[t][5] = v1.y; af[t][6] = v1.z; af[t][7] = v1.w;
+    }
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const float* p = Bs + (wn * (BN / 2) + u * 32 + li) * LDK + lh * 8;
+      float4 v0 = *reinterpret_cast<const float4*>(p);
+      float4 v1 = *reinterpret_cast<const float4*>(p + 4);
+      bf[u][0] = v0.x; bf[u][1] = v0.y; bf[u][2] = v0.z; bf[u][3] = v0.w;
+      bf[u][4] = v1.x; bf[u][5] = v1.y; bf[u][6] = v1.z; bf[u][7] = v1.w;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][s], bf[u][s], acc[t][u], 0, 0, 0);
+    if (has_next) {
+      float* nxt = lds + (cur ^ 1) * (BM + BN) * LDK;
+      la.store(nxt);
+      lb.store(nxt + BM * LDK);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // epilogue
+#pragma unroll
+  for (int u = 0; u < TN; ++u) {
+    const int n = n0 + wn * (BN / 2) + u * 32 + li;
+    if (n >= args.N) continue;
+    if (args.partial) {
+      float* dst = args.partial + (int64_t)zz * args.M * args.N + n;
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = m0 + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+          if (m < args.M) dst[(int64_t)m * args.N] = acc[t][u][q];
+        }
+    } else {
+      const int64_t an = epi_addr(args.E, 0, n);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = m0 + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+          if (m < args.M) epi_store(args.E, batch, acc[t][u][q], m, an + (int64_t)m * args.E.som);
+        }
+    }
+  }
+}
+
+__global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
+  const int64_t MN = (int64_t)args.M * args.N;
+  const int64_t total = MN * batch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int z = (int)(i / MN);
+    const int64_t mn = i - (int64_t)z * MN;
+    const int m = (int)(mn / args.N), n = (int)(mn - (int64_t)m * args.N);
+    const float* p = args.partial + (int64_t)z * args.splits * MN + mn;
+    float v = 0.f;
+    for (int s = 0; s < args.splits; ++s) v += p[s * MN];
+    epi_store(args.E, z, v, m, epi_addr(args.E, m, n));
+  }
+}
+
+static int operand_mode(const Gather& g, int K) {
+  if (!g.kcontig) return 2;
+  const bool dense = g.K1 == 1 && g.K2 == 1 && g.sk0 == 1 && g.Lh == 1 && g.Lw == 1 &&
+                     g.sh == 0 && g.sw == 0 && g.ch == 0 && g.cw == 0 && g.divh == 1 && g.divw == 1;
+  const bool aligned = (reinterpret_cast<uintptr_t>(g.base) % 16 == 0) && (g.sr0 % 4 == 0) &&
+                       (g.bstride % 4 == 0) && (K % 4 == 0);
+  return dense && aligned ? 0 : 1;
+}
+
+struct Plan {
+  int bm, splits, kchunk;
+};
+
+static Plan plan_for(int M, int N, int K, int batch) {
+  Plan p;
+  const int64_t t128 = cdiv(M, 128) * cdiv(N, 128) * (int64_t)batch;
+  p.bm = (M > 64 && N > 64 && t128 >= 160) ? 128 : 64;
+  const int64_t tiles = p.bm == 128 ? t128 : cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
+  int splits = 1;
+  const int64_t target = 512;
+  while (tiles * splits * 2 <= target && K / (splits * 2) >= 256) splits *= 2;
+  p.kchunk = (int)(cdiv(cdiv(K, splits), BK) * BK);
+  p.splits = (int)cdiv(K, p.kchunk);
+  return p;
+}
+
+size_t gemm_ws_bytes(int M, int N, int K, int batch) {
+  Plan p = plan_for(M, N, K, batch);
+  return p.splits > 1 ? (size_t)p.splits * batch * M * N * sizeof(float) : 0;
+}
+
+template <int BM, int BN>
+static void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
+  dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
+#define A2M_L(MA_, MB_) \
+  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, MA_, MB_>), grid, dim3(256), 0, st, a); return; }
+  A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2)
+  A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2)
+  A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2)
+#undef A2M_L
+}
+
+int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int K, int batch,
+         void* ws, size_t ws_bytes, hipStream_t stream, int force_split) {
+  A2M_CHECK_ARG(M > 0 && N > 0 && K >= 0 && batch > 0, "gemm: bad sizes M=%d N=%d K=%d batch=%d",
+                M, N, K, batch);
+  GemmArgs a;
+  a.A = A; a.B = B; a.E = E; a.M = M; a.N = N; a.K = K;
+  Plan p = plan_for(M, N, K, batch);
+  if (force_split > 0) {
+    p.kchunk = (int)(cdiv(cdiv(K, force_split), BK) * BK);
+    p.splits = (int)cdiv(K, p.kchunk);
+  }
+  if (K == 0) { p.splits = 1; p.kchunk = BK; }
+  a.splits = p.splits;
+  a.kchunk = p.kchunk;
+  a.partial = nullptr;
+  if (p.splits > 1) {
+    const size_t need = (size_t)p.splits * batch * M * N * sizeof(float);
+    if (ws == nullptr || ws_bytes < need) {
+      set_error("gemm: workspace too small (%zu < %zu bytes)", ws_bytes, need);
+      return A2M_EWS;
+    }
+    a.partial = static_cast<float*>(ws);
+  }
+  const int ma = operand_mode(A, K), mb = operand_mode(B, K);
+  if (p.bm == 128) launch_tile<128, 128>(a, ma, mb, batch, stream);
+  else launch_tile<64, 64>(a, ma, mb, batch, stream);
+  A2M_LAUNCH_CHECK();
+  if (p.splits > 1) {
+    const int64_t total = (int64_t)M * N * batch;
+    const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, a, batch);
+    A2M_LAUNCH_CHECK();
+  }
+  return A2M_OK;
+}
+
+}  // namespace a2m

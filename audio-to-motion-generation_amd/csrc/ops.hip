@@ -1,0 +1,412 @@
+// Convolution / linear / attention / normalisation entry points of the C-ABI.
+// The GEMM-shaped work goes through the implicit-GEMM MFMA engine (gemm.hip); the small
+// row-wise reductions (softmax, LayerNorm, channel pooling) are wave64 kernels here.
+#include <algorithm>
+#include <cstring>
+
+#include "a2m_internal.h"
+
+namespace a2m {
+
+static Epilogue epi_bn(float* y, const float* bias, const float* bn_w, const float* bn_b,
+                       const float* bn_rm, const float* bn_rv, float eps, int act, float slope) {
+  Epilogue e = epi_dense(y, 0);
+  e.bias = bias;
+  if (bn_w) { e.bn_w = bn_w; e.bn_b = bn_b; e.bn_rm = bn_rm; e.bn_rv = bn_rv; e.bn_eps = eps; }
+  e.act = act;
+  e.slope = slope;
+  return e;
+}
+
+static bool fits32(int64_t v) { return v >= 0 && v < (1LL << 31); }
+
+// ---------------------------------------------------------------------------- softmax
+// In-place row softmax, one wave64 per row (max-subtracted, like torch.softmax).
+__global__ __launch_bounds__(256) void softmax_rows_kernel(float* x, int rows, int n) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float* p = x + (int64_t)row * n;
+  float mx = -INFINITY;
+  for (int j = lane; j < n; j += 64) mx = fmaxf(mx, p[j]);
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float s = 0.f;
+  for (int j = lane; j < n; j += 64) {
+    const float e = expf(p[j] - mx);
+    p[j] = e;
+    s += e;
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float inv = 1.f / s;
+  for (int j = lane; j < n; j += 64) p[j] *= inv;
+}
+
+// --------------------------------------------------------------------- time interpolation
+// F.interpolate(size=(T,1), mode='bilinear', align_corners=False): source index
+// max(0, scale*(dst+0.5)-0.5), scale = in/out computed in fp32 (ATen's
+// area_pixel_compute_source_index); zero-weight taps are skipped so never-computed
+// (pruned) encoder columns are never read.
+__global__ void interp_time_kernel(const float* x, int B, int C, int H, int W, float* y, int T) {
+  const int64_t total = (int64_t)B * C * T;
+  const float sh = (float)H / (float)T;
+  const float sw = (float)W / 1.0f;
+  float srcw = sw * 0.5f - 0.5f;
+  srcw = srcw < 0.f ? 0.f : srcw;
+  const int w0 = (int)srcw;
+  const int w1 = w0 + (w0 < W - 1 ? 1 : 0);
+  const float lw1 = srcw - (float)w0, lw0 = 1.f - lw1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T);
+    const int64_t bc = i / T;
+    float src = sh * ((float)t + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+    const int h0 = (int)src;
+    const int h1 = h0 + (h0 < H - 1 ? 1 : 0);
+    const float lh1 = src - (float)h0, lh0 = 1.f - lh1;
+    const float* p = x + bc * H * W;
+    auto row = [&](int h) {
+      float v = lw0 * p[h * W + w0];
+      if (lw1 != 0.f) v += lw1 * p[h * W + w1];
+      return v;
+    };
+    float v = lh0 * row(h0);
+    if (lh1 != 0.f) v += lh1 * row(h1);
+    y[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------- channel attention
+// One workgroup per batch element: avg/max pooling over T (one wave per channel), the
+// shared 2-layer MLP for both pooled vectors, sigmoid-sum, then the channel rescale.
+__global__ __launch_bounds__(256) void channel_attention_kernel(const float* x, int C, int T,
+                                                                const float* w1, const float* b1,
+                                                                int Cr, const float* w2,
+                                                                const float* b2, float* y,
+                                                                float* att_out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* pavg = sm;
+  float* pmax = pavg + C;
+  float* hid = pmax + C;  // [2][Cr]
+  float* att = hid + 2 * Cr;
+  const int b = blockIdx.x;
+  const float* xb = x + (int64_t)b * C * T;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int c = wv; c < C; c += 4) {
+    const float* p = xb + (int64_t)c * T;
+    float s = 0.f, mx = -INFINITY;
+    for (int t = lane; t < T; t += 64) {
+      const float v = p[t];
+      s += v;
+      mx = fmaxf(mx, v);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o);
+      mx = fmaxf(mx, __shfl_xor(mx, o));
+    }
+    if (lane == 0) {
+      pavg[c] = s / (float)T;
+      pmax[c] = mx;
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 2 * Cr; j += blockDim.x) {
+    const int r = j % Cr;
+    const float* in = j < Cr ? pavg : pmax;
+    const float* wr = w1 + (int64_t)r * C;
+    float a = b1[r];
+    for (int c = 0; c < C; ++c) a += wr[c] * in[c];
+    hid[j] = a > 0.f ? a : 0.f;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float* wr = w2 + (int64_t)c * Cr;
+    float a0 = b2[c], a1 = b2[c];
+    for (int r = 0; r < Cr; ++r) {
+      a0 += wr[r] * hid[r];
+      a1 += wr[r] * hid[Cr + r];
+    }
+    const float s = 1.f / (1.f + expf(-a0)) + 1.f / (1.f + expf(-a1));
+    att[c] = s;
+    if (att_out) att_out[(int64_t)b * C + c] = s;
+  }
+  __syncthreads();
+  float* yb = y + (int64_t)b * C * T;
+  for (int64_t i = threadIdx.x; i < (int64_t)C * T; i += blockDim.x) yb[i] = xb[i] * att[i / T];
+}
+
+// ------------------------------------------------------------------------------ LayerNorm
+// One wave per row, D <= 64*8.  Biased variance, eps inside the sqrt (torch.layer_norm).
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int R, int D,
+                                                        const float* w, const float* b, float eps,
+                                                        float* y, int T, int64_t ys_b,
+                                                        int64_t ys_d, int64_t ys_t, float* mean_out,
+                                                        float* rstd_out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const float* p = x + (int64_t)row * D;
+  float v[8];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int d = lane + 64 * q;
+    v[q] = d < D ? p[d] : 0.f;
+    s += v[q];
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int d = lane + 64 * q;
+    const float c = d < D ? v[q] - mean : 0.f;
+    ss += c * c;
+  }
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  const float rstd = 1.f / sqrtf(ss / (float)D + eps);
+  float* yr = y + (int64_t)(row / T) * ys_b + (int64_t)(row % T) * ys_t;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int d = lane + 64 * q;
+    if (d < D) yr[d * ys_d] = (v[q] - mean) * rstd * w[d] + b[d];
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+__global__ void mean_time_kernel(const float* x, int64_t xs_b, int64_t xs_c, int C, int T, int BC,
+                                 float* y) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= BC) return;
+  const float* p = x + (int64_t)(i / C) * xs_b + (int64_t)(i % C) * xs_c;
+  float s = 0.f;
+  for (int t = lane; t < T; t += 64) s += p[t];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) y[i] = s / (float)T;
+}
+
+__global__ void repeat_time_kernel(const float* x, int C, int T, int64_t total, float* y,
+                                   int64_t ys_b, int64_t ys_c) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T);
+    const int64_t bc = i / T;
+    y[(bc / C) * ys_b + (bc % C) * ys_c + t] = x[bc];
+  }
+}
+
+int softmax_rows(float* x, int rows, int n, hipStream_t st) {
+  if (rows == 0) return A2M_OK;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, st, x,
+                     rows, n);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+}  // namespace a2m
+
+using namespace a2m;
+
+extern "C" {
+
+int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t, int32_t B,
+                       int32_t Ci, int32_t Tin, const float* w, const float* bias, int32_t Co,
+                       int32_t ks, int32_t stride, int32_t pad, const float* bn_w,
+                       const float* bn_b, const float* bn_rm, const float* bn_rv, float bn_eps,
+                       int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
+                       int64_t ys_t, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && w && y, "conv1d: null pointer");
+  A2M_CHECK_ARG(B > 0 && Ci > 0 && Tin > 0 && Co > 0 && ks > 0 && stride > 0 && pad >= 0,
+                "conv1d: bad shape B=%d Ci=%d T=%d Co=%d k=%d s=%d p=%d", B, Ci, Tin, Co, ks,
+                stride, pad);
+  const int Tout = (Tin + 2 * pad - ks) / stride + 1;
+  A2M_CHECK_ARG(Tout > 0, "conv1d: empty output");
+  A2M_CHECK_ARG(fits32(xs_b) && fits32(xs_c) && fits32(xs_t) && fits32(ys_b) && fits32(ys_c) &&
+                    fits32(ys_t) && fits32((int64_t)B * xs_b) && fits32((int64_t)B * ys_b),
+                "conv1d: tensor too large for 32-bit offsets");
+  Gather A = dense_rk(w, Ci * ks);
+  Gather Bg{};
+  if (ks == 1 && pad == 0 && stride == 1 && xs_b == (int64_t)Tin * xs_t) {
+    // rows n = b*T + t are uniformly strided: plain [N][Ci] (k-major when xs_c == 1)
+    Bg = xs_c == 1 ? dense_rk(x, (int)xs_t) : dense_kr(x, (int)xs_c);
+    if (xs_c != 1) Bg.sr0 = (int)xs_t;
+  } else {
+    Bg.base = x; Bg.bstride = 0;
+    Bg.sr0 = (int)xs_b; Bg.R1 = 1; Bg.R2 = Tout; Bg.ar1 = 0; Bg.ar2 = stride;
+    Bg.sk0 = (int)xs_c; Bg.K1 = 1; Bg.K2 = ks; Bg.bk1 = 0; Bg.bk2 = 1;
+    Bg.ch = 0; Bg.cw = -pad; Bg.divh = Bg.divw = 1; Bg.Lh = 1; Bg.Lw = Tin;
+    Bg.sh = 0; Bg.sw = (int)xs_t;
+    Bg.kcontig = (ks == 1 && xs_c == 1) ? 1 : 0;
+  }
+  Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+  E.N1 = 1; E.N2 = Tout; E.so0 = (int)ys_b; E.so1 = 0; E.so2 = (int)ys_t; E.som = (int)ys_c;
+  return gemm(A, Bg, E, Co, B * Tout, Ci * ks, 1, ws, ws_bytes, as_stream(stream));
+}
+
+int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
+                        int32_t Tin, const float* w, const float* bias, int32_t Co, int32_t ks,
+                        int32_t stride, int32_t pad, int32_t out_pad, const float* bn_w,
+                        const float* bn_b, const float* bn_rm, const float* bn_rv, float bn_eps,
+                        int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
+                        void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && w && y, "convt1d: null pointer");
+  const int Tout = (Tin - 1) * stride - 2 * pad + ks + out_pad;
+  A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && Tout > 0 && stride > 0,
+                "convt1d: bad shape");
+  A2M_CHECK_ARG(fits32((int64_t)B * xs_b) && fits32((int64_t)B * ys_b), "convt1d: too large");
+  // A(m=co, k=(ci,kk)) = W[ci][co][kk]
+  Gather A{};
+  A.base = w; A.sr0 = ks; A.R1 = A.R2 = 1;
+  A.sk0 = Co * ks; A.K1 = 1; A.K2 = ks; A.bk2 = 1; A.sw = 1; A.Lw = ks; A.Lh = 1;
+  A.divh = A.divw = 1; A.kcontig = 1;
+  // B(n=(b,t), k=(ci,kk)) = x[b][ci][(t + pad - kk) / stride]
+  Gather Bg{};
+  Bg.base = x; Bg.sr0 = (int)xs_b; Bg.R1 = 1; Bg.R2 = Tout; Bg.ar2 = 1;
+  Bg.sk0 = (int)xs_c; Bg.K1 = 1; Bg.K2 = ks; Bg.bk2 = -1; Bg.cw = pad;
+  Bg.divh = 1; Bg.divw = stride; Bg.Lh = 1; Bg.Lw = Tin; Bg.sw = 1; Bg.kcontig = 0;
+  Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+  E.N1 = 1; E.N2 = Tout; E.so0 = (int)ys_b; E.so2 = 1; E.som = (int)ys_c;
+  return gemm(A, Bg, E, Co, B * Tout, Ci * ks, 1, ws, ws_bytes, as_stream(stream));
+}
+
+int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
+                       const float* w, const float* bias, int32_t Co, int32_t kh, int32_t kw,
+                       int32_t stride, int32_t pad_h, int32_t pad_w, const float* bn_w,
+                       const float* bn_b, const float* bn_rm, const float* bn_rv, float bn_eps,
+                       int32_t act, float slope, float* y, int32_t Hout, int32_t Wout,
+                       int32_t w_lo, int32_t w_hi, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && w && y, "conv2d: null pointer");
+  A2M_CHECK_ARG(Hout == (H + 2 * pad_h - kh) / stride + 1 && Wout == (W + 2 * pad_w - kw) / stride + 1,
+                "conv2d: output geometry mismatch");
+  A2M_CHECK_ARG(0 <= w_lo && w_lo < w_hi && w_hi <= Wout, "conv2d: bad column range [%d,%d)",
+                w_lo, w_hi);
+  A2M_CHECK_ARG(fits32((int64_t)B * Ci * H * W) && fits32((int64_t)B * Co * Hout * Wout),
+                "conv2d: too large");
+  const int Wn = w_hi - w_lo;
+  Gather A = dense_rk(w, Ci * kh * kw);
+  Gather Bg{};
+  Bg.base = x; Bg.sr0 = Ci * H * W; Bg.R1 = Hout; Bg.R2 = Wn; Bg.ar1 = stride; Bg.ar2 = stride;
+  Bg.sk0 = H * W; Bg.K1 = kh; Bg.K2 = kw; Bg.bk1 = 1; Bg.bk2 = 1;
+  Bg.ch = -pad_h; Bg.cw = w_lo * stride - pad_w; Bg.divh = Bg.divw = 1; Bg.Lh = H; Bg.Lw = W;
+  Bg.sh = W; Bg.sw = 1; Bg.kcontig = 0;
+  Epilogue E = epi_bn(y + w_lo, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+  E.N1 = Hout; E.N2 = Wn; E.so0 = Co * Hout * Wout; E.so1 = Wout; E.so2 = 1; E.som = Hout * Wout;
+  return gemm(A, Bg, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, as_stream(stream));
+}
+
+int a2m_mean_time_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
+                      int32_t T, float* y, void* stream) {
+  A2M_CHECK_ARG(x && y && B > 0 && C > 0 && T > 0, "mean_time: bad args");
+  const int BC = B * C;
+  hipLaunchKernelGGL(mean_time_kernel, dim3((unsigned)cdiv(BC, 4)), dim3(256), 0,
+                     as_stream(stream), x, xs_b, xs_c, C, T, BC, y);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_repeat_time_f32(const float* x, int32_t B, int32_t C, int32_t T, float* y, int64_t ys_b,
+                        int64_t ys_c, void* stream) {
+  A2M_CHECK_ARG(x && y && B > 0 && C > 0 && T > 0, "repeat_time: bad args");
+  const int64_t total = (int64_t)B * C * T;
+  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+  hipLaunchKernelGGL(repeat_time_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, C, T,
+                     total, y, ys_b, ys_c);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_interp_time_f32(const float* x, int32_t B, int32_t C, int32_t H, int32_t W, float* y,
+                        int32_t T, void* stream) {
+  A2M_CHECK_ARG(x && y && B > 0 && C > 0 && H > 0 && W > 0 && T > 0, "interp: bad args");
+  const int64_t total = (int64_t)B * C * T;
+  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
+  hipLaunchKernelGGL(interp_time_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, B, C,
+                     H, W, y, T);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+size_t a2m_self_attention_ws_bytes(int32_t B, int32_t C, int32_t T) {
+  const int Cq = C / 8;
+  size_t s = 0;
+  s = std::max(s, gemm_ws_bytes(Cq, B * T, C, 1));
+  s = std::max(s, gemm_ws_bytes(C, B * T, C, 1));
+  s = std::max(s, gemm_ws_bytes(T, T, Cq, B));
+  s = std::max(s, gemm_ws_bytes(C, T, T, B));
+  return s;
+}
+
+int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
+                               const float* wq, const float* bq, const float* wk, const float* bk,
+                               const float* wv, const float* bv, const float* gamma,
+                               const float* res, float* y, int64_t y_bs, float* qkv,
+                               float* attn, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && wq && wk && wv && gamma && y && qkv && attn, "self_attention: null pointer");
+  A2M_CHECK_ARG(B > 0 && C >= 8 && C % 8 == 0 && T > 0, "self_attention: bad shape C=%d T=%d", C, T);
+  A2M_CHECK_ARG(x_bs == y_bs, "self_attention: x and y must share a layout");
+  A2M_CHECK_ARG(fits32((int64_t)B * x_bs) && fits32((int64_t)B * (C + C / 4) * T) &&
+                    fits32((int64_t)B * T * T),
+                "self_attention: too large");
+  hipStream_t st = as_stream(stream);
+  const int Cq = C / 8, Cqkv = C / 4 + C;
+  const int64_t qs_b = (int64_t)Cqkv * T;
+  int rc;
+  // q, k, v: 1x1 convolutions into qkv[b][0:Cq | Cq:2Cq | 2Cq:2Cq+C][t]
+  const float* ws_w[3] = {wq, wk, wv};
+  const float* ws_b[3] = {bq, bk, bv};
+  const int rows[3] = {Cq, Cq, C};
+  const int offs[3] = {0, Cq, 2 * Cq};
+  for (int i = 0; i < 3; ++i) {
+    rc = a2m_conv1d_fwd_f32(x, x_bs, T, 1, B, C, T, ws_w[i], ws_b[i], rows[i], 1, 1, 0, nullptr,
+                            nullptr, nullptr, nullptr, 0.f, A2M_ACT_NONE, 0.f,
+                            qkv + (int64_t)offs[i] * T, qs_b, T, 1, ws, ws_bytes, stream);
+    if (rc) return rc;
+  }
+  // scores[b][i][j] = sum_c q[b][c][i] k[b][c][j]
+  Gather Aq = dense_kr(qkv, T, qs_b);
+  Gather Bk = dense_kr(qkv + (int64_t)Cq * T, T, qs_b);
+  Epilogue Es = epi_dense(attn, T, (int64_t)T * T);
+  rc = gemm(Aq, Bk, Es, T, T, Cq, B, ws, ws_bytes, st);
+  if (rc) return rc;
+  rc = softmax_rows(attn, B * T, T, st);
+  if (rc) return rc;
+  // y[b][c][i] = gamma * sum_j v[b][c][j] attn[b][i][j] + x[b][c][i] (+ res)
+  Gather Av = dense_rk(qkv + (int64_t)2 * Cq * T, T, qs_b);
+  Gather Ba = dense_rk(attn, T, (int64_t)T * T);
+  Epilogue Eo = epi_dense(y, T, y_bs);
+  Eo.gamma = gamma;
+  Eo.res1 = x;
+  Eo.res2 = res;
+  return gemm(Av, Ba, Eo, C, T, T, B, ws, ws_bytes, st);
+}
+
+int a2m_channel_attention_fwd_f32(const float* x, int32_t B, int32_t C, int32_t T,
+                                  const float* w1, const float* b1, int32_t Cr, const float* w2,
+                                  const float* b2, float* y, float* att_out, void* stream) {
+  A2M_CHECK_ARG(x && w1 && b1 && w2 && b2 && y && B > 0 && C > 0 && Cr > 0 && T > 0,
+                "channel_attention: bad args");
+  const size_t lds = sizeof(float) * (3 * (size_t)C + 2 * Cr);
+  A2M_CHECK_ARG(lds <= 64 * 1024, "channel_attention: C too large");
+  hipLaunchKernelGGL(channel_attention_kernel, dim3(B), dim3(256), lds, as_stream(stream), x, C,
+                     T, w1, b1, Cr, w2, b2, y, att_out);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_layernorm_fwd_f32(const float* x, int32_t R, int32_t D, const float* w, const float* b,
+                          float eps, float* y, int32_t T, int64_t ys_b, int64_t ys_d,
+                          int64_t ys_t, float* mean_out, float* rstd_out, void* stream) {
+  A2M_CHECK_ARG(x && w && b && y && R >= 0 && D > 0 && D <= 512 && T > 0, "layernorm: bad args");
+  if (R == 0) return A2M_OK;
+  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)cdiv(R, 4)), dim3(256), 0,
+                     as_stream(stream), x, R, D, w, b, eps, y, T, ys_b, ys_d, ys_t, mean_out,
+                     rstd_out);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+}  // extern "C"

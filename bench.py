@@ -1,0 +1,243 @@
+"""Benchmark: pose-frames/sec on batch-64 x 64-frame clips (BASELINE.json metric, configs[1]).
+
+One step = HIP log-mel front end over B synthetic 16 kHz waveforms (69,269 samples -> 64
+frames each) + SelfAttention_G forward (eval) -> [B, 64, 104] poses, fp32, inputs resident
+in HBM.  The step is captured once in a HIP graph and replayed.  N GPUs = N independent
+replicas (inference does not shard further: "replicas only", weak scaling), launched one
+process per GPU by torch.distributed.run; max-over-ranks time.
+
+Printed JSON adds `roofline` (the dominant kernel -- the largest UNet implicit-GEMM conv --
+timed with HIP events on its own stream, against the fp32 MFMA peak), `mel_roofline`
+(log-mel kernel vs HBM peak), `path_roofline` (the whole G forward's useful FLOPs) and
+`cpu_baseline` (the torch-CPU oracle port on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'audio-to-motion-generation_amd'))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md, chip-level parameters
+HBM_PEAK_GBS = 8000.0
+SR, WIN, HOP = 16000, 2048, 1067
+
+
+def synth_wave(B, n, seed, device):
+    g = torch.Generator(device='cpu').manual_seed(seed)
+    t = torch.arange(n, dtype=torch.float64) / SR
+    f0 = 90 + 160 * torch.rand(B, 1, generator=g, dtype=torch.float64)
+    env = 0.5 * (1 + torch.sin(2 * torch.pi * 4.0 * t))
+    v = sum(a * torch.sin(2 * torch.pi * f0 * (h + 1) * t) for h, a in enumerate((0.3, 0.15, 0.08)))
+    w = (v * env + 0.1 * torch.randn(B, n, generator=g, dtype=torch.float64)).clamp(-1, 1)
+    return w.float().to(device)
+
+
+def g_forward_flops(B, T, C=256):
+    """Useful FLOPs of one G forward: 2*MACs of every conv/linear/bmm,
+    encoder counted over live columns only."""
+    f = 0
+
+    def conv(co, ci, k, L):
+        return 2 * co * ci * k * L
+    # encoder, live columns (9..54, 5..26, 3..12, 4..11, 7)
+    f += conv(64, 1, 16, T // 2 * 46) + conv(128, 64, 16, T // 4 * 22) + conv(256, 128, 16, T // 8 * 10)
+    f += conv(512, 256, 9, T // 8 * 8) + conv(256, 512, 24, T // 8 * 1)
+
+    def attn(c, t):
+        return conv(c // 4 + c, c, 1, t) + 2 * t * t * (c // 8) + 2 * c * t * t
+    f += conv(2 * C, C, 3, T) + conv(2 * C, 2 * C, 4, T // 2) + conv(4 * C, 2 * C, 3, T // 2)
+    f += conv(4 * C, 4 * C, 4, T // 4) + conv(8 * C, 4 * C, 3, T // 4) + attn(8 * C, T // 4)
+    f += conv(4 * C, 8 * C, 3, T // 4) + attn(8 * C, T // 2)   # convT 2048->1024 (Tin=T/4, 3 taps)
+    f += conv(4 * C, 8 * C, 3, T // 2) + conv(2 * C, 4 * C, 3, T // 2) + conv(2 * C, 4 * C, 3, T)
+    f += conv(C, 2 * C, 1, T)
+    for J, post_ca in ((10, 0), (42, 1)):
+        f += 2 * (2 * conv(C, C, 3, T) + attn(C, T)) + 2 * conv(C, C, 3, T) + 2 * attn(C, T)
+        f += conv(J * 64, C, 1, T) * 2                              # proj_in + proj_out
+        f += 3 * (J * T * 2 * 64 * 256) + 2 * (J * T * 2 * 64 * 128)  # 3 GAT + 2 GraphConv
+    f += conv(104, C, 1, T)
+    return f * B
+
+
+def run_dominant_kernel(dev, iters=20):
+    """Time the largest single implicit-GEMM launch of the step (UNet upsample_layers[1]:
+    Conv1d 2048->1024, k3, T/2=32, B=64, BN + LeakyReLU epilogue) with HIP events."""
+    from a2m import functional as F
+    B, Ci, Co, T = 64, 2048, 1024, 32
+    x = torch.randn(B, Ci, T, device=dev)
+    w = torch.randn(Co, Ci, 3, device=dev) * 0.01
+    b = torch.zeros(Co, device=dev)
+    bn = (torch.ones(Co, device=dev), torch.zeros(Co, device=dev), torch.zeros(Co, device=dev),
+          torch.ones(Co, device=dev), 1e-5)
+    y = torch.empty(B, Co, T, device=dev)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            F.conv1d(x, w, b, 1, 1, bn=bn, act=F.ACT_LRELU, out=y)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(iters):
+            F.conv1d(x, w, b, 1, 1, bn=bn, act=F.ACT_LRELU, out=y)
+        e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2.0 * Co * Ci * 3 * B * T
+    return ms, flops
+
+
+def run_mel_kernel(dev, wave, iters=50):
+    from a2m.mel_features import log_mel_batch
+    out = log_mel_batch(wave)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(iters):
+            log_mel_batch(wave, out=out)
+        e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    nbytes = wave.numel() * 4 + out.numel() * 4       # algorithmic: wav in + mel out
+    return ms, nbytes
+
+
+def cpu_baseline(B=8, T=64, max_s=20.0):
+    """torch-CPU fp32 oracle port (numpy float64 mel + functional G) on a bounded sample."""
+    sys.path.insert(0, REPO)
+    import numpy as np
+    from oracle import mel as omel, model as omodel, synth, weights
+    from a2m.real_motion_model import SelfAttention_G
+    threads = torch.get_num_threads()
+    shapes = {k: tuple(v.shape) for k, v in SelfAttention_G(p=0.0).state_dict().items()}
+    sd = weights.make_state_dict(shapes, seed=7)
+    wav = synth.speech_like(B, synth.samples_for_frames(T), seed=1)
+
+    def step():
+        mel = np.stack([omel.log_mel(w, **omel.BUILD_CFG) for w in wav]).astype(np.float32)
+        with torch.no_grad():
+            omodel.generator(sd, torch.from_numpy(mel))
+    step()
+    times, t_all = [], time.perf_counter()
+    while len(times) < 5 and time.perf_counter() - t_all < max_s:
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {'value': round(B * T / med, 1), 'unit': 'pose-frames/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{B} clips x {T} frames (numpy fp64 log-mel + torch-CPU fp32 G forward), '
+                      f'median of {len(times)} runs, {threads} threads'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=64)
+    ap.add_argument('--frames', type=int, default=64)
+    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    from a2m.mel_features import log_mel_batch
+    from a2m.real_motion_model import SelfAttention_G
+
+    B, T = args.batch, args.frames
+    n = (T - 1) * HOP + WIN
+    torch.manual_seed(1234 + rank)
+    g = SelfAttention_G(time_steps=T, p=0.2)
+    for m in g.modules():
+        if hasattr(m, 'gamma'):
+            torch.nn.init.constant_(m.gamma, 0.3)
+    g = g.to(dev).eval()
+    wave = synth_wave(B, n, seed=rank, device=dev)
+
+    def step():
+        mel = log_mel_batch(wave)
+        out, _ = g(mel)
+        return out
+
+    with torch.no_grad():
+        step()
+        torch.cuda.synchronize()
+        graph = None
+        if not args.no_graph:
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream(dev).wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_out = step()
+        run = graph.replay if graph is not None else step
+        for _ in range(args.warmup):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = t.item()
+        out = static_out if graph is not None else step()
+        assert torch.isfinite(out).all()
+
+        ms_step = elapsed / args.steps * 1e3
+        value = world * B * T / (elapsed / args.steps)
+        k_ms, k_flops = run_dominant_kernel(dev)
+        mel_ms, mel_bytes = run_mel_kernel(dev, wave)
+    path_tf = g_forward_flops(B, T) / (ms_step * 1e-3) / 1e12
+    result = {
+        'metric': 'pose-frames/sec (whole node), PATS 64-frame clips batch 64, 1/2/4/8 MI355X',
+        'value': round(value, 1), 'unit': 'pose-frames/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'data': 'synthetic 16 kHz speech-like audio, random-init weights',
+        'config': {'workload': 'configs[1]: log-mel + SelfAttention_G forward (eval), batch-64 x 64-frame '
+                               'clips per GPU, replicas only', 'global_batch': B * world, 'seq_len': T,
+                   'parallelism': f'replicas{world}', 'hip_graph': graph is not None},
+        'roofline': {'bound': 'mfma', 'kernel': 'gemm_kernel (UNet up conv 2048->1024 k3, B64 T32)',
+                     'achieved': round(k_flops / (k_ms * 1e-3) / 1e12, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': round(k_flops / (k_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                     'traffic': None, 'ms_per_launch': round(k_ms, 4)},
+        'mel_roofline': {'bound': 'hbm', 'achieved': round(mel_bytes / (mel_ms * 1e-3) / 1e9, 1),
+                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(mel_bytes / (mel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         'ms_per_launch': round(mel_ms, 4)},
+        'path_roofline': {'bound': 'mfma', 'achieved': round(path_tf, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
+                          'unit': 'TFLOP/s', 'frac': round(path_tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                          'gflop_per_step': round(g_forward_flops(B, T) / 1e9, 1)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

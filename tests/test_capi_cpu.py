@@ -1,0 +1,129 @@
+"""CPU-side checks of the boundary: the C-ABI library loads and exports every symbol that
+include/a2m.h declares, host-side plan building matches the reference filterbank, and the
+drop-in modules expose the reference's state_dict keys.  No GPU compute here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, golden, golden_keys
+
+HEADER = os.path.join(REPO, 'include', 'a2m.h')
+
+
+def header_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r'^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\*?(a2m_[a-z0-9_]+)\(', src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from a2m import _native
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(_native.lib, s), s
+    assert sorted(_native.SIGNATURES) == syms
+    assert _native.lib.a2m_version() == 1
+
+
+def test_logmel_geometry_and_frames():
+    from a2m import _native as N
+    w, h, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    assert N.lib.a2m_logmel_geometry(16000, 0.128, 1 / 15, ctypes.byref(w), ctypes.byref(h), ctypes.byref(n)) == 0
+    assert (w.value, h.value, n.value) == (2048, 1067, 2048)
+    assert N.lib.a2m_logmel_num_frames(69269, 2048, 1067) == 64
+    assert N.lib.a2m_logmel_num_frames(2048, 2048, 1067) == 1
+    assert N.lib.a2m_logmel_num_frames(2047, 2048, 1067) == 0
+    assert N.lib.a2m_logmel_num_frames(513141, 2048, 1067) == 480
+
+
+def _plan_arrays(sr, win, hop, nm, lo, hi):
+    from a2m import _native as N
+    nb = N.lib.a2m_logmel_plan_bytes(sr, win, hop, nm, lo, hi)
+    buf = (ctypes.c_uint8 * nb)()
+    assert N.lib.a2m_logmel_plan_build(sr, win, hop, nm, lo, hi, buf, nb) == 0
+    raw = bytes(buf)
+    hdr = np.frombuffer(raw[:48], dtype=np.int32)
+    window, hopn, nfft, n_mels, n_bins, nnz = hdr[:6]
+    o_win, o_tw, o_start, o_len, o_woff, o_w = hdr[6:12]
+    start = np.frombuffer(raw[o_start:o_start + 4 * n_mels], dtype=np.int32)
+    ln = np.frombuffer(raw[o_len:o_len + 4 * n_mels], dtype=np.int32)
+    woff = np.frombuffer(raw[o_woff:o_woff + 4 * n_mels], dtype=np.int32)
+    wts = np.frombuffer(raw[o_w:o_w + 4 * nnz], dtype=np.float32)
+    dense = np.zeros((n_bins, n_mels), dtype=np.float32)
+    for m in range(n_mels):
+        dense[start[m]:start[m] + ln[m], m] = wts[woff[m]:woff[m] + ln[m]]
+    hann = np.frombuffer(raw[o_win:o_win + 4 * window], dtype=np.float32)
+    return dense, hann, nfft
+
+
+def test_logmel_plan_matches_reference_filterbank():
+    z = golden('mel.npz')
+    dense, hann, nfft = _plan_arrays(16000, 0.128, 1 / 15, 128, 125.0, 7500.0)
+    ref = z['mel_build_matrix']
+    assert np.array_equal(dense, ref.astype(np.float32))
+    assert (ref != 0).sum() == (dense != 0).sum()
+    n = np.arange(2048)
+    assert np.array_equal(hann, (0.5 - 0.5 * np.cos(2 * np.pi / 2048 * n)).astype(np.float32))
+
+
+def test_logmel_plan_errors_match_reference_valueerror_text():
+    from a2m import _native as N
+    z = golden('mel.npz')
+    cases = [(-1.0, 7500.0), (8000.0, 7000.0), (125.0, 9000.0)]
+    for (lo, hi), msg in zip(cases, z['mel_errors']):
+        buf = (ctypes.c_uint8 * 64)()
+        rc = N.lib.a2m_logmel_plan_build(16000, 0.004, 0.001, 8, lo, hi, buf, 64)
+        assert rc == N.A2M_EINVAL
+        assert N.last_error() == msg
+
+
+def test_state_dict_keys_match_reference():
+    from a2m.real_motion_model import SelfAttention_D, SelfAttention_G
+    keys = golden_keys()
+    g = SelfAttention_G(p=0.0)
+    d = SelfAttention_D(out_channels=64, p=0.0)
+    for mod, ref in ((g, keys['G']), (d, keys['D'])):
+        sd = mod.state_dict()
+        assert sorted(sd) == sorted(ref)
+        for k, shp in ref.items():
+            assert list(sd[k].shape) == shp, k
+
+
+def test_old_pyg_gat_keys_load():
+    from a2m.graph_layers import GATConv
+    m = GATConv(64, 64, heads=4, concat=False)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    w = sd.pop('lin.weight')
+    sd['lin_src.weight'] = w + 1
+    sd['lin_dst.weight'] = w + 1
+    m.load_state_dict(sd)
+    assert torch.equal(m.lin.weight, w + 1)
+
+
+def test_skeleton_tables_match_reference():
+    from a2m import skeleton as S
+    z = golden('losses.npz')
+    assert S.triples(10, 42) == [tuple(t) for t in z['hand_triples'].tolist()]
+    assert S.triples(0, 10) == [tuple(t) for t in z['body_triples'].tolist()]
+    assert S.edge_index(0, 10).shape == (2, 18)
+    assert S.edge_index(10, 42).shape == (2, 80)
+    ptr, idx = S.in_neighbour_csr(S.edge_index(10, 42), 42)
+    assert ptr[-1] == 80 and int(ptr[1] - ptr[0]) == 5   # each hand root has 5 children
+
+
+def test_encoder_live_columns():
+    from a2m.model_layers import AudioEncoder
+    enc = AudioEncoder()
+    assert enc.live_columns(128) == [(9, 55), (5, 27), (3, 13), (4, 12), (7, 8)]
+
+
+def test_ops_refuse_cpu_tensors():
+    from a2m import functional as F
+    x = torch.zeros(1, 4, 8)
+    w = torch.zeros(4, 4, 3)
+    with pytest.raises(RuntimeError, match='no CPU fallback'):
+        F.conv1d(x, w)

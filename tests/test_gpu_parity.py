@@ -1,0 +1,266 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle / reference goldens.
+
+Tolerance: north_star's 1e-4 relative fp32, measured as max|gpu - ref| / max|ref| per tensor.
+Per-op tests compare with a plain PyTorch fp32 CPU computation of the same op.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+DEV = 'cuda'
+
+
+def _rand(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).float()
+
+
+# ------------------------------------------------------------------------------ log-mel
+def test_logmel_build_config_vs_reference():
+    from a2m.mel_features import log_mel_batch
+    z = golden('mel.npz')
+    wav = torch.from_numpy(z['mel_build_wave']).to(DEV)
+    out = log_mel_batch(wav).cpu().numpy()
+    assert out.shape == (2, 64, 128)
+    assert rel_err(out, z['mel_build_out']) < TOL
+
+
+def test_logmel_reference_signature_and_edges():
+    from a2m.mel_features import log_mel_spectrogram
+    z = golden('mel.npz')
+    out = log_mel_spectrogram(z['mel_repr_wave'], audio_sample_rate=16000, log_offset=0.01,
+                              window_length_secs=0.025, hop_length_secs=0.010, num_mel_bins=64,
+                              lower_edge_hertz=125, upper_edge_hertz=7500)
+    assert out.shape == z['mel_repr_out'].shape and rel_err(out, z['mel_repr_out']) < TOL
+    # reference defaults: 8 kHz, 20 mels, log_offset 0 (fft 256 -> radix-2 + radix-4 stages)
+    out = log_mel_spectrogram(z['mel_default_wave'])
+    assert rel_err(out, z['mel_default_out']) < TOL
+    build = dict(audio_sample_rate=16000, log_offset=0.01, window_length_secs=0.128,
+                 hop_length_secs=1 / 15, num_mel_bins=128, lower_edge_hertz=125.0, upper_edge_hertz=7500.0)
+    assert rel_err(log_mel_spectrogram(z['mel_oneframe_wave'], **build), z['mel_oneframe_out']) < TOL
+    assert log_mel_spectrogram(z['mel_oneframe_wave'][:2047], **build).shape == (0, 128)
+    with pytest.raises(ValueError, match='Nyquist'):
+        log_mel_spectrogram(z['mel_oneframe_wave'], **{**build, 'upper_edge_hertz': 9000.0})
+
+
+# ------------------------------------------------------------------------------ per op
+@pytest.mark.parametrize('B,Ci,Co,T,k,s,p', [(3, 16, 24, 20, 3, 1, 1), (2, 32, 64, 17, 4, 2, 1),
+                                             (4, 40, 8, 9, 1, 1, 0), (2, 256, 512, 64, 3, 1, 1),
+                                             (2, 104, 64, 63, 4, 2, 1), (1, 7, 130, 5, 3, 1, 1)])
+def test_conv1d_bn_act(B, Ci, Co, T, k, s, p):
+    from a2m import functional as F
+    x, w, b = _rand(B, Ci, T, seed=1), _rand(Co, Ci, k, seed=2, scale=0.3), _rand(Co, seed=3)
+    bw, bb, rm, rv = _rand(Co, seed=4).abs() + 0.5, _rand(Co, seed=5), _rand(Co, seed=6), _rand(Co, seed=7).abs() + 0.5
+    ref = torch.nn.functional.conv1d(x, w, b, stride=s, padding=p)
+    ref = torch.nn.functional.batch_norm(ref, rm, rv, bw, bb, False, 0.0, 1e-5)
+    ref = torch.nn.functional.leaky_relu(ref, 0.2)
+    d = [t.to(DEV) for t in (x, w, b, bw, bb, rm, rv)]
+    out = F.conv1d(d[0], d[1], d[2], s, p, bn=(d[3], d[4], d[5], d[6], 1e-5), act=F.ACT_LRELU)
+    assert rel_err(out.cpu(), ref) < TOL
+
+
+def test_conv1d_strided_views_and_linear():
+    from a2m import functional as F
+    x = _rand(3, 50, 12, seed=8)
+    w, b = _rand(30, 20, 3, seed=9, scale=0.2), _rand(30, seed=10)
+    big = torch.zeros(3, 90, 12)
+    ref = torch.nn.functional.conv1d(x[:, 10:30], w, b, padding=1)
+    xd, bd = x.to(DEV), big.to(DEV)
+    F.conv1d(xd[:, 10:30], w.to(DEV), b.to(DEV), 1, 1, out=bd[:, 40:70])
+    assert rel_err(bd[:, 40:70].cpu(), ref) < TOL and bd[:, :40].abs().max() == 0
+    xl, wl, bl = _rand(37, 640, seed=11), _rand(256, 640, seed=12, scale=0.05), _rand(256, seed=13)
+    out = F.linear(xl.to(DEV), wl.to(DEV), bl.to(DEV))
+    assert rel_err(out.cpu(), torch.nn.functional.linear(xl, wl, bl)) < TOL
+    # [B, C, T] -> [B, T, O] (proj_in layout) and transposed input (D's first conv)
+    xt = _rand(2, 63, 104, seed=14)
+    w1 = _rand(64, 104, 4, seed=15, scale=0.1)
+    ref = torch.nn.functional.conv1d(xt.transpose(1, 2), w1, None, stride=2, padding=1)
+    out = F.conv1d(xt.to(DEV).transpose(1, 2), w1.to(DEV), None, 2, 1)
+    assert rel_err(out.cpu(), ref) < TOL
+
+
+@pytest.mark.parametrize('B,Ci,Co,T', [(2, 64, 32, 8), (3, 2048, 1024, 16), (2, 40, 24, 7)])
+def test_convt1d_bn_relu(B, Ci, Co, T):
+    from a2m import functional as F
+    x, w, b = _rand(B, Ci, T, seed=20), _rand(Ci, Co, 3, seed=21, scale=0.1), _rand(Co, seed=22)
+    bw, bb, rm, rv = _rand(Co, seed=23).abs() + .5, _rand(Co, seed=24), _rand(Co, seed=25), _rand(Co, seed=26).abs() + .5
+    ref = torch.nn.functional.conv_transpose1d(x, w, b, stride=2, padding=1, output_padding=1)
+    ref = torch.relu(torch.nn.functional.batch_norm(ref, rm, rv, bw, bb, False, 0.0, 1e-5))
+    d = [t.to(DEV) for t in (x, w, b, bw, bb, rm, rv)]
+    out = F.convt1d(d[0], d[1], d[2], bn=(d[3], d[4], d[5], d[6], 1e-5), act=F.ACT_RELU)
+    assert out.shape == ref.shape and rel_err(out.cpu(), ref) < TOL
+
+
+def test_conv2d_column_range():
+    from a2m import functional as F
+    x, w, b = _rand(2, 8, 16, 32, seed=30), _rand(12, 8, 4, 4, seed=31, scale=0.2), _rand(12, seed=32)
+    ref = torch.nn.functional.conv2d(x, w, b, stride=2, padding=1)
+    out = torch.full(ref.shape, float('nan'), device=DEV)
+    F.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), 2, (1, 1), cols=(3, 11), out=out)
+    assert rel_err(out[..., 3:11].cpu(), ref[..., 3:11]) < TOL
+    assert torch.isnan(out[..., :3]).all() and torch.isnan(out[..., 11:]).all()
+    w2 = _rand(6, 8, 3, 8, seed=33, scale=0.2)
+    ref2 = torch.nn.functional.conv2d(x, w2, None, stride=1, padding=(1, 3))
+    out2 = F.conv2d(x.to(DEV), w2.to(DEV), None, 1, (1, 3))
+    assert rel_err(out2.cpu(), ref2) < TOL
+
+
+def test_interp_time():
+    from a2m import functional as F
+    x = _rand(2, 5, 8, 15, seed=40)
+    ref = torch.nn.functional.interpolate(x, size=(64, 1), mode='bilinear').squeeze(-1)
+    assert rel_err(F.interp_time(x.to(DEV), 64).cpu(), ref) < TOL
+    x2 = _rand(1, 3, 60, 15, seed=41)
+    ref2 = torch.nn.functional.interpolate(x2, size=(480, 1), mode='bilinear').squeeze(-1)
+    assert rel_err(F.interp_time(x2.to(DEV), 480).cpu(), ref2) < TOL
+
+
+@pytest.mark.parametrize('B,C,T', [(2, 256, 64), (2, 2048, 16), (1, 64, 480), (3, 16, 5)])
+def test_self_attention(B, C, T):
+    from a2m import functional as F
+    from oracle import model as OM
+    x, res = _rand(B, C, T, seed=50), _rand(B, C, T, seed=51)
+    sd = {'a.query_conv.weight': _rand(C // 8, C, 1, seed=52, scale=C ** -0.5),
+          'a.query_conv.bias': _rand(C // 8, seed=53, scale=0.1),
+          'a.key_conv.weight': _rand(C // 8, C, 1, seed=54, scale=C ** -0.5),
+          'a.key_conv.bias': _rand(C // 8, seed=55, scale=0.1),
+          'a.value_conv.weight': _rand(C, C, 1, seed=56, scale=C ** -0.5),
+          'a.value_conv.bias': _rand(C, seed=57, scale=0.1), 'a.gamma': torch.tensor([0.37])}
+    ref = OM.self_attention(OM.Ctx(sd), 'a', x) + res
+    d = {k: v.to(DEV) for k, v in sd.items()}
+    out = F.self_attention(x.to(DEV), d['a.query_conv.weight'], d['a.query_conv.bias'],
+                           d['a.key_conv.weight'], d['a.key_conv.bias'], d['a.value_conv.weight'],
+                           d['a.value_conv.bias'], d['a.gamma'], res=res.to(DEV))
+    assert rel_err(out.cpu(), ref) < TOL
+
+
+def test_channel_attention_layernorm_mean_repeat():
+    from a2m import functional as F
+    from oracle import model as OM
+    x = _rand(3, 256, 64, seed=60)
+    sd = {'c.fc.0.weight': _rand(32, 256, seed=61, scale=0.06), 'c.fc.0.bias': _rand(32, seed=62, scale=0.1),
+          'c.fc.2.weight': _rand(256, 32, seed=63, scale=0.2), 'c.fc.2.bias': _rand(256, seed=64, scale=0.1)}
+    ref = OM.channel_attention(OM.Ctx(sd), 'c', x)
+    d = [sd[k].to(DEV) for k in ('c.fc.0.weight', 'c.fc.0.bias', 'c.fc.2.weight', 'c.fc.2.bias')]
+    assert rel_err(F.channel_attention(x.to(DEV), *d).cpu(), ref) < TOL
+    rows = _rand(3 * 64, 256, seed=65)
+    w, b = _rand(256, seed=66).abs() + .5, _rand(256, seed=67)
+    ref = torch.nn.functional.layer_norm(rows, (256,), w, b).view(3, 64, 256).permute(0, 2, 1)
+    out = F.layernorm_to_bct(rows.to(DEV), w.to(DEV), b.to(DEV), 64)
+    assert rel_err(out.cpu(), ref) < TOL
+    assert rel_err(F.mean_time(x.to(DEV)[:, 100:200]).cpu(), x[:, 100:200].mean(2)) < TOL
+    buf = torch.zeros(3, 20, 4, device=DEV)
+    F.repeat_time(x.to(DEV)[:, :10, 0].contiguous(), buf[:, 10:])
+    assert torch.equal(buf[:, 10:].cpu(), x[:, :10, :1].expand(3, 10, 4)) and buf[:, :10].abs().max() == 0
+
+
+@pytest.mark.parametrize('part,J,lo', [('body', 10, 0), ('hand', 42, 10)])
+def test_graph_layers_vs_oracle(part, J, lo):
+    from a2m import functional as F
+    from a2m import skeleton as S
+    from oracle import model as OM
+    Fr = 37
+    x = _rand(Fr * J, 64, seed=70)
+    ei = S.edge_index(lo, J)
+    edges = OM.expand_edges(ei, J, Fr)
+    ptr, idx = S.in_neighbour_csr(ei, J)
+    lw, asrc, adst, bias = _rand(256, 64, seed=71, scale=0.15), _rand(1, 4, 64, seed=72, scale=0.3), \
+        _rand(1, 4, 64, seed=73, scale=0.3), _rand(64, seed=74, scale=0.1)
+    lnw, lnb = _rand(64, seed=75).abs() + .5, _rand(64, seed=76, scale=0.1)
+    g = OM._gat_fn(x, edges, lw, asrc, adst, bias, 4)
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(g, (64,), lnw, lnb), 0.2) + x
+    dv = lambda t: t.to(DEV)
+    out = F.graph_layer(dv(x), J, 0, dv(ptr), dv(idx), dv(lw), None, dv(asrc), dv(adst), dv(bias), dv(lnw), dv(lnb))
+    assert rel_err(out.cpu(), ref) < TOL
+    bare = F.graph_layer(dv(x), J, 0, dv(ptr), dv(idx), dv(lw), None, dv(asrc), dv(adst), dv(bias),
+                         None, None, norm_res=False)
+    assert rel_err(bare.cpu(), g) < TOL
+    wr, br, wo = _rand(64, 64, seed=77, scale=0.12), _rand(64, seed=78, scale=0.1), _rand(64, 64, seed=79, scale=0.12)
+    sd = {'g.lin_rel.weight': wr, 'g.lin_rel.bias': br, 'g.lin_root.weight': wo}
+    gc = OM.graph_conv(OM.Ctx(sd), 'g', x, edges)
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(gc, (64,), lnw, lnb), 0.2) + x
+    out = F.graph_layer(dv(x), J, 1, dv(ptr), dv(idx), dv(wr), dv(wo), None, None, dv(br), dv(lnw), dv(lnb))
+    assert rel_err(out.cpu(), ref) < TOL
+
+
+def test_pose_losses_vs_reference():
+    from a2m import functional as F
+    z = golden('losses.npz')
+    out = F.pose_losses(torch.from_numpy(z['gen']).to(DEV), torch.from_numpy(z['real']).to(DEV)).cpu()
+    assert rel_err(out[0], z['bone']) < TOL and rel_err(out[1], z['angle']) < TOL
+    out2 = F.pose_losses(torch.from_numpy(z['gen']).to(DEV)).cpu()
+    assert rel_err(out2[1], z['angle']) < TOL
+
+
+# ------------------------------------------------------------------------------ full model
+def _g(g_state):
+    from a2m.real_motion_model import SelfAttention_G
+    m = SelfAttention_G(p=0.0)
+    m.load_state_dict(g_state, strict=False)
+    return m.to(DEV).eval()
+
+
+def test_generator_eval_vs_reference(g_state):
+    z = golden('g_eval_b2t64.npz')
+    m = _g(g_state)
+    with torch.no_grad():
+        out, losses = m(torch.from_numpy(z['audio']).to(DEV), real_pose=torch.from_numpy(z['real_pose']).to(DEV))
+        feats = m.audio_encoder(torch.from_numpy(z['audio']).to(DEV))
+        ref_feats = m.unet(feats)
+    assert rel_err(feats.cpu(), z['act/audio_encoder']) < TOL
+    assert rel_err(ref_feats.cpu(), z['act/unet']) < TOL
+    assert rel_err(out.cpu(), z['pose']) < TOL
+    assert rel_err(losses[0].cpu(), z['bone']) < TOL
+    assert rel_err(losses[1].cpu(), z['angle']) < TOL
+
+
+def test_generator_longform_vs_reference(g_state):
+    z = golden('g_eval_b1t480.npz')
+    m = _g(g_state)
+    with torch.no_grad():
+        out, losses = m(torch.from_numpy(z['audio']).to(DEV))
+    assert rel_err(out.cpu(), z['pose']) < TOL
+    assert len(losses) == 1 and rel_err(losses[0].cpu(), z['angle']) < TOL
+
+
+def test_mel_plus_generator_end_to_end(g_state):
+    """wave -> HIP log-mel -> HIP generator vs reference mel_features + reference G."""
+    from a2m.mel_features import log_mel_batch
+    zm, z = golden('mel.npz'), golden('g_eval_b2t64.npz')
+    m = _g(g_state)
+    with torch.no_grad():
+        mel = log_mel_batch(torch.from_numpy(zm['mel_build_wave']).to(DEV))
+        out, _ = m(mel, real_pose=torch.from_numpy(z['real_pose']).to(DEV))
+    assert rel_err(out.cpu(), z['pose']) < TOL
+
+
+def test_discriminator_eval_vs_reference(d_state):
+    from a2m.real_motion_model import SelfAttention_D
+    z = golden('g_eval_b2t64.npz')
+    d = SelfAttention_D(out_channels=64, p=0.0)
+    d.load_state_dict(d_state, strict=False)
+    d = d.to(DEV).eval()
+    with torch.no_grad():
+        out, _ = d(torch.diff(torch.from_numpy(z['real_pose']), dim=1).to(DEV))
+    assert rel_err(out.cpu(), z['d_real']) < TOL
+
+
+def test_full_size_batch_invariance(g_state):
+    """B=64 x T=64 (the bench workload): every clip's output equals the same clip run alone
+    (clips are independent in eval mode) and is finite."""
+    from a2m.mel_features import log_mel_batch
+    from oracle import synth
+    m = _g(g_state)
+    wav = torch.from_numpy(synth.speech_like(64, synth.samples_for_frames(64), seed=3)).to(DEV)
+    with torch.no_grad():
+        mel = log_mel_batch(wav)
+        out, losses = m(mel)
+        solo, _ = m(mel[17:18])
+        solo2, _ = m(mel[63:64])
+    assert torch.isfinite(out).all() and torch.isfinite(losses[0])
+    assert rel_err(out[17:18].cpu(), solo.cpu()) < TOL
+    assert rel_err(out[63:64].cpu(), solo2.cpu()) < TOL
