@@ -248,11 +248,11 @@ int a2m_logmel_plan_build(int32_t sample_rate, double window_secs, double hop_se
 int a2m_logmel_f32(const float* wave, int64_t n_clips, int64_t clip_stride, int64_t n_samples,
                    int32_t window, int32_t hop, int32_t fft_len, int32_t n_mels,
                    const void* dev_plan, float log_offset, float* out, void* stream) {
-  A2M_CHECK_ARG(wave && out && dev_plan, "logmel: null pointer");
   A2M_CHECK_ARG(fft_len >= 4 && (fft_len & (fft_len - 1)) == 0 && window <= fft_len && hop > 0,
                 "logmel: bad geometry window=%d hop=%d fft_len=%d", window, hop, fft_len);
   const int64_t nf = a2m_logmel_num_frames(n_samples, window, hop);
-  if (nf == 0 || n_clips == 0) return A2M_OK;
+  if (nf == 0 || n_clips == 0) return A2M_OK;  // empty output, like the reference's (0, n_mels)
+  A2M_CHECK_ARG(wave && out && dev_plan, "logmel: null pointer");
   A2M_CHECK_ARG(n_clips * nf < (1LL << 31), "logmel: too many frames");
   const size_t lds = sizeof(float) * (2 * (size_t)fft_len + fft_len / 2 + 1 + 3);
   A2M_CHECK_ARG(lds <= 160 * 1024, "logmel: fft_len %d too large for LDS", fft_len);
