@@ -226,10 +226,9 @@ def graph_layer(x, J, kind, nbr_ptr, nbr_idx, w0, w1, att_src, att_dst, bias, ln
     F = x.shape[0] // J
     if out is None:
         out = torch.empty_like(x)
-    N.check(N.lib.a2m_graph_layer_fwd_f32(_p(x), F, J, kind, int(norm_res), _p(nbr_ptr), _p(nbr_idx), _p(w0),
-                                          _p(w1), _p(att_src), _p(att_dst), _p(bias), _p(ln_w),
-                                          _p(ln_b), slope, _p(out), None, _p(pre_ln), None, 0,
-                                          _stream()))
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_graph_layer_fwd_f32(
+        _p(x), F, J, kind, int(norm_res), _p(nbr_ptr), _p(nbr_idx), _p(w0), _p(w1), _p(att_src),
+        _p(att_dst), _p(bias), _p(ln_w), _p(ln_b), slope, _p(out), None, _p(pre_ln), wp, wn, _stream()))
     return out
 
 

@@ -60,6 +60,9 @@ def in_neighbour_csr(ei, n):
     for i in range(n):
         idx += [s for s, d in zip(src, dst) if d == i]
         ptr.append(len(idx))
+        # the fused graph kernel keeps <= 8 in-neighbours (incl. GAT's self loop) per node
+        assert ptr[-1] - ptr[-2] <= 7, 'in-degree > 7 is not supported by the graph kernel'
+    assert n <= 128, 'graphs of more than 128 nodes are not supported by the graph kernel'
     return torch.tensor(ptr, dtype=torch.int32), torch.tensor(idx, dtype=torch.int32)
 
 

@@ -12,6 +12,8 @@
 // k+1 are issued into registers before the MFMAs of tile k; LDS is double-buffered so one
 // barrier per K-step suffices.  Split-K writes fp32 partial slabs to a workspace that a
 // second kernel reduces in a fixed order (bitwise reproducible) and runs the epilogue on.
+#include <cstdlib>
+
 #include "a2m_internal.h"
 
 namespace a2m {
@@ -325,14 +327,29 @@ struct Plan {
   int bm, splits, kchunk;
 };
 
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+// Tile / split-K choice: fill the 256 CUs with >= ~2 workgroups each while keeping every
+// K-slice >= 256 deep.  A2M_GEMM_TILE=64|128 and A2M_GEMM_SPLIT=n override (experiments).
 static Plan plan_for(int M, int N, int K, int batch) {
-  Plan p;
+  static const int force_tile = env_int("A2M_GEMM_TILE", 0);
+  static const int force_split = env_int("A2M_GEMM_SPLIT", 0);
+  auto splits_for = [&](int64_t tiles) {
+    int s = 1;
+    while (s < 16 && tiles * s < 512 && K / (s * 2) >= 256) s *= 2;
+    return s;
+  };
   const int64_t t128 = cdiv(M, 128) * cdiv(N, 128) * (int64_t)batch;
-  p.bm = (M > 64 && N > 64 && t128 >= 160) ? 128 : 64;
-  const int64_t tiles = p.bm == 128 ? t128 : cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
-  int splits = 1;
-  const int64_t target = 512;
-  while (tiles * splits * 2 <= target && K / (splits * 2) >= 256) splits *= 2;
+  const int64_t t64 = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
+  const int s128 = splits_for(t128), s64 = splits_for(t64);
+  Plan p;
+  p.bm = (M >= 128 && N >= 128 && t128 * s128 >= 256) ? 128 : 64;
+  if (force_tile == 64 || force_tile == 128) p.bm = force_tile;
+  int splits = p.bm == 128 ? s128 : s64;
+  if (force_split > 0) splits = force_split;
   p.kchunk = (int)(cdiv(cdiv(K, splits), BK) * BK);
   p.splits = (int)cdiv(K, p.kchunk);
   return p;

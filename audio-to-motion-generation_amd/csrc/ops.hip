@@ -199,6 +199,53 @@ __global__ void repeat_time_kernel(const float* x, int C, int T, int64_t total, 
   }
 }
 
+// ConvTranspose1d weight [Ci][Co][ks] -> per output phase r: P_r[co][tap*Ci + ci] (see
+// a2m_convt1d_fwd_f32).  Phase of tap kk: r = (kk - pad) mod s; phases stored in order.
+__device__ __forceinline__ int phase_taps(int r, int ks, int s, int pad, int* kk0) {
+  int n = 0;
+  *kk0 = -1;
+  for (int kk = 0; kk < ks; ++kk)
+    if ((((r + pad - kk) % s) + s) % s == 0) { if (*kk0 < 0) *kk0 = kk; ++n; }
+  return n;
+}
+
+__global__ void convt_pack_kernel(const float* w, int Ci, int Co, int ks, int s, int pad, float* out) {
+  const int64_t total = (int64_t)Ci * Co * ks;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % ks);
+    const int64_t t = i / ks;
+    const int co = (int)(t % Co), ci = (int)(t / Co);
+    const int r = (((kk - pad) % s) + s) % s;
+    int64_t off = 0;
+    int kk0;
+    for (int rr = 0; rr < r; ++rr) off += (int64_t)Co * Ci * phase_taps(rr, ks, s, pad, &kk0);
+    const int nt = phase_taps(r, ks, s, pad, &kk0);
+    const int tap = (kk - kk0) / s;
+    out[off + ((int64_t)co * nt + tap) * Ci + ci] = w[i];
+  }
+}
+
+// [wq; wk; wv] -> wcat [C/4 + C][C], biases -> bcat (zeros where a bias pointer is NULL)
+__global__ void stack_qkv_kernel(const float* wq, const float* bq, const float* wk, const float* bk,
+                                 const float* wv, const float* bv, int C, float* wcat, float* bcat) {
+  const int Cq = C / 8;
+  const int64_t total = (int64_t)(2 * Cq + C) * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / C);
+    const int64_t col = i - (int64_t)row * C;
+    const float* src = row < Cq ? wq + (int64_t)row * C : row < 2 * Cq ? wk + (int64_t)(row - Cq) * C
+                                                                          : wv + (int64_t)(row - 2 * Cq) * C;
+    wcat[i] = src[col];
+    if (col == 0) {
+      const float* b = row < Cq ? bq : row < 2 * Cq ? bk : bv;
+      const int r = row < Cq ? row : row < 2 * Cq ? row - Cq : row - 2 * Cq;
+      bcat[row] = b ? b[r] : 0.f;
+    }
+  }
+}
+
 int softmax_rows(float* x, int rows, int n, hipStream_t st) {
   if (rows == 0) return A2M_OK;
   hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, st, x,
@@ -255,22 +302,56 @@ int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, i
                         void* ws, size_t ws_bytes, void* stream) {
   A2M_CHECK_ARG(x && w && y, "convt1d: null pointer");
   const int Tout = (Tin - 1) * stride - 2 * pad + ks + out_pad;
-  A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && Tout > 0 && stride > 0,
+  A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && Tout > 0 && stride > 0 && pad >= 0,
                 "convt1d: bad shape");
-  A2M_CHECK_ARG(fits32((int64_t)B * xs_b) && fits32((int64_t)B * ys_b), "convt1d: too large");
-  // A(m=co, k=(ci,kk)) = W[ci][co][kk]
-  Gather A{};
-  A.base = w; A.sr0 = ks; A.R1 = A.R2 = 1;
-  A.sk0 = Co * ks; A.K1 = 1; A.K2 = ks; A.bk2 = 1; A.sw = 1; A.Lw = ks; A.Lh = 1;
-  A.divh = A.divw = 1; A.kcontig = 1;
-  // B(n=(b,t), k=(ci,kk)) = x[b][ci][(t + pad - kk) / stride]
-  Gather Bg{};
-  Bg.base = x; Bg.sr0 = (int)xs_b; Bg.R1 = 1; Bg.R2 = Tout; Bg.ar2 = 1;
-  Bg.sk0 = (int)xs_c; Bg.K1 = 1; Bg.K2 = ks; Bg.bk2 = -1; Bg.cw = pad;
-  Bg.divh = 1; Bg.divw = stride; Bg.Lh = 1; Bg.Lw = Tin; Bg.sw = 1; Bg.kcontig = 0;
-  Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
-  E.N1 = 1; E.N2 = Tout; E.so0 = (int)ys_b; E.so2 = 1; E.som = (int)ys_c;
-  return gemm(A, Bg, E, Co, B * Tout, Ci * ks, 1, ws, ws_bytes, as_stream(stream));
+  A2M_CHECK_ARG(fits32((int64_t)B * xs_b) && fits32((int64_t)B * ys_b) &&
+                    fits32((int64_t)Ci * Co * ks),
+                "convt1d: too large");
+  // Output-phase decomposition: out[s*u + r] only sees the taps kk with
+  // (r + pad - kk) % s == 0, at input u + (r + pad - kk)/s.  Each phase is a dense GEMM over
+  // K = taps_r * Ci (no zero-inserted work); weights are packed per phase as
+  // P_r[co][tap*Ci + ci] = W[ci][co][kk_tap] into the head of the workspace.
+  const size_t pack_bytes = ((size_t)Ci * Co * ks * sizeof(float) + 255) & ~size_t(255);
+  if (!ws || ws_bytes < pack_bytes) {
+    set_error("convt1d: workspace too small (%zu < %zu bytes)", ws_bytes, pack_bytes);
+    return A2M_EWS;
+  }
+  float* packed = static_cast<float*>(ws);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(convt_pack_kernel, dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Ci * Co * ks, 256), 8192)),
+                     dim3(256), 0, st, w, Ci, Co, ks, stride, pad, packed);
+  A2M_LAUNCH_CHECK();
+  size_t off = 0;
+  for (int r = 0; r < stride; ++r) {
+    int kk0 = -1, ntap = 0;
+    for (int kk = 0; kk < ks; ++kk)
+      if ((((r + pad - kk) % stride) + stride) % stride == 0) { if (kk0 < 0) kk0 = kk; ++ntap; }
+    const int nu = (Tout - r + stride - 1) / stride;
+    if (nu <= 0) continue;
+    float* yr = y + r;
+    if (ntap == 0) {  // this phase only gets the bias / BN / act of zero
+      Gather Az = dense_rk(packed, 1);
+      Gather Bz = dense_rk(x, 1);
+      Epilogue E = epi_bn(yr, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+      E.N1 = 1; E.N2 = nu; E.so0 = (int)ys_b; E.so2 = stride; E.som = (int)ys_c;
+      int rc = gemm(Az, Bz, E, Co, B * nu, 0, 1, nullptr, 0, st);
+      if (rc) return rc;
+      continue;
+    }
+    const int off0 = (r + pad - kk0) / stride;  // exact; later taps shift the input by -1 each
+    Gather A = dense_rk(packed + off, ntap * Ci);
+    Gather Bg{};
+    Bg.base = x; Bg.sr0 = (int)xs_b; Bg.R1 = nu; Bg.R2 = 1; Bg.ar1 = 1; Bg.ar2 = 0;
+    Bg.K1 = ntap; Bg.K2 = Ci; Bg.sk0 = 0; Bg.bk1 = -1; Bg.bk2 = 1; Bg.ch = off0; Bg.cw = 0;
+    Bg.divh = Bg.divw = 1; Bg.Lh = Tin; Bg.Lw = Ci; Bg.sh = 1; Bg.sw = (int)xs_c; Bg.kcontig = 0;
+    Epilogue E = epi_bn(yr, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+    E.N1 = 1; E.N2 = nu; E.so0 = (int)ys_b; E.so2 = stride; E.som = (int)ys_c;
+    int rc = gemm(A, Bg, E, Co, B * nu, ntap * Ci, 1, static_cast<char*>(ws) + pack_bytes,
+                  ws_bytes - pack_bytes, st);
+    if (rc) return rc;
+    off += (size_t)Co * ntap * Ci;
+  }
+  return A2M_OK;
 }
 
 int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
@@ -355,17 +436,24 @@ int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t 
   const int Cq = C / 8, Cqkv = C / 4 + C;
   const int64_t qs_b = (int64_t)Cqkv * T;
   int rc;
-  // q, k, v: 1x1 convolutions into qkv[b][0:Cq | Cq:2Cq | 2Cq:2Cq+C][t]
-  const float* ws_w[3] = {wq, wk, wv};
-  const float* ws_b[3] = {bq, bk, bv};
-  const int rows[3] = {Cq, Cq, C};
-  const int offs[3] = {0, Cq, 2 * Cq};
-  for (int i = 0; i < 3; ++i) {
-    rc = a2m_conv1d_fwd_f32(x, x_bs, T, 1, B, C, T, ws_w[i], ws_b[i], rows[i], 1, 1, 0, nullptr,
-                            nullptr, nullptr, nullptr, 0.f, A2M_ACT_NONE, 0.f,
-                            qkv + (int64_t)offs[i] * T, qs_b, T, 1, ws, ws_bytes, stream);
-    if (rc) return rc;
+  // q, k, v as ONE 1x1 convolution with the three weights stacked in the workspace head:
+  // qkv[b][0:Cq | Cq:2Cq | 2Cq:2Cq+C][t]
+  const size_t wcat_bytes = (((size_t)Cqkv * C + Cqkv) * sizeof(float) + 255) & ~size_t(255);
+  if (!ws || ws_bytes < wcat_bytes) {
+    set_error("self_attention: workspace too small (%zu < %zu bytes)", ws_bytes, wcat_bytes);
+    return A2M_EWS;
   }
+  float* wcat = static_cast<float*>(ws);
+  float* bcat = wcat + (size_t)Cqkv * C;
+  hipLaunchKernelGGL(stack_qkv_kernel, dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Cqkv * C, 256), 8192)),
+                     dim3(256), 0, st, wq, bq, wk, bk, wv, bv, C, wcat, bcat);
+  A2M_LAUNCH_CHECK();
+  ws = static_cast<char*>(ws) + wcat_bytes;
+  ws_bytes -= wcat_bytes;
+  rc = a2m_conv1d_fwd_f32(x, x_bs, T, 1, B, C, T, wcat, bcat, Cqkv, 1, 1, 0, nullptr, nullptr,
+                          nullptr, nullptr, 0.f, A2M_ACT_NONE, 0.f, qkv, qs_b, T, 1, ws, ws_bytes,
+                          stream);
+  if (rc) return rc;
   // scores[b][i][j] = sum_c q[b][c][i] k[b][c][j]
   Gather Aq = dense_kr(qkv, T, qs_b);
   Gather Bk = dense_kr(qkv + (int64_t)Cq * T, T, qs_b);
