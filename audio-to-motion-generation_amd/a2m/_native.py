@@ -16,6 +16,7 @@ I64 = ctypes.c_int64
 F32 = ctypes.c_float
 F64 = ctypes.c_double
 SZ = ctypes.c_size_t
+U64 = ctypes.c_uint64
 
 # name -> (restype, argtypes); mirrors include/a2m.h
 SIGNATURES = {
@@ -33,8 +34,8 @@ SIGNATURES = {
                                            P, P, P, P, F32, I32, F32, P, I64, I64, P, SZ, P]),
     'a2m_conv2d_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, I32,
                                           P, P, P, P, F32, I32, F32, P, I32, I32, I32, I32, P, SZ, P]),
-    'a2m_mean_time_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P]),
-    'a2m_repeat_time_f32': (ctypes.c_int, [P, I32, I32, I32, P, I64, I64, P]),
+    'a2m_mean_time_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, F32, P, P]),
+    'a2m_repeat_time_f32': (ctypes.c_int, [P, I32, I32, I32, F32, P, I64, I64, P]),
     'a2m_interp_time_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, I32, P]),
     'a2m_self_attention_fwd_f32': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, P, P, P, P, P,
                                                   I64, P, P, P, SZ, P]),
@@ -44,6 +45,34 @@ SIGNATURES = {
     'a2m_graph_layer_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32, P, P,
                                                P, P, SZ, P]),
     'a2m_pose_losses_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, P, P, SZ, P]),
+    # ---- training step
+    'a2m_bn_train_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, P, P, F32, F32, F32, I32,
+                                            U64, I32, F32, P, I64, I64, P, P, P, SZ, P]),
+    'a2m_bn_train_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, I32, P, P, P, P, F32, I32,
+                                            U64, I32, F32, P, P, P, P, P, SZ, P]),
+    'a2m_dropout_f32': (ctypes.c_int, [P, I64, F32, U64, P, P]),
+    'a2m_sum_bt_f32': (ctypes.c_int, [P, I64, I64, I64, I32, I32, I32, P, I32, P]),
+    'a2m_layernorm_bwd_f32': (ctypes.c_int, [P, I64, I64, I64, I32, P, I32, I32, P, P, P, P, P, P, P, SZ, P]),
+    'a2m_conv2d_dgrad_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, I32,
+                                            I32, P, I64, I64, I64, I64, I32, P, SZ, P]),
+    'a2m_conv2d_wgrad_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, I64, I64, I64, I64, I32, I32, I32, I32,
+                                            I32, I32, I32, I32, I32, P, I32, P, SZ, P]),
+    'a2m_self_attention_bwd_ws_bytes': (SZ, [I32, I32, I32]),
+    'a2m_self_attention_bwd_f32': (ctypes.c_int, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P, P, P, P, P, P,
+                                                  P, P, P, P, P, P, SZ, P]),
+    'a2m_channel_attention_bwd_f32': (ctypes.c_int, [P, P, I32, I32, I32, P, P, I32, P, P, P, P, P, P, P, P,
+                                                     SZ, P]),
+    'a2m_graph_layer_bwd_f32': (ctypes.c_int, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32, P, P,
+                                               P, P, P, P, P, P, P, SZ, P]),
+    'a2m_interp_time_bwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, I32, P]),
+    'a2m_pose_losses_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, P, P, P, SZ, P]),
+    'a2m_motion_losses_f32': (ctypes.c_int, [P, P, I32, I32, I32, P, P, P, P, SZ, P]),
+    'a2m_mse_loss_f32': (ctypes.c_int, [P, P, I64, P, P, P, P, SZ, P]),
+    'a2m_diff_time_f32': (ctypes.c_int, [P, I32, I32, I32, P, P]),
+    'a2m_diff_time_bwd_f32': (ctypes.c_int, [P, I32, I32, I32, P, I32, P]),
+    'a2m_adam_f32': (ctypes.c_int, [P, P, P, P, I64, F32, F32, F32, F32, F32, I32, P]),
+    'a2m_gemm_f32': (ctypes.c_int, [I32, I32, I32, I32, I32, I32, P, I64, I64, I64, I64, P, I64, I64, I64,
+                                    I64, I64, P, I64, I64, I64, I64, P, F32, I32, P, SZ, P]),
 }
 
 A2M_EINVAL, A2M_EHIP, A2M_EWS = -1, -2, -3

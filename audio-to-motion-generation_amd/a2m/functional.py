@@ -148,22 +148,24 @@ def interp_time(x, T, out=None):
     return out
 
 
-def mean_time(x, out=None):
+def mean_time(x, out=None, scale=1.0):
+    """out[b, c] = scale * mean_t x[b, c, t]."""
     _check_dev(x, out)
     B, C, T = x.shape
     assert x.stride(2) == 1
     if out is None:
         out = torch.empty(B, C, device=x.device)
-    N.check(N.lib.a2m_mean_time_f32(_p(x), x.stride(0), x.stride(1), B, C, T, _p(out), _stream()))
+    N.check(N.lib.a2m_mean_time_f32(_p(x), x.stride(0), x.stride(1), B, C, T, scale, _p(out), _stream()))
     return out
 
 
-def repeat_time(x, out):
-    """out[b, c, t] = x[b, c] for a [B, C, T] (t-contiguous) view `out`."""
+def repeat_time(x, out, scale=1.0):
+    """out[b, c, t] = scale * x[b, c] for a [B, C, T] (t-contiguous) view `out`."""
     _check_dev(x, out)
     B, C, T = out.shape
     assert x.is_contiguous() and tuple(x.shape) == (B, C) and out.stride(2) == 1
-    N.check(N.lib.a2m_repeat_time_f32(_p(x), B, C, T, _p(out), out.stride(0), out.stride(1), _stream()))
+    N.check(N.lib.a2m_repeat_time_f32(_p(x), B, C, T, scale, _p(out), out.stride(0), out.stride(1),
+                                      _stream()))
     return out
 
 
@@ -288,3 +290,269 @@ def log_mel(wave, plan, log_offset, out=None):
     N.check(N.lib.a2m_logmel_f32(_p(wave), C, wave.stride(0), S, plan.window, plan.hop, plan.fft_len,
                                  plan.n_mels, _p(plan.dev), float(log_offset), _p(out), _stream()))
     return out
+
+
+# =============================================================================== training
+DROP_NONE, DROP_BEFORE, DROP_BEFORE_CH, DROP_AFTER = 0, 1, 2, 3
+
+
+def _bcl(t):
+    """(B, C, L, stride_b, stride_c) of a [B, C, ...] tensor whose trailing dims are contiguous."""
+    B, C = t.shape[0], t.shape[1]
+    L = 1
+    for s in t.shape[2:]:
+        L *= s
+    inner = 1
+    for d in range(t.dim() - 1, 1, -1):
+        assert t.stride(d) == inner, 'trailing dims must be contiguous'
+        inner *= t.shape[d]
+    return B, C, L, t.stride(0), t.stride(1)
+
+
+def bn_train(x, gamma, beta, rmean, rvar, momentum, eps, p, mode, seed, act, slope=0.2, out=None):
+    """Training-mode BatchNorm fused with dropout and activation; updates rmean / rvar."""
+    _check_dev(x, gamma, beta, rmean, rvar, out)
+    B, C, L, xsb, xsc = _bcl(x)
+    if out is None:
+        out = torch.empty(x.shape, device=x.device)
+    _, _, _, ysb, ysc = _bcl(out)
+    mean = torch.empty(C, device=x.device)
+    rstd = torch.empty(C, device=x.device)
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_train_fwd_f32(
+        _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(rmean), _p(rvar), momentum, eps, p, mode,
+        seed, act, slope, _p(out), ysb, ysc, _p(mean), _p(rstd), wp, wn, _stream()))
+    return out, mean, rstd
+
+
+def bn_train_bwd(dy, x, gamma, beta, mean, rstd, p, mode, seed, act, slope=0.2, want_bias=True):
+    _check_dev(dy, x)
+    B, C, L, xsb, xsc = _bcl(x)
+    _, _, _, dsb, dsc = _bcl(dy)
+    dx = torch.empty(x.shape, device=x.device)
+    dg = torch.empty(C, device=x.device) if gamma is not None else None
+    db = torch.empty(C, device=x.device) if beta is not None else None
+    dbias = torch.empty(C, device=x.device) if want_bias else None
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_train_bwd_f32(
+        _p(dy), dsb, dsc, _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(mean), _p(rstd), p, mode,
+        seed, act, slope, _p(dx), _p(dg), _p(db), _p(dbias), wp, wn, _stream()))
+    return dx, dg, db, dbias
+
+
+def _as4d(t):
+    return t.unsqueeze(2) if t.dim() == 3 else t
+
+
+def conv_dgrad(dy, w, x_shape, stride, pad, dx=None, accumulate=False):
+    """dX of conv{1,2}d(x, w, stride, pad); dy contiguous [B, Co, (Ho,) Wo]."""
+    _check_dev(dy, w, dx)
+    dy = dy.contiguous()
+    d4 = _as4d(dy)
+    w4 = w.unsqueeze(2) if w.dim() == 3 else w
+    B, Co, Ho, Wo = d4.shape
+    _, Ci, kh, kw = w4.shape
+    if len(x_shape) == 3:
+        H, W, sh, sw, ph, pw = 1, x_shape[2], 1, stride, 0, pad
+    else:
+        H, W = x_shape[2], x_shape[3]
+        sh = sw = stride
+        ph, pw = pad
+    if dx is None:
+        dx = torch.empty(x_shape, device=dy.device)
+    x4 = _as4d(dx)
+    _with_ws(dy.device, lambda wp, wn: N.lib.a2m_conv2d_dgrad_f32(
+        _p(dy), B, Co, Ho, Wo, _p(w), Ci, H, W, kh, kw, sh, sw, ph, pw, _p(dx), x4.stride(0),
+        x4.stride(1), x4.stride(2), x4.stride(3), int(accumulate), wp, wn, _stream()))
+    return dx
+
+
+def conv_wgrad(dy, x, w_shape, stride, pad, dw=None, accumulate=False):
+    """dW of conv{1,2}d(x, w, stride, pad); dy contiguous."""
+    _check_dev(dy, x, dw)
+    dy = dy.contiguous()
+    d4, x4 = _as4d(dy), _as4d(x)
+    B, Co, Ho, Wo = d4.shape
+    _, Ci, H, W = x4.shape
+    if len(w_shape) == 3:
+        kh, kw, sh, sw, ph, pw = 1, w_shape[2], 1, stride, 0, pad
+    else:
+        kh, kw = w_shape[2], w_shape[3]
+        sh = sw = stride
+        ph, pw = pad
+    if dw is None:
+        dw = torch.empty(w_shape, device=dy.device)
+    _with_ws(dy.device, lambda wp, wn: N.lib.a2m_conv2d_wgrad_f32(
+        _p(dy), B, Co, Ho, Wo, _p(x), x4.stride(0), x4.stride(1), x4.stride(2), x4.stride(3), Ci, H, W,
+        kh, kw, sh, sw, ph, pw, _p(dw), int(accumulate), wp, wn, _stream()))
+    return dw
+
+
+def gemm(M, N, K, A, a_m, a_k, B, b_n, b_k, C, c_m, c_n, N1=1, K1=1, batch=1, a_bs=0, b_bs=0, c_bs=0,
+         bias=None, accumulate=False):
+    """C[m][n] (+)= sum_k A(m,k) B(n,k) (+bias[m]).  a_k/b_k/b_n/c_n are (outer, inner) stride
+    pairs when K1 / N1 > 1 (k = k0*K1 + k1, n = n0*N1 + n1), plain ints otherwise."""
+    _check_dev(A, B, C, bias)
+    ak0, ak1 = a_k if isinstance(a_k, tuple) else (a_k, 0)
+    bk0, bk1 = b_k if isinstance(b_k, tuple) else (b_k, 0)
+    bn0, bn1 = b_n if isinstance(b_n, tuple) else (b_n, 0)
+    cn0, cn1 = c_n if isinstance(c_n, tuple) else (c_n, 0)
+    _with_ws(C.device, lambda wp, wn: N.lib.a2m_gemm_f32(
+        M, N, N1, K, K1, batch, _p(A), a_bs, a_m, ak0, ak1, _p(B), b_bs, bn0, bn1, bk0, bk1, _p(C), c_bs,
+        c_m, cn0, cn1, _p(bias), 1.0, int(accumulate), wp, wn, _stream()))
+    return C
+
+
+def sum_bt(x, out=None, accumulate=False):
+    """out[c] = sum over (b, t) of x [B, C, T] (t stride arbitrary)."""
+    _check_dev(x, out)
+    B, C, T = x.shape
+    if out is None:
+        out = torch.empty(C, device=x.device)
+    N.check(N.lib.a2m_sum_bt_f32(_p(x), x.stride(0), x.stride(1), x.stride(2), B, C, T, _p(out),
+                                 int(accumulate), _stream()))
+    return out
+
+
+def dropout(x, p, seed, out=None):
+    _check_dev(x, out)
+    assert x.is_contiguous()
+    if out is None:
+        out = torch.empty_like(x)
+    N.check(N.lib.a2m_dropout_f32(_p(x), x.numel(), p, seed, _p(out), _stream()))
+    return out
+
+
+def layernorm_bwd(dy_bct, x_rows, w, mean, rstd, T):
+    _check_dev(dy_bct, x_rows, w, mean, rstd)
+    R, D = x_rows.shape
+    dx = torch.empty_like(x_rows)
+    dw = torch.empty(D, device=x_rows.device)
+    db = torch.empty(D, device=x_rows.device)
+    s = dy_bct.stride()
+    _with_ws(x_rows.device, lambda wp, wn: N.lib.a2m_layernorm_bwd_f32(
+        _p(dy_bct), s[0], s[1], s[2], T, _p(x_rows), R, D, _p(w), _p(mean), _p(rstd), _p(dx), _p(dw),
+        _p(db), wp, wn, _stream()))
+    return dx, dw, db
+
+
+def self_attention_bwd(dy, x, weights, qkv, attn):
+    wq, bq, wk, bk, wv, bv, gamma = weights
+    _check_dev(dy, x, qkv, attn)
+    B, C, T = x.shape
+    dy = dy.contiguous()
+    assert x.stride(0) == dy.stride(0) and x.stride(1) == T and x.stride(2) == 1
+    dx = torch.empty(B, C, T, device=x.device)
+    dwq, dwk, dwv = torch.empty_like(wq), torch.empty_like(wk), torch.empty_like(wv)
+    dbq = torch.empty_like(bq) if bq is not None else None
+    dbk = torch.empty_like(bk) if bk is not None else None
+    dbv = torch.empty_like(bv) if bv is not None else None
+    dg = torch.empty(1, device=x.device)
+    need = N.lib.a2m_self_attention_bwd_ws_bytes(B, C, T)
+    WS.get(x.device, need)
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_self_attention_bwd_f32(
+        _p(dy), _p(x), x.stride(0), B, C, T, _p(wq), _p(bq), _p(wk), _p(bk), _p(wv), _p(bv), _p(gamma),
+        _p(qkv), _p(attn), _p(dx), _p(dwq), _p(dbq), _p(dwk), _p(dbk), _p(dwv), _p(dbv), _p(dg), wp, wn,
+        _stream()))
+    return dx, (dwq, dbq, dwk, dbk, dwv, dbv, dg)
+
+
+def channel_attention_bwd(dy, x, w1, b1, w2, b2):
+    _check_dev(dy, x)
+    x = x.contiguous()
+    dy = dy.contiguous()
+    B, C, T = x.shape
+    dx = torch.empty_like(x)
+    g = [torch.empty_like(t) for t in (w1, b1, w2, b2)]
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_channel_attention_bwd_f32(
+        _p(dy), _p(x), B, C, T, _p(w1), _p(b1), w1.shape[0], _p(w2), _p(b2), _p(dx), *[_p(t) for t in g],
+        wp, wn, _stream()))
+    return dx, g
+
+
+def graph_layer_bwd(x, dy, J, kind, nbr_ptr, nbr_idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
+                    slope=0.2, norm_res=True):
+    _check_dev(x, dy)
+    dy = dy.contiguous()
+    F = x.shape[0] // J
+    dx = torch.empty_like(x)
+    dw0 = torch.empty_like(w0)
+    dw1 = torch.empty_like(w1) if w1 is not None else None
+    das = torch.empty_like(att_src) if att_src is not None else None
+    dad = torch.empty_like(att_dst) if att_dst is not None else None
+    dbias = torch.empty_like(bias)
+    dlw = torch.empty_like(ln_w) if norm_res else None
+    dlb = torch.empty_like(ln_b) if norm_res else None
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_graph_layer_bwd_f32(
+        _p(x), _p(dy), F, J, kind, int(norm_res), _p(nbr_ptr), _p(nbr_idx), _p(w0), _p(w1), _p(att_src),
+        _p(att_dst), _p(bias), _p(ln_w), _p(ln_b), slope, _p(dx), _p(dw0), _p(dw1), _p(das), _p(dad),
+        _p(dbias), _p(dlw), _p(dlb), wp, wn, _stream()))
+    return dx, dw0, dw1, das, dad, dbias, dlw, dlb
+
+
+def interp_time_bwd(dy, H, W):
+    _check_dev(dy)
+    dy = dy.contiguous()
+    B, C, T = dy.shape
+    dx = torch.empty(B, C, H, W, device=dy.device)
+    N.check(N.lib.a2m_interp_time_bwd_f32(_p(dy), B, C, H, W, _p(dx), T, _stream()))
+    return dx
+
+
+def pose_losses_bwd(gen, real, grad_out, dgen):
+    _check_dev(gen, real, grad_out, dgen)
+    B, T, _ = gen.shape
+    rs = real.stride() if real is not None else (0, 0, 1)
+    _with_ws(gen.device, lambda wp, wn: N.lib.a2m_pose_losses_bwd_f32(
+        _p(gen), gen.stride(0), gen.stride(1), _p(real), rs[0], rs[1], B, T, _p(grad_out.contiguous()),
+        _p(dgen), wp, wn, _stream()))
+    return dgen
+
+
+def motion_losses(fake, real, grad_terms=None):
+    """terms = [L1(motion), smoothness, jerk] (version5_model_train.py:216-248); with
+    grad_terms (device [3]) also dfake = sum_i grad_terms[i] dterms[i]/dfake."""
+    _check_dev(fake, real, grad_terms)
+    fake = fake.contiguous()
+    real = real.contiguous() if real is not None else None
+    B, T, Fd = fake.shape
+    terms = torch.empty(3, device=fake.device)
+    dfake = torch.empty_like(fake) if grad_terms is not None else None
+    gt = grad_terms.contiguous() if grad_terms is not None else None
+    _with_ws(fake.device, lambda wp, wn: N.lib.a2m_motion_losses_f32(
+        _p(fake), _p(real), B, T, Fd, _p(terms), _p(gt), _p(dfake), wp, wn, _stream()))
+    return terms, dfake
+
+
+def mse_loss(pred, target, grad_loss=None, want_grad=False):
+    """loss = mean (pred - target)^2; dpred = grad_loss * 2 (pred - target) / n if wanted."""
+    _check_dev(pred, target, grad_loss)
+    pred, target = pred.contiguous(), target.contiguous()
+    loss = torch.empty((), device=pred.device)
+    d = torch.empty_like(pred) if (want_grad or grad_loss is not None) else None
+    _with_ws(pred.device, lambda wp, wn: N.lib.a2m_mse_loss_f32(
+        _p(pred), _p(target), pred.numel(), _p(loss), _p(grad_loss), _p(d), wp, wn, _stream()))
+    return loss, d
+
+
+def diff_time(x):
+    _check_dev(x)
+    x = x.contiguous()
+    B, T, Fd = x.shape
+    y = torch.empty(B, T - 1, Fd, device=x.device)
+    N.check(N.lib.a2m_diff_time_f32(_p(x), B, T, Fd, _p(y), _stream()))
+    return y
+
+
+def diff_time_bwd(dy, dx=None, accumulate=False):
+    _check_dev(dy, dx)
+    dy = dy.contiguous()
+    B, T1, Fd = dy.shape
+    if dx is None:
+        dx = torch.empty(B, T1 + 1, Fd, device=dy.device)
+    N.check(N.lib.a2m_diff_time_bwd_f32(_p(dy), B, T1 + 1, Fd, _p(dx), int(accumulate), _stream()))
+    return dx
+
+
+def adam_(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
+    _check_dev(param, grad, exp_avg, exp_avg_sq)
+    N.check(N.lib.a2m_adam_f32(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), lr, beta1,
+                               beta2, eps, weight_decay, step, _stream()))

@@ -1,0 +1,66 @@
+"""Adam over a flat parameter buffer (torch.optim.Adam semantics, the optimiser of
+version5_model_train.py:285-286), one fused HIP kernel per step.
+
+On construction the module's parameters are re-seated as views of one contiguous buffer and
+their .grad as views of one contiguous gradient buffer, so autograd accumulates straight
+into it, the data-parallel all-reduce is a single collective over `flat_grad`, and the
+update is one launch over `flat`.  `param_groups[0]['lr']` may be changed between steps
+(DynamicGANTraining.adjust_learning_rates does).
+"""
+import torch
+
+from . import functional as F
+
+
+class FlatAdam:
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        self.params = [p for p in params if p.requires_grad]
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, device=dev)
+        self.flat_grad = torch.zeros(n, device=dev)
+        self.exp_avg = torch.zeros(n, device=dev)
+        self.exp_avg_sq = torch.zeros(n, device=dev)
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            p.grad = self.flat_grad[off:off + k].view_as(p)
+            off += k
+        self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)]
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none=False):
+        self.flat_grad.zero_()
+        for p, (o, k) in zip(self.params, self._spans()):
+            if p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + k].data_ptr():
+                p.grad = self.flat_grad[o:o + k].view_as(p)
+
+    def _spans(self):
+        off = 0
+        for p in self.params:
+            yield off, p.numel()
+            off += p.numel()
+
+    @torch.no_grad()
+    def step(self):
+        # a gradient that autograd replaced instead of accumulating in place is folded back
+        for p, (o, k) in zip(self.params, self._spans()):
+            if p.grad is not None and p.grad.data_ptr() != self.flat_grad[o:o + k].data_ptr():
+                self.flat_grad[o:o + k].copy_(p.grad.reshape(-1))
+                p.grad = self.flat_grad[o:o + k].view_as(p)
+        self.step_count += 1
+        g = self.param_groups[0]
+        F.adam_(self.flat, self.flat_grad, self.exp_avg, self.exp_avg_sq, g['lr'], g['betas'][0],
+                g['betas'][1], g['eps'], g['weight_decay'], self.step_count)
+
+    def state_dict(self):
+        return {'step': self.step_count, 'exp_avg': self.exp_avg.clone(), 'exp_avg_sq': self.exp_avg_sq.clone(),
+                'param_groups': [dict(g) for g in self.param_groups]}
+
+    def load_state_dict(self, sd):
+        self.step_count = sd['step']
+        self.exp_avg.copy_(sd['exp_avg'])
+        self.exp_avg_sq.copy_(sd['exp_avg_sq'])
+        self.param_groups = [dict(g) for g in sd['param_groups']]

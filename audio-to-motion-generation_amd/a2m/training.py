@@ -1,0 +1,189 @@
+"""The per-clip GAN training step of version5_model_train.py on the HIP path, data-parallel
+over clips with one process per GPU.
+
+  DynamicGANTraining   version5_model_train.py:12-180 (host-side schedule: G/D step counts,
+                       learning-rate adaptation, smoothed noisy labels)
+  pos_to_motion        :208-213        compute_temporal_smoothness_loss :216-230
+  compute_jerk_loss    :233-248        one iteration (G steps, then D steps) :342-414
+
+Data parallelism: every rank runs the step on its shard of the batch;
+gradients of the network being stepped are averaged with ONE all-reduce over the
+optimiser's flat gradient buffer (RCCL over xGMI on MI355X, gloo in CPU tests).  The two
+scalar losses are averaged before they enter the schedule so every rank takes identical
+branches.  BatchNorm uses per-rank batch statistics (PyTorch DDP default, no SyncBN).
+The discriminator's parameters are frozen during the G steps: the reference computes their
+gradients there and throws them away (optimizer_D.zero_grad() at :388).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import autograd as AG
+from .optim import FlatAdam
+
+
+class DynamicGANTraining:
+    def __init__(self, g_lr=5e-6, d_lr=10e-6):
+        self.g_lr_initial = self.g_lr_current = g_lr
+        self.d_lr_initial = self.d_lr_current = d_lr
+        self.d_loss_history, self.g_loss_history = [], []
+        self.d_strong_threshold, self.g_weak_threshold, self.g_strong_threshold = 0.20, 0.80, 0.10
+        self.d_train_freq, self.g_train_freq = 1, 3
+        self.min_d_freq, self.max_d_freq, self.min_g_freq, self.max_g_freq = 1, 2, 2, 6
+        self.real_label_smooth, self.fake_label_smooth = 0.98, 0.02
+        self.dynamic_smooth = False
+        self.verbose = False
+
+    def _say(self, msg):
+        if self.verbose:
+            print(msg)
+
+    def update_loss_history(self, d_loss, g_loss):
+        self.d_loss_history = (self.d_loss_history + [d_loss])[-100:]
+        self.g_loss_history = (self.g_loss_history + [g_loss])[-100:]
+
+    def get_recent_avg_loss(self, window=10):
+        d, g = self.d_loss_history, self.g_loss_history
+        if len(d) >= window:
+            d, g = d[-window:], g[-window:]
+        return np.mean(d), np.mean(g)
+
+    def should_train_discriminator(self):
+        if not self.d_loss_history:
+            return True
+        d, g = self.get_recent_avg_loss()
+        return not (d < self.d_strong_threshold and g > self.g_weak_threshold)
+
+    def adjust_training_frequency(self, epoch):
+        if len(self.d_loss_history) >= 10:
+            d, g = self.get_recent_avg_loss()
+            ratio = d / (g + 1e-8)
+            if ratio < 0.15 or d < 0.1:
+                self.d_train_freq = max(1, self.d_train_freq - 1)
+                self.g_train_freq = min(self.max_g_freq, self.g_train_freq + 1)
+                self._say(f'D too strong: G={self.g_train_freq}, D={self.d_train_freq}')
+            elif ratio > 2.5:
+                self.d_train_freq = min(self.max_d_freq, self.d_train_freq + 1)
+                self.g_train_freq = max(self.min_g_freq, self.g_train_freq - 1)
+                self._say(f'G too strong: G={self.g_train_freq}, D={self.d_train_freq}')
+        return self.g_train_freq, self.d_train_freq
+
+    def adjust_learning_rates(self, optimizer_g, optimizer_d, epoch):
+        if len(self.d_loss_history) < 10:
+            g_lr, d_lr = self.g_lr_initial, self.d_lr_initial
+        else:
+            d, g = self.get_recent_avg_loss()
+            if d < self.d_strong_threshold:
+                self.d_lr_current *= 0.9
+                self.g_lr_current *= 1.05
+            elif d > 0.65 and g < 0.3:
+                self.d_lr_current *= 1.05
+                self.g_lr_current *= 0.9
+            g_lr, d_lr = self.g_lr_current, self.d_lr_current
+        for grp in optimizer_g.param_groups:
+            grp['lr'] = g_lr
+        for grp in optimizer_d.param_groups:
+            grp['lr'] = d_lr
+
+    def get_smooth_labels(self, epoch, batch_size, device, is_real=True, generator=None):
+        progress = min(max(epoch / 60.0, 0.0), 1.0)
+        noise_std = 0.01 - progress * (0.01 - 0.002)
+        if is_real:
+            val, lo, hi = self.real_label_smooth - 0.05 * (1 - progress), 0.85, 1.0
+        else:
+            val, lo, hi = self.fake_label_smooth + 0.05 * (1 - progress), 0.0, 0.15
+        noise = torch.randn(batch_size, 4, device=device, generator=generator) * noise_std
+        return (torch.full((batch_size, 4), val, device=device) + noise).clamp_(lo, hi)
+
+
+def pos_to_motion(pose):
+    return AG.pos_to_motion(pose)
+
+
+def compute_temporal_smoothness_loss_and_jerk(fake_pose, real_pose):
+    """[L1(real motion, fake motion), smoothness, jerk] from POSES (fused kernel)."""
+    return AG.motion_terms(fake_pose, real_pose)
+
+
+class GANTrainer:
+    """One version5_model_train.py iteration per call, optionally data-parallel."""
+
+    def __init__(self, generator, discriminator, lr=10e-4, lambda_gan=1.0, lambda_d=1.0,
+                 dynamic=None, fixed_labels=None, process_group=None):
+        self.G, self.D = generator, discriminator
+        self.opt_G = FlatAdam(generator.parameters(), lr=lr)
+        self.opt_D = FlatAdam(discriminator.parameters(), lr=lr)
+        self.dyn = dynamic if dynamic is not None else DynamicGANTraining(g_lr=lr / 2, d_lr=lr)
+        self.lambda_gan, self.lambda_d = lambda_gan, lambda_d
+        self.fixed_labels = fixed_labels          # (valid, fake) values for deterministic runs
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.last_d_loss = None
+
+    def _allreduce_(self, t):
+        if self.world > 1:
+            dist.all_reduce(t, group=self.pg)
+            t.div_(self.world)
+
+    def _labels(self, epoch, B, dev):
+        if self.fixed_labels is not None:
+            v, f = self.fixed_labels
+            return torch.full((B, 4), v, device=dev), torch.full((B, 4), f, device=dev)
+        return (self.dyn.get_smooth_labels(epoch, B, dev, True),
+                self.dyn.get_smooth_labels(epoch, B, dev, False))
+
+    def g_step(self, audio, real_pose, valid):
+        self.opt_G.zero_grad()
+        fake_pose, internal = self.G(audio, real_pose=real_pose)
+        fake_d, _ = self.D(pos_to_motion(fake_pose))
+        terms = compute_temporal_smoothness_loss_and_jerk(fake_pose, real_pose)
+        g_loss = terms[0] + self.lambda_gan * AG.mse_loss(fake_d, valid) + 0.1 * terms[1] + 0.05 * terms[2]
+        for loss in internal:
+            g_loss = g_loss + loss
+        g_loss.backward()
+        self._allreduce_(self.opt_G.flat_grad)
+        self.opt_G.step()
+        return g_loss.detach()
+
+    def d_step(self, audio, real_motion, valid, fake):
+        self.opt_D.zero_grad()
+        with torch.no_grad():
+            fp, _ = self.G(audio)
+            fm = pos_to_motion(fp)
+        fake_d, _ = self.D(fm.detach())
+        real_d, _ = self.D(real_motion)
+        d_loss = AG.mse_loss(real_d, valid) + self.lambda_d * AG.mse_loss(fake_d, fake)
+        d_loss.backward()
+        self._allreduce_(self.opt_D.flat_grad)
+        self.opt_D.step()
+        return d_loss.detach()
+
+    def iteration(self, audio, real_pose, epoch=0, g_freq=None, d_freq=None, sync_losses=True):
+        """version5_model_train.py:330-414 for one batch; returns (D_loss, G_loss) tensors."""
+        dev = audio.device
+        gf = g_freq if g_freq is not None else self.dyn.g_train_freq
+        df = d_freq if d_freq is not None else self.dyn.d_train_freq
+        valid, fake = self._labels(epoch, audio.shape[0], dev)
+        real_motion = pos_to_motion(real_pose)
+        d_params = [p for p in self.D.parameters()]
+        for p in d_params:
+            p.requires_grad_(False)
+        try:
+            for _ in range(gf):
+                g_loss = self.g_step(audio, real_pose, valid)
+        finally:
+            for p in d_params:
+                p.requires_grad_(True)
+        d_loss = None
+        if self.dyn.should_train_discriminator():
+            for _ in range(df):
+                d_loss = self.d_step(audio, real_motion, valid, fake)
+        if d_loss is None:  # reference reuses the last logged D loss when D is skipped
+            d_loss = self.last_d_loss if self.last_d_loss is not None else torch.ones((), device=dev)
+        self.last_d_loss = d_loss
+        if sync_losses:
+            pair = torch.stack([d_loss.reshape(()), g_loss.reshape(())])
+            self._allreduce_(pair)
+            d_val, g_val = pair.tolist()
+            self.dyn.update_loss_history(d_val, g_val)
+        return d_loss, g_loss

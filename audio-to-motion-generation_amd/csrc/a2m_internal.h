@@ -107,4 +107,18 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
          void* ws, size_t ws_bytes, hipStream_t stream, int force_split = 0);
 size_t gemm_ws_bytes(int M, int N, int K, int batch);
 
+// shared host-side launch helpers (defined next to their kernels)
+int softmax_rows(float* x, int rows, int n, hipStream_t st);                       // ops.hip
+int stack_qkv(const float* wq, const float* bq, const float* wk, const float* bk,  // ops.hip
+              const float* wv, const float* bv, int C, float* wcat, float* bcat, hipStream_t st);
+int reduce_cols(const float* part, int rows, int stride, int cols, float* out,     // train_norm.hip
+                int accumulate, hipStream_t st);
+
+inline Gather gather_bct(const float* x, int64_t bs, int cs, int T) {  // rows n=(b,t), k=c of [B][C][T]
+  Gather g{};
+  g.base = x; g.sr0 = (int)bs; g.R1 = 1; g.R2 = T; g.ar2 = 1; g.sw = 1; g.Lw = T;
+  g.sk0 = cs; g.K1 = 1; g.K2 = 1; g.Lh = 1; g.divh = g.divw = 1; g.kcontig = 0;
+  return g;
+}
+
 }  // namespace a2m

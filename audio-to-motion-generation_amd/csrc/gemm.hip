@@ -339,7 +339,7 @@ static Plan plan_for(int M, int N, int K, int batch) {
   static const int force_split = env_int("A2M_GEMM_SPLIT", 0);
   auto splits_for = [&](int64_t tiles) {
     int s = 1;
-    while (s < 16 && tiles * s < 512 && K / (s * 2) >= 256) s *= 2;
+    while (s < 64 && tiles * s < 512 && K / (s * 2) >= 256) s *= 2;
     return s;
   };
   const int64_t t128 = cdiv(M, 128) * cdiv(N, 128) * (int64_t)batch;

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int R, i
 }
 
 __global__ void mean_time_kernel(const float* x, int64_t xs_b, int64_t xs_c, int C, int T, int BC,
-                                 float* y) {
+                                 float scale, float* y) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= BC) return;
@@ -186,16 +186,16 @@ __global__ void mean_time_kernel(const float* x, int64_t xs_b, int64_t xs_c, int
   float s = 0.f;
   for (int t = lane; t < T; t += 64) s += p[t];
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (lane == 0) y[i] = s / (float)T;
+  if (lane == 0) y[i] = scale * (s / (float)T);
 }
 
-__global__ void repeat_time_kernel(const float* x, int C, int T, int64_t total, float* y,
-                                   int64_t ys_b, int64_t ys_c) {
+__global__ void repeat_time_kernel(const float* x, int C, int T, int64_t total, float scale,
+                                   float* y, int64_t ys_b, int64_t ys_c) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int t = (int)(i % T);
     const int64_t bc = i / T;
-    y[(bc / C) * ys_b + (bc % C) * ys_c + t] = x[bc];
+    y[(bc / C) * ys_b + (bc % C) * ys_c + t] = scale * x[bc];
   }
 }
 
@@ -244,6 +244,15 @@ __global__ void stack_qkv_kernel(const float* wq, const float* bq, const float* 
       bcat[row] = b ? b[r] : 0.f;
     }
   }
+}
+
+int stack_qkv(const float* wq, const float* bq, const float* wk, const float* bk, const float* wv,
+              const float* bv, int C, float* wcat, float* bcat, hipStream_t st) {
+  const int64_t total = (int64_t)(C / 4 + C) * C;
+  hipLaunchKernelGGL(stack_qkv_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 8192)),
+                     dim3(256), 0, st, wq, bq, wk, bk, wv, bv, C, wcat, bcat);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
 }
 
 int softmax_rows(float* x, int rows, int n, hipStream_t st) {
@@ -380,22 +389,22 @@ int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t
 }
 
 int a2m_mean_time_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
-                      int32_t T, float* y, void* stream) {
+                      int32_t T, float scale, float* y, void* stream) {
   A2M_CHECK_ARG(x && y && B > 0 && C > 0 && T > 0, "mean_time: bad args");
   const int BC = B * C;
   hipLaunchKernelGGL(mean_time_kernel, dim3((unsigned)cdiv(BC, 4)), dim3(256), 0,
-                     as_stream(stream), x, xs_b, xs_c, C, T, BC, y);
+                     as_stream(stream), x, xs_b, xs_c, C, T, BC, scale, y);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }
 
-int a2m_repeat_time_f32(const float* x, int32_t B, int32_t C, int32_t T, float* y, int64_t ys_b,
-                        int64_t ys_c, void* stream) {
+int a2m_repeat_time_f32(const float* x, int32_t B, int32_t C, int32_t T, float scale, float* y,
+                        int64_t ys_b, int64_t ys_c, void* stream) {
   A2M_CHECK_ARG(x && y && B > 0 && C > 0 && T > 0, "repeat_time: bad args");
   const int64_t total = (int64_t)B * C * T;
   const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
   hipLaunchKernelGGL(repeat_time_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, C, T,
-                     total, y, ys_b, ys_c);
+                     total, scale, y, ys_b, ys_c);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

@@ -1,0 +1,157 @@
+// Convolution backward on the implicit-GEMM engine.
+//
+// dgrad: dX = conv_transpose(dY, W).  Decomposed by output phase (rh, rw) so a stride-s
+// conv's dgrad never multiplies the (s^2 - 1)/s^2 structural zeros a naive transposed
+// convolution would: phase (rh, rw) of dX only meets the taps with (r + pad - k) % s == 0,
+// each a dense GEMM over K = Co * taps_h * taps_w with per-phase packed weights.
+// wgrad: dW[co][ci,kh,kw] = sum_{b,ho,wo} dY[b][co][ho][wo] X[b][ci][ho*s+kh-ph][wo*s+kw-pw],
+// a GEMM over K = B*Ho*Wo with split-K (partials reduced in a fixed order).
+// 1-D convs are the H = 1 case; ConvTranspose1d's dgrad / wgrad are a plain conv forward /
+// this wgrad with the operands' roles exchanged (see a2m.autograd).
+#include <algorithm>
+
+#include "a2m_internal.h"
+
+namespace a2m {
+
+struct PhaseTaps {
+  int k0, n;  // first tap, tap count (taps are k0, k0 + s, ...)
+};
+
+static PhaseTaps phase_taps_h(int r, int k, int s, int pad) {
+  PhaseTaps t{-1, 0};
+  for (int kk = 0; kk < k; ++kk)
+    if ((((r + pad - kk) % s) + s) % s == 0) { if (t.k0 < 0) t.k0 = kk; ++t.n; }
+  return t;
+}
+
+// P_(rh,rw)[ci][(co*nth + th)*ntw + tw] = W[co][ci][kh0 + s*th][kw0 + s*tw]
+__global__ void dgrad_pack_kernel(const float* w, int Co, int Ci, int kh, int kw, int nth, int ntw,
+                                  int kh0, int kw0, int sh, int sw, float* out) {
+  const int64_t total = (int64_t)Ci * Co * nth * ntw;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int tw = (int)(i % ntw);
+    int64_t t = i / ntw;
+    const int th = (int)(t % nth);
+    t /= nth;
+    const int co = (int)(t % Co);
+    const int ci = (int)(t / Co);
+    out[i] = w[(((int64_t)co * Ci + ci) * kh + kh0 + sh * th) * kw + kw0 + sw * tw];
+  }
+}
+
+}  // namespace a2m
+
+using namespace a2m;
+
+extern "C" {
+
+int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int32_t Wo,
+                         const float* w, int32_t Ci, int32_t H, int32_t W, int32_t kh, int32_t kw,
+                         int32_t stride_h, int32_t stride_w, int32_t pad_h, int32_t pad_w,
+                         float* dx, int64_t dxs_b, int64_t dxs_c, int64_t dxs_h, int64_t dxs_w,
+                         int32_t accumulate, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(dy && w && dx && B > 0 && Co > 0 && Ci > 0 && H > 0 && W > 0 && kh > 0 && kw > 0 &&
+                    stride_h > 0 && stride_w > 0 && pad_h >= 0 && pad_w >= 0,
+                "conv_dgrad: bad args");
+  A2M_CHECK_ARG(Ho == (H + 2 * pad_h - kh) / stride_h + 1 && Wo == (W + 2 * pad_w - kw) / stride_w + 1,
+                "conv_dgrad: output geometry mismatch");
+  A2M_CHECK_ARG((int64_t)B * Co * Ho * Wo < (1LL << 31) && (int64_t)B * dxs_b < (1LL << 31),
+                "conv_dgrad: too large");
+  const size_t pack_bytes = ((size_t)Ci * Co * kh * kw * sizeof(float) + 255) & ~size_t(255);
+  if (!ws || ws_bytes < pack_bytes) {
+    set_error("conv_dgrad: workspace too small (%zu < %zu bytes)", ws_bytes, pack_bytes);
+    return A2M_EWS;
+  }
+  hipStream_t st = as_stream(stream);
+  float* packed = static_cast<float*>(ws);
+  for (int rh = 0; rh < stride_h; ++rh) {
+    const int nuh = (H - rh + stride_h - 1) / stride_h;
+    if (nuh <= 0) continue;
+    const PhaseTaps th = phase_taps_h(rh, kh, stride_h, pad_h);
+    for (int rw = 0; rw < stride_w; ++rw) {
+      const int nuw = (W - rw + stride_w - 1) / stride_w;
+      if (nuw <= 0) continue;
+      const PhaseTaps tw = phase_taps_h(rw, kw, stride_w, pad_w);
+      const int K = Co * th.n * tw.n;
+      Epilogue E = epi_dense(dx + rh * dxs_h + rw * dxs_w, 0);
+      E.N1 = nuh; E.N2 = nuw; E.so0 = (int)dxs_b; E.so1 = (int)(stride_h * dxs_h);
+      E.so2 = (int)(stride_w * dxs_w); E.som = (int)dxs_c; E.accumulate = accumulate;
+      Gather A = dense_rk(packed, std::max(K, 1));
+      Gather Bg{};
+      Bg.base = dy; Bg.sr0 = Co * Ho * Wo; Bg.R1 = nuh; Bg.R2 = nuw; Bg.ar1 = 1; Bg.ar2 = 1;
+      Bg.sk0 = Ho * Wo; Bg.K1 = std::max(th.n, 1); Bg.K2 = std::max(tw.n, 1); Bg.bk1 = -1; Bg.bk2 = -1;
+      Bg.ch = K ? (rh + pad_h - th.k0) / stride_h : 0;
+      Bg.cw = K ? (rw + pad_w - tw.k0) / stride_w : 0;
+      Bg.divh = Bg.divw = 1; Bg.Lh = Ho; Bg.Lw = Wo; Bg.sh = Wo; Bg.sw = 1; Bg.kcontig = 0;
+      if (K > 0) {
+        hipLaunchKernelGGL(dgrad_pack_kernel,
+                           dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Ci * K, 256), 8192)),
+                           dim3(256), 0, st, w, Co, Ci, kh, kw, th.n, tw.n, th.k0, tw.k0, stride_h,
+                           stride_w, packed);
+        A2M_LAUNCH_CHECK();
+      }
+      int rc = gemm(A, Bg, E, Ci, B * nuh * nuw, K, 1, static_cast<char*>(ws) + pack_bytes,
+                    ws_bytes - pack_bytes, st);
+      if (rc) return rc;
+    }
+  }
+  return A2M_OK;
+}
+
+int a2m_conv2d_wgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int32_t Wo,
+                         const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_h, int64_t xs_w,
+                         int32_t Ci, int32_t H, int32_t W, int32_t kh, int32_t kw,
+                         int32_t stride_h, int32_t stride_w, int32_t pad_h, int32_t pad_w,
+                         float* dw, int32_t accumulate, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(dy && x && dw && B > 0 && Co > 0 && Ci > 0 && Ho > 0 && Wo > 0, "conv_wgrad: bad args");
+  A2M_CHECK_ARG((int64_t)B * Co * Ho * Wo < (1LL << 31) && (int64_t)B * xs_b < (1LL << 31),
+                "conv_wgrad: too large");
+  // A(m=co, k=(b,ho,wo)) = dY[b][co][ho][wo]   (dY contiguous)
+  Gather A{};
+  A.base = dy; A.sr0 = Ho * Wo; A.R1 = A.R2 = 1;
+  A.sk0 = Co * Ho * Wo; A.K1 = Ho; A.K2 = Wo; A.bk1 = 1; A.bk2 = 1; A.Lh = Ho; A.Lw = Wo;
+  A.sh = Wo; A.sw = 1; A.divh = A.divw = 1; A.kcontig = 1;
+  // B(n=(ci,ih,iw), k=(b,ho,wo)) = X[b][ci][ho*s + ih - ph][wo*s + iw - pw]
+  Gather Bg{};
+  Bg.base = x; Bg.sr0 = (int)xs_c; Bg.R1 = kh; Bg.R2 = kw; Bg.ar1 = 1; Bg.ar2 = 1;
+  Bg.sk0 = (int)xs_b; Bg.K1 = Ho; Bg.K2 = Wo; Bg.bk1 = stride_h; Bg.bk2 = stride_w;
+  Bg.ch = -pad_h; Bg.cw = -pad_w; Bg.divh = Bg.divw = 1; Bg.Lh = H; Bg.Lw = W;
+  Bg.sh = (int)xs_h; Bg.sw = (int)xs_w; Bg.kcontig = 1;
+  Epilogue E = epi_dense(dw, Ci * kh * kw);
+  E.accumulate = accumulate;
+  return gemm(A, Bg, E, Co, Ci * kh * kw, B * Ho * Wo, 1, ws, ws_bytes, as_stream(stream));
+}
+
+int a2m_gemm_f32(int32_t M, int32_t N, int32_t N1, int32_t K, int32_t K1, int32_t batch,
+                 const float* A, int64_t a_bs, int64_t a_m, int64_t a_k0, int64_t a_k1,
+                 const float* B, int64_t b_bs, int64_t b_n0, int64_t b_n1, int64_t b_k0,
+                 int64_t b_k1, float* C, int64_t c_bs, int64_t c_m, int64_t c_n0, int64_t c_n1,
+                 const float* bias, float alpha, int32_t accumulate, void* ws, size_t ws_bytes,
+                 void* stream) {
+  A2M_CHECK_ARG(A && B && C && M > 0 && N > 0 && K >= 0 && batch > 0 && N1 > 0 && K1 > 0 &&
+                    N % N1 == 0 && K % K1 == 0, "gemm: bad args");
+  A2M_CHECK_ARG(alpha == 1.f, "gemm: only alpha = 1 is supported");
+  auto fits = [](int64_t v) { return v > -(1LL << 31) && v < (1LL << 31); };
+  A2M_CHECK_ARG(fits(a_m) && fits(a_k0) && fits(a_k1) && fits(b_n0) && fits(b_n1) && fits(b_k0) &&
+                    fits(b_k1) && fits(c_m) && fits(c_n0) && fits(c_n1), "gemm: stride too large");
+  Gather Ag{};
+  Ag.base = A; Ag.bstride = a_bs; Ag.sr0 = (int)a_m; Ag.R1 = Ag.R2 = 1;
+  Ag.sk0 = (int)a_k0; Ag.K1 = K1; Ag.K2 = 1; Ag.bk1 = 1; Ag.sh = (int)a_k1; Ag.Lh = K1; Ag.Lw = 1;
+  Ag.divh = Ag.divw = 1;
+  Ag.kcontig = (K1 > 1 ? a_k1 == 1 : a_k0 == 1) ? 1 : 0;
+  if (K1 == 1 && Ag.kcontig) { Ag.sh = 0; Ag.bk1 = 0; }  // plain [M][K] -> vectorisable
+  Gather Bg{};
+  Bg.base = B; Bg.bstride = b_bs; Bg.sr0 = (int)b_n0; Bg.R1 = 1; Bg.R2 = N1; Bg.ar2 = 1;
+  Bg.sw = (int)b_n1; Bg.Lw = N1; Bg.sk0 = (int)b_k0; Bg.K1 = K1; Bg.K2 = 1; Bg.bk1 = 1;
+  Bg.sh = (int)b_k1; Bg.Lh = K1; Bg.divh = Bg.divw = 1;
+  Bg.kcontig = (K1 > 1 ? b_k1 == 1 : b_k0 == 1) ? 1 : 0;
+  if (N1 == 1 && K1 == 1 && Bg.kcontig) { Bg.R2 = 1; Bg.ar2 = 0; Bg.sw = 0; Bg.sh = 0; Bg.bk1 = 0; }
+  Epilogue E = epi_dense(C, 0, c_bs);
+  E.N1 = 1; E.N2 = N1; E.so0 = (int)c_n0; E.so2 = (int)c_n1; E.som = (int)c_m;
+  E.bias = bias; E.accumulate = accumulate;
+  return gemm(Ag, Bg, E, M, N, K, batch, ws, ws_bytes, as_stream(stream));
+}
+
+}  // extern "C"

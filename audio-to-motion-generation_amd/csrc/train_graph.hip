@@ -1,0 +1,485 @@
+// Backward of the fused skeleton-graph layer (forward: graph.hip).
+//
+// Per workgroup of whole frames (<= 128 nodes) the forward is recomputed from x (attention
+// logits, per-head edge softmax, aggregated inputs Y_h, pre-LayerNorm output o), then:
+//   LN/LeakyReLU/residual:  du = dy * leaky'(u),  do = rstd (g - mean g - ohat mean(g ohat)),
+//                           g = du * ln_w;  dln_w += du ohat, dln_b += du, dbias += do
+//   GAT (4 heads, mean):    dY_h = do W_h / 4                         (MFMA)
+//                           dalpha_ijh = dY_h,i . x_j;  softmax + LeakyReLU backward -> ds
+//                           da_dst[i,h] = sum_j ds_ijh,  da_src[j,h] = sum_i ds_ijh
+//                           dx_j += sum_i alpha_ijh dY_h,i + da_src[j,h] U_h + da_dst[j,h] U_4+h
+//                           dU_q += sum_n da_q[n] x_n   (U_h = W_h^T att_h, chained on the host)
+//   GraphConv:              dagg = do W_rel, dx = do W_root + sum_{i ~ j} dagg_i
+// Gathers over the (symmetric) skeleton graph replace scatters, so every sum has a fixed
+// order.  Weight gradients need sums over all nodes: the kernel writes Y_h (GAT) / agg
+// (GraphConv) and do (x 1/4 for GAT) to global memory and the host reduces them with
+// engine GEMMs; bias / LayerNorm / U partials are reduced per workgroup.
+#include <algorithm>
+
+#include "a2m_internal.h"
+
+namespace a2m {
+
+constexpr int BF = 64;
+constexpr int BH = 4;
+constexpr int BMAXN = 128;
+constexpr int BZP = BF + 4;
+constexpr int BDEG = 8;
+constexpr int BPART = 3 * BF + 2 * BH * BF;  // dbias | dln_w | dln_b | dU[8][64]
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// acc[t] += A[rows][64] (LDS, pitch BZP) . W^T where B(n=j, k=c) = Wt(j, c) given by functor
+template <class WF>
+__device__ __forceinline__ void mfma_rows64(floatx16 (&acc)[2], const float* A, int arow, int lh,
+                                            int li, WF wf) {
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc) {
+    const float* p = A + arow * BZP + kc * 16 + lh * 8;
+    const float4 a0 = *reinterpret_cast<const float4*>(p);
+    const float4 a1 = *reinterpret_cast<const float4*>(p + 4);
+    const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float bf[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) bf[s] = wf(t * 32 + li, kc * 16 + lh * 8 + s);
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void acc_to_lds(const floatx16 (&acc)[2], float* dst, int wave, int lh,
+                                           int li, float scale) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+      dst[r * BZP + t * 32 + li] = acc[t][q] * scale;
+    }
+}
+
+__device__ __forceinline__ void zero_acc(floatx16 (&acc)[2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+}
+
+__global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, int F, int J, int kind, int norm_res,
+    const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_idx, const float* __restrict__ w0,
+    const float* __restrict__ w1, const float* __restrict__ Ug, const float* __restrict__ bias,
+    const float* __restrict__ ln_w, const float* __restrict__ ln_b, float slope,
+    float* __restrict__ dx, float* __restrict__ ybuf, float* __restrict__ dout,
+    float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float xs[BMAXN * BZP];
+  __shared__ __attribute__((aligned(16))) float bufA[BMAXN * BZP];
+  __shared__ __attribute__((aligned(16))) float bufB[BMAXN * BZP];
+  __shared__ float U[2 * BH][BF];
+  __shared__ float al[BMAXN][2 * BH];
+  __shared__ float ew[BMAXN][BDEG];
+  __shared__ float dsb[BMAXN][BDEG];
+  __shared__ float dal[BMAXN][2];
+  __shared__ unsigned char nbl[BMAXN][BDEG];
+  __shared__ unsigned char ndeg[BMAXN];
+  __shared__ float red[16][3 * BF];
+
+  const int fpb = BMAXN / J;
+  const int NBmax = fpb * J;
+  const int64_t node0 = (int64_t)blockIdx.x * NBmax;
+  const int NB = (int)min<int64_t>(NBmax, (int64_t)F * J - node0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5, cg = tid & 15, nr0 = tid >> 4;
+  const int arow = wave * 32 + li;
+  const int ywidth = kind == 0 ? BH * BF : BF;
+
+  for (int i = tid; i < BMAXN * (BF / 4); i += blockDim.x) {
+    const int n = i / (BF / 4), q = i % (BF / 4);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n < NB) v = *reinterpret_cast<const float4*>(x + (node0 + n) * BF + q * 4);
+    *reinterpret_cast<float4*>(xs + n * BZP + q * 4) = v;
+  }
+  if (kind == 0)
+    for (int i = tid; i < 2 * BH * BF; i += blockDim.x) (&U[0][0])[i] = Ug[i];
+  for (int n = tid; n < BMAXN; n += blockDim.x) {
+    int d = 0;
+    if (n < NB) {
+      const int f0 = (n / J) * J, ln = n % J;
+      for (int e = nbr_ptr[ln]; e < nbr_ptr[ln + 1] && d < BDEG; ++e) nbl[n][d++] = f0 + nbr_idx[e];
+      if (kind == 0 && d < BDEG) nbl[n][d++] = n;
+    }
+    ndeg[n] = d;
+  }
+  __syncthreads();
+  if (kind == 0) {
+    for (int i = tid; i < NB * 2 * BH; i += blockDim.x) {
+      const int n = i >> 3, q = i & 7;
+      float s = 0.f;
+      for (int k = 0; k < BF; ++k) s += xs[n * BZP + k] * U[q][k];
+      al[n][q] = s;
+    }
+    __syncthreads();
+  }
+
+  auto edge_softmax = [&](int h) {
+    for (int n = tid; n < NB; n += blockDim.x) {
+      const int d = ndeg[n];
+      const float ad = al[n][BH + h];
+      float e[BDEG];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < BDEG; ++q)
+        if (q < d) {
+          const float s = al[nbl[n][q]][h] + ad;
+          e[q] = s > 0.f ? s : s * 0.2f;
+          mx = fmaxf(mx, e[q]);
+        }
+      float den = 0.f;
+#pragma unroll
+      for (int q = 0; q < BDEG; ++q)
+        if (q < d) { e[q] = expf(e[q] - mx); den += e[q]; }
+      const float inv = 1.f / (den + 1e-16f);
+#pragma unroll
+      for (int q = 0; q < BDEG; ++q) ew[n][q] = q < d ? e[q] * inv : 0.f;
+    }
+  };
+
+  // ---------------------------------------------------------------- forward recompute
+  floatx16 acc[2];
+  zero_acc(acc);
+  const int nseg = kind == 0 ? BH : 2;
+  for (int seg = 0; seg < nseg; ++seg) {
+    const float* Wseg = kind == 0 ? w0 + (int64_t)seg * BF * BF : (seg == 0 ? w0 : w1);
+    const float* A = bufA;
+    if (kind == 0 || seg == 0) {
+      if (kind == 0) {
+        edge_softmax(seg);
+        __syncthreads();
+      }
+      for (int i = tid; i < BMAXN * 16; i += blockDim.x) {
+        const int n = i >> 4, c4 = i & 15;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int d = n < NB ? ndeg[n] : 0;
+        for (int q = 0; q < d; ++q) {
+          const float w = kind == 0 ? ew[n][q] : 1.f;
+          const float4 v = *reinterpret_cast<const float4*>(xs + nbl[n][q] * BZP + c4 * 4);
+          a.x += w * v.x; a.y += w * v.y; a.z += w * v.z; a.w += w * v.w;
+        }
+        *reinterpret_cast<float4*>(bufA + n * BZP + c4 * 4) = a;
+        if (n < NB) *reinterpret_cast<float4*>(ybuf + (node0 + n) * ywidth + seg * BF + c4 * 4) = a;
+      }
+      __syncthreads();
+    } else {
+      A = xs;
+    }
+    mfma_rows64(acc, A, arow, lh, li, [&](int j, int c) { return Wseg[j * BF + c]; });
+    __syncthreads();
+  }
+  acc_to_lds(acc, bufA, wave, lh, li, kind == 0 ? 1.f / BH : 1.f);  // o (bias added below)
+  __syncthreads();
+
+  // ---------------------------------------------------------------- LN / act / residual bwd
+  float dxa[8][4];
+  float pb[4] = {0.f, 0.f, 0.f, 0.f}, plw[4] = {0.f, 0.f, 0.f, 0.f}, plb[4] = {0.f, 0.f, 0.f, 0.f};
+  const float oscale = kind == 0 ? 1.f / BH : 1.f;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int n = nr0 + 16 * r;
+    float o[4], g4[4];
+    const float4 dy4 = n < NB ? *reinterpret_cast<const float4*>(dy + (node0 + n) * BF + cg * 4)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float dyv[4] = {dy4.x, dy4.y, dy4.z, dy4.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = bufA[n * BZP + cg * 4 + q] + bias[cg * 4 + q];
+    float dov[4];
+    if (norm_res) {
+      float s = o[0] + o[1] + o[2] + o[3];
+      for (int m = 1; m < 16; m <<= 1) s += __shfl_xor(s, m);
+      const float mean = s * (1.f / BF);
+      float ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ss += (o[q] - mean) * (o[q] - mean);
+      for (int m = 1; m < 16; m <<= 1) ss += __shfl_xor(ss, m);
+      const float rstd = 1.f / sqrtf(ss * (1.f / BF) + 1e-5f);
+      float sg = 0.f, sgx = 0.f, oh[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = cg * 4 + q;
+        oh[q] = (o[q] - mean) * rstd;
+        const float u = oh[q] * ln_w[c] + ln_b[c];
+        const float du = n < NB ? dyv[q] * (u > 0.f ? 1.f : slope) : 0.f;
+        plw[q] += du * oh[q];
+        plb[q] += du;
+        g4[q] = du * ln_w[c];
+        sg += g4[q];
+        sgx += g4[q] * oh[q];
+      }
+      for (int m = 1; m < 16; m <<= 1) {
+        sg += __shfl_xor(sg, m);
+        sgx += __shfl_xor(sgx, m);
+      }
+      const float mg = sg * (1.f / BF), mgx = sgx * (1.f / BF);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dov[q] = n < NB ? rstd * (g4[q] - mg - oh[q] * mgx) : 0.f;
+        dxa[r][q] = n < NB ? dyv[q] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dov[q] = dyv[q];
+        dxa[r][q] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pb[q] += dov[q];
+    *reinterpret_cast<float4*>(bufB + n * BZP + cg * 4) = make_float4(dov[0], dov[1], dov[2], dov[3]);
+    if (n < NB)
+      *reinterpret_cast<float4*>(dout + (node0 + n) * BF + cg * 4) =
+          make_float4(dov[0] * oscale, dov[1] * oscale, dov[2] * oscale, dov[3] * oscale);
+  }
+  __syncthreads();
+
+  float dU[2];  // per-thread slice of the dU partial: items tid and tid + 256 of [8][64]
+  dU[0] = dU[1] = 0.f;
+  if (kind == 0) {
+    for (int h = 0; h < BH; ++h) {
+      edge_softmax(h);
+      // dY_h = do W_h / 4  -> bufA
+      zero_acc(acc);
+      const float* Wh = w0 + (int64_t)h * BF * BF;
+      mfma_rows64(acc, bufB, arow, lh, li, [&](int j, int c) { return Wh[c * BF + j]; });
+      acc_to_lds(acc, bufA, wave, lh, li, 1.f / BH);
+      __syncthreads();
+      // dalpha[n][q] = dY_h[n] . x[nbl[n][q]]  (16 lanes per node)
+      for (int i = tid; i < BMAXN * 16; i += blockDim.x) {
+        const int n = i >> 4, c4 = i & 15;
+        const int d = ndeg[n];
+        const float4 g = *reinterpret_cast<const float4*>(bufA + n * BZP + c4 * 4);
+        for (int q = 0; q < BDEG; ++q) {
+          float v = 0.f;
+          if (q < d) {
+            const float4 xv = *reinterpret_cast<const float4*>(xs + nbl[n][q] * BZP + c4 * 4);
+            v = g.x * xv.x + g.y * xv.y + g.z * xv.z + g.w * xv.w;
+          }
+          for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m);
+          if (c4 == 0) dsb[n][q] = v;
+        }
+      }
+      __syncthreads();
+      // softmax + LeakyReLU backward: ds (pre-activation logit grads), da_dst
+      for (int n = tid; n < NB; n += blockDim.x) {
+        const int d = ndeg[n];
+        const float ad = al[n][BH + h];
+        float sdot = 0.f;
+        for (int q = 0; q < d; ++q) sdot += ew[n][q] * dsb[n][q];
+        float sum = 0.f;
+        for (int q = 0; q < d; ++q) {
+          const float s = al[nbl[n][q]][h] + ad;
+          const float de = ew[n][q] * (dsb[n][q] - sdot);
+          const float ds = de * (s > 0.f ? 1.f : 0.2f);
+          dsb[n][q] = ds;
+          sum += ds;
+        }
+        dal[n][1] = sum;
+      }
+      __syncthreads();
+      // da_src[j] = sum over the targets i that have j as a source (symmetric graph)
+      for (int j = tid; j < NB; j += blockDim.x) {
+        float s = 0.f;
+        for (int q = 0; q < ndeg[j]; ++q) {
+          const int i = nbl[j][q];
+          for (int p = 0; p < ndeg[i]; ++p)
+            if (nbl[i][p] == j) { s += dsb[i][p]; break; }
+        }
+        dal[j][0] = s;
+      }
+      __syncthreads();
+      // dx += aggregation adjoint + logit adjoint;  dU partials
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int n = nr0 + 16 * r;
+        if (n >= NB) continue;
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < ndeg[n]; ++q) {
+          const int i = nbl[n][q];
+          float alpha = 0.f;
+          for (int p = 0; p < ndeg[i]; ++p)
+            if (nbl[i][p] == n) { alpha = ew[i][p]; break; }
+          const float4 g = *reinterpret_cast<const float4*>(bufA + i * BZP + cg * 4);
+          a[0] += alpha * g.x; a[1] += alpha * g.y; a[2] += alpha * g.z; a[3] += alpha * g.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          dxa[r][q] += a[q] + dal[n][0] * U[h][cg * 4 + q] + dal[n][1] * U[BH + h][cg * 4 + q];
+      }
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int item = tid + 256 * k2;  // [8][64]
+        const int qq = item / BF, k = item % BF;
+        if ((qq & 3) != h) continue;
+        const int which = qq >> 2;  // 0: src, 1: dst
+        float s = 0.f;
+        for (int n = 0; n < NB; ++n) s += dal[n][which] * xs[n * BZP + k];
+        dU[k2] += s;
+      }
+      __syncthreads();
+    }
+  } else {
+    // dagg = do W_rel -> bufA ; dx_root = do W_root -> xs (x no longer needed)
+    zero_acc(acc);
+    mfma_rows64(acc, bufB, arow, lh, li, [&](int j, int c) { return w0[c * BF + j]; });
+    acc_to_lds(acc, bufA, wave, lh, li, 1.f);
+    zero_acc(acc);
+    mfma_rows64(acc, bufB, arow, lh, li, [&](int j, int c) { return w1[c * BF + j]; });
+    __syncthreads();
+    acc_to_lds(acc, xs, wave, lh, li, 1.f);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int n = nr0 + 16 * r;
+      if (n >= NB) continue;
+      float a[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = xs[n * BZP + cg * 4 + q];
+      for (int q = 0; q < ndeg[n]; ++q) {
+        const float4 g = *reinterpret_cast<const float4*>(bufA + nbl[n][q] * BZP + cg * 4);
+        a[0] += g.x; a[1] += g.y; a[2] += g.z; a[3] += g.w;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dxa[r][q] += a[q];
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int n = nr0 + 16 * r;
+    if (n < NB)
+      *reinterpret_cast<float4*>(dx + (node0 + n) * BF + cg * 4) =
+          make_float4(dxa[r][0], dxa[r][1], dxa[r][2], dxa[r][3]);
+  }
+  // per-workgroup partials: reduce the 16 row-groups through LDS
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[nr0][cg * 4 + q] = pb[q];
+    red[nr0][BF + cg * 4 + q] = plw[q];
+    red[nr0][2 * BF + cg * 4 + q] = plb[q];
+  }
+  __syncthreads();
+  float* pp = part + (int64_t)blockIdx.x * BPART;
+  for (int c = tid; c < 3 * BF; c += blockDim.x) {
+    float s = 0.f;
+    for (int g = 0; g < 16; ++g) s += red[g][c];
+    pp[c] = s;
+  }
+  if (kind == 0) {
+    pp[3 * BF + tid] = dU[0];
+    pp[3 * BF + 256 + tid] = dU[1];
+  }
+}
+
+// dU -> att gradients and the extra dW terms: U_q[k] = sum_c W_h[c][k] att_q[c]
+//   datt_q[c] = sum_k W_h[c][k] dU_q[k];   dW_h[c][k] += att_src_h[c] dU_h[k] + att_dst_h[c] dU_4+h[k]
+__global__ void graph_att_bwd_kernel(const float* w0, const float* att_src, const float* att_dst,
+                                     const float* dU, float* dw0, float* datt_src, float* datt_dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // [4][64][64] (h, c, k)
+  if (i < BH * BF * BF) {
+    const int h = i / (BF * BF), c = (i / BF) % BF, k = i % BF;
+    dw0[i] += att_src[h * BF + c] * dU[h * BF + k] + att_dst[h * BF + c] * dU[(BH + h) * BF + k];
+  }
+  if (i < 2 * BH * BF) {
+    const int q = i / BF, c = i % BF, h = q & 3;
+    float s = 0.f;
+    for (int k = 0; k < BF; ++k) s += w0[((int64_t)h * BF + c) * BF + k] * dU[q * BF + k];
+    (q < BH ? datt_src : datt_dst)[h * BF + c] = s;
+  }
+}
+
+__global__ void graph_att_proj_kernel2(const float* w0, const float* att_src, const float* att_dst,
+                                       float* Ug) {
+  const int q = threadIdx.x / BF, k = threadIdx.x % BF, h = q & 3;
+  const float* att = (q < BH ? att_src : att_dst) + h * BF;
+  float s = 0.f;
+  for (int c = 0; c < BF; ++c) s += w0[((int64_t)h * BF + c) * BF + k] * att[c];
+  Ug[threadIdx.x] = s;
+}
+
+}  // namespace a2m
+
+using namespace a2m;
+
+extern "C" int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t F, int32_t J,
+                                       int32_t kind, int32_t norm_res, const int32_t* nbr_ptr,
+                                       const int32_t* nbr_idx, const float* w0, const float* w1,
+                                       const float* att_src, const float* att_dst,
+                                       const float* bias, const float* ln_w, const float* ln_b,
+                                       float slope, float* dx, float* dw0, float* dw1,
+                                       float* datt_src, float* datt_dst, float* dbias,
+                                       float* dln_w, float* dln_b, void* ws, size_t ws_bytes,
+                                       void* stream) {
+  A2M_CHECK_ARG(x && dy && dx && nbr_ptr && nbr_idx && w0 && bias && dw0 && dbias,
+                "graph_layer_bwd: null pointer");
+  A2M_CHECK_ARG(J > 0 && J <= BMAXN && F > 0, "graph_layer_bwd: bad shape");
+  A2M_CHECK_ARG(kind == 0 ? (att_src && att_dst && datt_src && datt_dst) : (kind == 1 && w1 && dw1),
+                "graph_layer_bwd: bad kind / params");
+  A2M_CHECK_ARG(!norm_res || (ln_w && ln_b && dln_w && dln_b), "graph_layer_bwd: LN params");
+  const int fpb = BMAXN / J;
+  const int blocks = (int)cdiv(F, fpb);
+  const int64_t Nn = (int64_t)F * J;
+  const int yw = kind == 0 ? BH * BF : BF;
+  auto al256 = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t b_u = al256(sizeof(float) * 2 * BH * BF);
+  const size_t b_y = al256(sizeof(float) * Nn * yw);
+  const size_t b_do = al256(sizeof(float) * Nn * BF);
+  const size_t b_part = al256(sizeof(float) * (size_t)blocks * BPART);
+  const size_t b_red = al256(sizeof(float) * BPART);
+  const size_t fixed = b_u + b_y + b_do + b_part + b_red;
+  const size_t need = fixed + gemm_ws_bytes(BF, BH * BF, (int)Nn, 1) + gemm_ws_bytes(BF, BF, (int)Nn, 2);
+  if (!ws || ws_bytes < need) {
+    set_error("graph_layer_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need);
+    return A2M_EWS;
+  }
+  char* p = static_cast<char*>(ws);
+  float* Ug = reinterpret_cast<float*>(p); p += b_u;
+  float* ybuf = reinterpret_cast<float*>(p); p += b_y;
+  float* dob = reinterpret_cast<float*>(p); p += b_do;
+  float* part = reinterpret_cast<float*>(p); p += b_part;
+  float* redv = reinterpret_cast<float*>(p); p += b_red;
+  void* gws = p;
+  const size_t gbytes = ws_bytes - fixed;
+  hipStream_t st = as_stream(stream);
+  if (kind == 0) {
+    hipLaunchKernelGGL(graph_att_proj_kernel2, dim3(1), dim3(2 * BH * BF), 0, st, w0, att_src, att_dst, Ug);
+    A2M_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(graph_layer_bwd_kernel, dim3(blocks), dim3(256), 0, st, x, dy, F, J, kind, norm_res,
+                     nbr_ptr, nbr_idx, w0, w1, Ug, bias, ln_w, ln_b, slope, dx, ybuf, dob, part);
+  A2M_LAUNCH_CHECK();
+  const int cols = kind == 0 ? BPART : 3 * BF;
+  int rc = reduce_cols(part, blocks, BPART, cols, redv, 0, st);
+  if (rc) return rc;
+  A2M_CHECK_HIP(hipMemcpyAsync(dbias, redv, sizeof(float) * BF, hipMemcpyDeviceToDevice, st));
+  if (norm_res) {
+    A2M_CHECK_HIP(hipMemcpyAsync(dln_w, redv + BF, sizeof(float) * BF, hipMemcpyDeviceToDevice, st));
+    A2M_CHECK_HIP(hipMemcpyAsync(dln_b, redv + 2 * BF, sizeof(float) * BF, hipMemcpyDeviceToDevice, st));
+  }
+  // weight gradients: sum over all nodes of do (x) Y
+  if (kind == 0) {
+    // dW_h[c][k] = sum_n dout[n][c] Y[n][h*64 + k]   (batch over heads)
+    rc = gemm(dense_kr(dob, BF, 0), dense_kr(ybuf, yw, BF), epi_dense(dw0, BF, (int64_t)BF * BF), BF, BF,
+              (int)Nn, BH, gws, gbytes, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(graph_att_bwd_kernel, dim3((unsigned)cdiv(BH * BF * BF, 256)), dim3(256), 0, st, w0,
+                       att_src, att_dst, redv + 3 * BF, dw0, datt_src, datt_dst);
+    A2M_LAUNCH_CHECK();
+  } else {
+    rc = gemm(dense_kr(dob, BF), dense_kr(ybuf, BF), epi_dense(dw0, BF), BF, BF, (int)Nn, 1, gws, gbytes, st);
+    if (rc) return rc;
+    rc = gemm(dense_kr(dob, BF), dense_kr(x, BF), epi_dense(dw1, BF), BF, BF, (int)Nn, 1, gws, gbytes, st);
+    if (rc) return rc;
+  }
+  return A2M_OK;
+}

@@ -1,0 +1,415 @@
+// Training-step losses, small adjoints and the Adam update.
+//   pose losses backward   real_motion_model.py:307-461
+//   motion terms           version5_model_train.py:208-248 (L1 on motion, smoothness, jerk)
+//   MSE (adversarial)      version5_model_train.py:367, 400-403
+//   pos_to_motion          version5_model_train.py:208-213
+//   interpolate backward   model_layers.py:277
+//   Adam                   torch.optim.Adam defaults (version5_model_train.py:285-286)
+#include <algorithm>
+
+#include "a2m_internal.h"
+
+namespace a2m {
+
+__constant__ int kPar[52] = {-1, 0, 1, 2, 0, 4, 5, 0, 7, 7, 6,
+                             10, 11, 12, 13, 10, 15, 16, 17, 10, 19, 20, 21, 10, 23, 24, 25,
+                             10, 27, 28, 29, 3, 31, 32, 33, 34, 31, 36, 37, 38, 31, 40, 41,
+                             42, 31, 44, 45, 46, 31, 48, 49, 50};
+__constant__ int kHT[30][3] = {
+    {0, 1, 2}, {1, 2, 3}, {2, 3, 4}, {0, 5, 6}, {5, 6, 7}, {6, 7, 8}, {0, 9, 10}, {9, 10, 11},
+    {10, 11, 12}, {0, 13, 14}, {13, 14, 15}, {14, 15, 16}, {0, 17, 18}, {17, 18, 19}, {18, 19, 20},
+    {21, 22, 23}, {22, 23, 24}, {23, 24, 25}, {21, 26, 27}, {26, 27, 28}, {27, 28, 29},
+    {21, 30, 31}, {30, 31, 32}, {31, 32, 33}, {21, 34, 35}, {34, 35, 36}, {35, 36, 37},
+    {21, 38, 39}, {38, 39, 40}, {39, 40, 41}};
+__constant__ int kBT[5][3] = {{0, 1, 2}, {1, 2, 3}, {0, 4, 5}, {4, 5, 6}, {0, 7, 8}};
+
+constexpr float kPi = 3.14159265358979f;
+constexpr int kTC = 32;  // time steps per LDS chunk in the pose-loss backward
+
+__device__ __forceinline__ double bsum(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+// angle a = atan2(cross(u,v), dot(u,v)), u = p_j - p_a, v = p_c - p_j; dL/da = g
+__device__ __forceinline__ void angle_grad(const float* p, int a, int j, int c, float g, float* d) {
+  const float ux = p[2 * j] - p[2 * a], uy = p[2 * j + 1] - p[2 * a + 1];
+  const float vx = p[2 * c] - p[2 * j], vy = p[2 * c + 1] - p[2 * j + 1];
+  const float cr = ux * vy - uy * vx, dt = ux * vx + uy * vy;
+  const float den = cr * cr + dt * dt;
+  if (den == 0.f || g == 0.f) return;
+  const float gcr = g * dt / den, gdt = -g * cr / den;  // d atan2(y,x)/dy = x/r^2, /dx = -y/r^2
+  // cross = ux vy - uy vx ; dot = ux vx + uy vy
+  const float gux = gcr * vy + gdt * vx, guy = -gcr * vx + gdt * vy;
+  const float gvx = -gcr * uy + gdt * ux, gvy = gcr * ux + gdt * uy;
+  atomicAdd(&d[2 * j], gux - gvx);
+  atomicAdd(&d[2 * j + 1], guy - gvy);
+  atomicAdd(&d[2 * a], -gux);
+  atomicAdd(&d[2 * a + 1], -guy);
+  atomicAdd(&d[2 * c], gvx);
+  atomicAdd(&d[2 * c + 1], gvy);
+}
+
+// One workgroup per clip.  LDS accumulation (atomics on LDS within one workgroup): the
+// order of float additions into one pose coordinate varies with thread timing, within
+// ~1 ulp per term.
+__global__ __launch_bounds__(256) void pose_loss_bwd_kernel(const float* gen, int64_t gs_b,
+                                                            int64_t gs_t, const float* real,
+                                                            int64_t rs_b, int64_t rs_t, int B, int T,
+                                                            const float* grad_out, float* dgen) {
+  __shared__ float lg[51], lr[51], coef[51];
+  __shared__ float acc[kTC * 104];
+  __shared__ double red[4];
+  const int b = blockIdx.x;
+  const float gbone = real ? grad_out[0] : 0.f, gang = grad_out[1];
+  // mean bone lengths over time (as in the forward)
+  for (int i = threadIdx.x; i < 102; i += blockDim.x) {
+    const bool isr = i >= 51;
+    if (isr && !real) continue;
+    const int jb = (i % 51) + 1, pj = kPar[jb];
+    const float* base = isr ? real + b * rs_b : gen + b * gs_b;
+    const int64_t st = isr ? rs_t : gs_t;
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float* p = base + t * st;
+      const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
+      s += sqrtf(dx * dx + dy * dy);
+    }
+    (isr ? lr : lg)[i % 51] = s / (float)T;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 51; k += blockDim.x)
+    coef[k] = real ? gbone * 2.f * (lg[k] - lr[k]) / (float)(B * 51) / (float)T : 0.f;
+  __syncthreads();
+  const float gh = gang * 0.7f / (float)(B * T * 30), gb = gang * 0.3f / (float)(B * T * 5);
+  for (int t0 = 0; t0 < T; t0 += kTC) {
+    const int nt = min(kTC, T - t0);
+    for (int i = threadIdx.x; i < kTC * 104; i += blockDim.x) acc[i] = 0.f;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt * 51; i += blockDim.x) {  // bones
+      const int tt = i / 51, k = i % 51, jb = k + 1, pj = kPar[jb];
+      const float* p = gen + b * gs_b + (t0 + tt) * gs_t;
+      const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
+      const float n = sqrtf(dx * dx + dy * dy);
+      if (n == 0.f || coef[k] == 0.f) continue;
+      const float s = coef[k] / n;
+      float* a = acc + tt * 104;
+      atomicAdd(&a[2 * jb], s * dx);
+      atomicAdd(&a[2 * jb + 1], s * dy);
+      atomicAdd(&a[2 * pj], -s * dx);
+      atomicAdd(&a[2 * pj + 1], -s * dy);
+    }
+    for (int i = threadIdx.x; i < nt * 35; i += blockDim.x) {  // angle triples
+      const int tt = i / 35, q = i % 35;
+      const float* p = gen + b * gs_b + (t0 + tt) * gs_t;
+      float* a = acc + tt * 104;
+      if (q < 30) {
+        const int* tr = kHT[q];
+        const float* ph = p + 20;
+        const float ux = ph[2 * tr[1]] - ph[2 * tr[0]], uy = ph[2 * tr[1] + 1] - ph[2 * tr[0] + 1];
+        const float vx = ph[2 * tr[2]] - ph[2 * tr[1]], vy = ph[2 * tr[2] + 1] - ph[2 * tr[1] + 1];
+        const float ang = atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
+        const float g = (ang < 0.f ? -gh : 0.f) + (ang > kPi ? gh : 0.f);
+        angle_grad(ph, tr[0], tr[1], tr[2], g, a + 20);
+      } else {
+        const int* tr = kBT[q - 30];
+        const float ux = p[2 * tr[1]] - p[2 * tr[0]], uy = p[2 * tr[1] + 1] - p[2 * tr[0] + 1];
+        const float vx = p[2 * tr[2]] - p[2 * tr[1]], vy = p[2 * tr[2] + 1] - p[2 * tr[1] + 1];
+        const float ang = atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
+        const float g = (ang < -0.5f * kPi ? -gb : 0.f) + (ang > kPi ? gb : 0.f);
+        angle_grad(p, tr[0], tr[1], tr[2], g, a);
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt * 104; i += blockDim.x)
+      dgen[((int64_t)b * T + t0) * 104 + i] += acc[i];
+    __syncthreads();
+  }
+  (void)red;
+}
+
+// motion terms on [B][T][F]; one workgroup per clip, partials to part[b][3]; dfake written
+__global__ __launch_bounds__(256) void motion_terms_kernel(const float* fake, const float* real, int B,
+                                                           int T, int Fd, const float* gterms,
+                                                           float* part, float* dfake) {
+  __shared__ double red[4];
+  __shared__ float nacc[512], njerk[512];  // per-time norms (T <= 512)
+  const int b = blockIdx.x;
+  const float* fp = fake + (int64_t)b * T * Fd;
+  const float* rp = real ? real + (int64_t)b * T * Fd : nullptr;
+  auto m = [&](const float* p, int t, int f) { return p[(t + 1) * Fd + f] - p[t * Fd + f]; };
+  // L1 over motion
+  double l1 = 0.0;
+  if (rp)
+    for (int i = threadIdx.x; i < (T - 1) * Fd; i += blockDim.x) {
+      const int t = i / Fd, f = i % Fd;
+      l1 += fabsf(m(fp, t, f) - m(rp, t, f));
+    }
+  // norms of acceleration (T-2) and jerk (T-3)
+  for (int t = threadIdx.x; t < T; t += blockDim.x) {
+    float sa = 0.f, sj = 0.f;
+    if (t < T - 2)
+      for (int f = 0; f < Fd; ++f) {
+        const float a = m(fp, t + 1, f) - m(fp, t, f);
+        sa += a * a;
+      }
+    if (t < T - 3)
+      for (int f = 0; f < Fd; ++f) {
+        const float j = (m(fp, t + 2, f) - m(fp, t + 1, f)) - (m(fp, t + 1, f) - m(fp, t, f));
+        sj += j * j;
+      }
+    nacc[t] = sqrtf(sa);
+    njerk[t] = sqrtf(sj);
+  }
+  __syncthreads();
+  double sa = 0.0, sj = 0.0;
+  for (int t = threadIdx.x; t < T; t += blockDim.x) {
+    if (t < T - 2) sa += nacc[t];
+    if (t < T - 3) sj += njerk[t];
+  }
+  l1 = bsum(l1, red);
+  sa = bsum(sa, red);
+  sj = bsum(sj, red);
+  if (threadIdx.x == 0) {
+    part[3 * b] = (float)l1;
+    part[3 * b + 1] = (float)sa;
+    part[3 * b + 2] = (float)sj;
+  }
+  if (!dfake || !gterms) return;
+  // gradient w.r.t. motion m[t][f] (t < T-1), then the diff adjoint
+  const float w1 = gterms[0], ws_ = gterms[1], wj = gterms[2];
+  const float cl1 = rp ? w1 / (float)(B * (T - 1) * Fd) : 0.f;
+  const float cs = T > 2 ? ws_ / (float)(B * (T - 2)) : 0.f, cj = T > 3 ? wj / (float)(B * (T - 3)) : 0.f;
+  auto gm = [&](int t, int f) -> float {  // dL/dm[t][f]
+    float g = 0.f;
+    if (rp) {
+      const float d = m(fp, t, f) - m(rp, t, f);
+      g += cl1 * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
+    }
+    // acc[s] = m[s+1] - m[s]  (s < T-2)
+    if (t - 1 >= 0 && t - 1 < T - 2 && nacc[t - 1] > 0.f) g += cs * (m(fp, t, f) - m(fp, t - 1, f)) / nacc[t - 1];
+    if (t < T - 2 && nacc[t] > 0.f) g -= cs * (m(fp, t + 1, f) - m(fp, t, f)) / nacc[t];
+    // jerk[s] = m[s+2] - 2 m[s+1] + m[s]  (s < T-3)
+    for (int s = t - 2; s <= t; ++s) {
+      if (s < 0 || s >= T - 3 || njerk[s] == 0.f) continue;
+      const float js = m(fp, s + 2, f) - 2.f * m(fp, s + 1, f) + m(fp, s, f);
+      const float coef = (s == t) ? 1.f : (s == t - 1 ? -2.f : 1.f);
+      g += cj * coef * js / njerk[s];
+    }
+    return g;
+  };
+  for (int i = threadIdx.x; i < T * Fd; i += blockDim.x) {
+    const int t = i / Fd, f = i % Fd;
+    float g = 0.f;
+    if (t - 1 >= 0) g += gm(t - 1, f);  // pose[t] enters m[t-1] with +
+    if (t < T - 1) g -= gm(t, f);       // and m[t] with -
+    dfake[(int64_t)b * T * Fd + i] = g;
+  }
+}
+
+__global__ void terms_final_kernel(const float* part, int B, int T, int Fd, int has_real, float* terms) {
+  if (threadIdx.x != 0) return;
+  double a = 0.0, s = 0.0, j = 0.0;
+  for (int b = 0; b < B; ++b) {
+    a += part[3 * b];
+    s += part[3 * b + 1];
+    j += part[3 * b + 2];
+  }
+  terms[0] = has_real ? (float)(a / ((double)B * (T - 1) * Fd)) : 0.f;
+  terms[1] = T > 2 ? (float)(s / ((double)B * (T - 2))) : 0.f;
+  terms[2] = T > 3 ? (float)(j / ((double)B * (T - 3))) : 0.f;
+}
+
+__global__ __launch_bounds__(256) void mse_partial_kernel(const float* p, const float* t, int64_t n,
+                                                          const float* gl, float* part, float* dpred) {
+  __shared__ double red[4];
+  double s = 0.0;
+  const float g = gl ? gl[0] : 1.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float d = p[i] - t[i];
+    s += (double)d * d;
+    if (dpred) dpred[i] = g * (2.f * d / (float)n);
+  }
+  s = bsum(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = (float)s;
+}
+
+__global__ void mse_final_kernel(const float* part, int nb, int64_t n, float* loss) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < nb; ++i) s += part[i];
+  loss[0] = (float)(s / (double)n);
+}
+
+__global__ void diff_time_kernel(const float* x, int T, int Fd, int64_t total, float* y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / ((int64_t)(T - 1) * Fd);
+    const int64_t r = i - b * (T - 1) * Fd;
+    const float* xb = x + b * T * Fd;
+    y[i] = xb[r + Fd] - xb[r];
+  }
+}
+
+__global__ void diff_time_bwd_kernel(const float* dy, int T, int Fd, int64_t total, float* dx, int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / ((int64_t)T * Fd);
+    const int t = (int)((i / Fd) % T), f = (int)(i % Fd);
+    const float* g = dy + b * (T - 1) * Fd;
+    float v = 0.f;
+    if (t >= 1) v += g[(t - 1) * Fd + f];
+    if (t < T - 1) v -= g[t * Fd + f];
+    dx[i] = accumulate ? dx[i] + v : v;
+  }
+}
+
+// adjoint of interp_time_kernel (ops.hip): dx[b][c][h][w] = sum_t weight(t -> h, w) dy[b][c][t]
+__global__ void interp_time_bwd_kernel(const float* dy, int C, int H, int W, int T, int64_t total, float* dx) {
+  const float sh = (float)H / (float)T;
+  float srcw = (float)W * 0.5f - 0.5f;
+  srcw = srcw < 0.f ? 0.f : srcw;
+  const int w0 = (int)srcw;
+  const int w1 = w0 + (w0 < W - 1 ? 1 : 0);
+  const float lw1 = srcw - (float)w0, lw0 = 1.f - lw1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int w = (int)(i % W);
+    const int h = (int)((i / W) % H);
+    const int64_t bc = i / ((int64_t)H * W);
+    float wcoef = 0.f;
+    if (w == w0) wcoef += lw0;
+    if (w == w1 && lw1 != 0.f) wcoef += lw1;
+    float v = 0.f;
+    if (wcoef != 0.f) {
+      const float* g = dy + bc * T;
+      for (int t = 0; t < T; ++t) {
+        float src = sh * ((float)t + 0.5f) - 0.5f;
+        src = src < 0.f ? 0.f : src;
+        const int h0 = (int)src;
+        const int h1 = h0 + (h0 < H - 1 ? 1 : 0);
+        const float l1 = src - (float)h0, l0 = 1.f - l1;
+        float c = 0.f;
+        if (h0 == h) c += l0;
+        if (h1 == h && l1 != 0.f) c += l1;
+        v += c * g[t];
+      }
+    }
+    dx[i] = v * wcoef;
+  }
+}
+
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+                            float b2, float eps, float wd, float bc1, float bc2_sqrt) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    if (wd != 0.f) gi += wd * p[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] -= (lr / bc1) * (mi / denom);
+  }
+}
+
+}  // namespace a2m
+
+using namespace a2m;
+
+extern "C" {
+
+int a2m_pose_losses_bwd_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
+                            int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, const float* grad_out,
+                            float* dgen, void* ws, size_t ws_bytes, void* stream) {
+  (void)ws; (void)ws_bytes;
+  A2M_CHECK_ARG(gen && grad_out && dgen && B > 0 && T > 0, "pose_losses_bwd: bad args");
+  hipLaunchKernelGGL(pose_loss_bwd_kernel, dim3(B), dim3(256), 0, as_stream(stream), gen, gs_b, gs_t,
+                     real, rs_b, rs_t, B, T, grad_out, dgen);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_motion_losses_f32(const float* fake, const float* real, int32_t B, int32_t T, int32_t Fd,
+                          float* terms, const float* grad_terms, float* dfake, void* ws,
+                          size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(fake && terms && B > 0 && T > 1 && T <= 512 && Fd > 0, "motion_losses: bad args");
+  const size_t need = sizeof(float) * 3 * (size_t)B;
+  if (!ws || ws_bytes < need) { set_error("motion_losses: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
+  hipStream_t st = as_stream(stream);
+  float* part = static_cast<float*>(ws);
+  hipLaunchKernelGGL(motion_terms_kernel, dim3(B), dim3(256), 0, st, fake, real, B, T, Fd, grad_terms,
+                     part, dfake);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(terms_final_kernel, dim3(1), dim3(64), 0, st, part, B, T, Fd, real != nullptr ? 1 : 0,
+                     terms);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_mse_loss_f32(const float* pred, const float* target, int64_t n, float* loss,
+                     const float* grad_loss, float* dpred, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(pred && target && loss && n > 0, "mse_loss: bad args");
+  const int nb = (int)std::min<int64_t>(cdiv(n, 256), 256);
+  if (!ws || ws_bytes < sizeof(float) * nb) { set_error("mse_loss: workspace too small (%zu < %zu bytes)", ws_bytes, sizeof(float) * nb); return A2M_EWS; }
+  hipStream_t st = as_stream(stream);
+  float* part = static_cast<float*>(ws);
+  hipLaunchKernelGGL(mse_partial_kernel, dim3(nb), dim3(256), 0, st, pred, target, n, grad_loss, part, dpred);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mse_final_kernel, dim3(1), dim3(64), 0, st, part, nb, n, loss);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_diff_time_f32(const float* x, int32_t B, int32_t T, int32_t Fd, float* y, void* stream) {
+  A2M_CHECK_ARG(x && y && B > 0 && T > 1 && Fd > 0, "diff_time: bad args");
+  const int64_t total = (int64_t)B * (T - 1) * Fd;
+  hipLaunchKernelGGL(diff_time_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 4096)), dim3(256), 0,
+                     as_stream(stream), x, T, Fd, total, y);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_diff_time_bwd_f32(const float* dy, int32_t B, int32_t T, int32_t Fd, float* dx, int32_t accumulate,
+                          void* stream) {
+  A2M_CHECK_ARG(dy && dx && B > 0 && T > 1 && Fd > 0, "diff_time_bwd: bad args");
+  const int64_t total = (int64_t)B * T * Fd;
+  hipLaunchKernelGGL(diff_time_bwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 4096)), dim3(256),
+                     0, as_stream(stream), dy, T, Fd, total, dx, accumulate);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_interp_time_bwd_f32(const float* dy, int32_t B, int32_t C, int32_t H, int32_t W, float* dx, int32_t T,
+                            void* stream) {
+  A2M_CHECK_ARG(dy && dx && B > 0 && C > 0 && H > 0 && W > 0 && T > 0, "interp_time_bwd: bad args");
+  const int64_t total = (int64_t)B * C * H * W;
+  hipLaunchKernelGGL(interp_time_bwd_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 8192)),
+                     dim3(256), 0, as_stream(stream), dy, C, H, W, T, total, dx);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
+                 float beta1, float beta2, float eps, float weight_decay, int32_t step, void* stream) {
+  A2M_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && n >= 0 && step >= 1, "adam: bad args");
+  if (n == 0) return A2M_OK;
+  const double bc1 = 1.0 - std::pow((double)beta1, step);
+  const double bc2 = 1.0 - std::pow((double)beta2, step);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 8192)), dim3(256), 0,
+                     as_stream(stream), param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps,
+                     weight_decay, (float)bc1, (float)std::sqrt(bc2));
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,410 @@
+// Training-mode normalisation, dropout and reduction kernels.
+//
+// BatchNorm (train): ConvNormRelu applies conv -> dropout -> BN -> act (model_layers.py:118);
+// the discriminator applies conv -> BN -> LeakyReLU -> dropout (real_motion_model.py:504-551).
+// Statistics are per channel over (batch, spatial) exactly as nn.BatchNorm*d in training
+// mode: biased variance normalises, the running variance gets the unbiased one, momentum
+// 0.1.  Per-channel sums are reduced in float64 over (channel, slice) partials, so any
+// B*L fits (encoder layer 0: 131,072 elements per channel) with deterministic order.
+// Dropout masks come from a counter-based hash of (seed, logical element index) and are
+// regenerated in the backward pass rather than stored.
+#include "a2m_internal.h"
+
+namespace a2m {
+
+constexpr int kSlice = 4096;  // elements of one channel per workgroup
+
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+// keep-scale of element: 0 (dropped) or 1/(1-p)
+__device__ __forceinline__ float drop_scale(uint64_t seed, uint64_t idx, float p) {
+  if (p <= 0.f) return 1.f;
+  const float u = (float)(hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
+  return u >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+enum DropMode { DROP_NONE = 0, DROP_BEFORE = 1, DROP_BEFORE_CH = 2, DROP_AFTER = 3 };
+
+struct BNArgs {
+  const float* x; int64_t xs_b, xs_c;
+  int B, C, L, slices;
+  float p; int mode; uint64_t seed;
+};
+
+__device__ __forceinline__ float pre_drop(const BNArgs& a, int b, int c, int l) {
+  if (a.mode == DROP_BEFORE) return drop_scale(a.seed, ((uint64_t)b * a.C + c) * a.L + l, a.p);
+  if (a.mode == DROP_BEFORE_CH) return drop_scale(a.seed, (uint64_t)b * a.C + c, a.p);
+  return 1.f;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  return s;
+}
+
+// partial (sum z, sum z^2) per (channel, slice)
+__global__ __launch_bounds__(256) void bn_stats_kernel(BNArgs a, double* part) {
+  __shared__ double red[4];
+  const int c = blockIdx.x / a.slices, s = blockIdx.x % a.slices;
+  const int64_t N = (int64_t)a.B * a.L;
+  const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int b = (int)(i / a.L), l = (int)(i % a.L);
+    const float z = a.x[b * a.xs_b + c * a.xs_c + l] * pre_drop(a, b, c, l);
+    s1 += z;
+    s2 += (double)z * z;
+  }
+  s1 = block_sum_d(s1, red);
+  s2 = block_sum_d(s2, red);
+  if (threadIdx.x == 0) {
+    part[2 * ((int64_t)c * a.slices + s)] = s1;
+    part[2 * ((int64_t)c * a.slices + s) + 1] = s2;
+  }
+}
+
+__global__ void bn_finalize_kernel(const double* part, int C, int slices, int64_t N, float eps,
+                                   float momentum, float* rmean, float* rvar, float* mean_out,
+                                   float* rstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < slices; ++s) {
+    s1 += part[2 * ((int64_t)c * slices + s)];
+    s2 += part[2 * ((int64_t)c * slices + s) + 1];
+  }
+  const double mean = s1 / (double)N;
+  double var = s2 / (double)N - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  mean_out[c] = (float)mean;
+  rstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) {
+    const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+}
+
+__device__ __forceinline__ float act_fwd(float v, int act, float slope) {
+  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == ACT_LRELU) return v > 0.f ? v : v * slope;
+  return v;
+}
+
+__device__ __forceinline__ float act_grad(float pre, int act, float slope) {
+  if (act == ACT_RELU) return pre > 0.f ? 1.f : 0.f;
+  if (act == ACT_LRELU) return pre > 0.f ? 1.f : slope;
+  return 1.f;
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(BNArgs a, const float* mean, const float* rstd,
+                                                       const float* gamma, const float* beta,
+                                                       int act, float slope, float* y,
+                                                       int64_t ys_b, int64_t ys_c) {
+  const int c = blockIdx.x / a.slices, s = blockIdx.x % a.slices;
+  const int64_t N = (int64_t)a.B * a.L;
+  const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
+  const float mu = mean[c], rs = rstd[c], g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int b = (int)(i / a.L), l = (int)(i % a.L);
+    const float z = a.x[b * a.xs_b + c * a.xs_c + l] * pre_drop(a, b, c, l);
+    float v = act_fwd((z - mu) * rs * g + bt, act, slope);
+    if (a.mode == DROP_AFTER) v *= drop_scale(a.seed, ((uint64_t)b * a.C + c) * a.L + l, a.p);
+    y[b * ys_b + c * ys_c + l] = v;
+  }
+}
+
+struct BNBwdArgs {
+  BNArgs f;
+  const float* dy; int64_t dys_b, dys_c;
+  const float* mean; const float* rstd; const float* gamma; const float* beta;
+  int act; float slope;
+};
+
+// g = dL/d(bn output before act): dy * act' (* drop-after scale)
+__device__ __forceinline__ float bn_g(const BNBwdArgs& a, int b, int c, int l, float xhat) {
+  const float gm = a.gamma ? a.gamma[c] : 1.f, bt = a.beta ? a.beta[c] : 0.f;
+  float g = a.dy[b * a.dys_b + c * a.dys_c + l] * act_grad(xhat * gm + bt, a.act, a.slope);
+  if (a.f.mode == DROP_AFTER) g *= drop_scale(a.f.seed, ((uint64_t)b * a.f.C + c) * a.f.L + l, a.f.p);
+  return g;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_stats_kernel(BNBwdArgs a, double* part) {
+  __shared__ double red[4];
+  const BNArgs& f = a.f;
+  const int c = blockIdx.x / f.slices, s = blockIdx.x % f.slices;
+  const int64_t N = (int64_t)f.B * f.L;
+  const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
+  const float mu = a.mean[c], rs = a.rstd[c];
+  double sg = 0.0, sgx = 0.0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int b = (int)(i / f.L), l = (int)(i % f.L);
+    const float xhat = (f.x[b * f.xs_b + c * f.xs_c + l] * pre_drop(f, b, c, l) - mu) * rs;
+    const float g = bn_g(a, b, c, l, xhat);
+    sg += g;
+    sgx += (double)g * xhat;
+  }
+  sg = block_sum_d(sg, red);
+  sgx = block_sum_d(sgx, red);
+  if (threadIdx.x == 0) {
+    part[2 * ((int64_t)c * f.slices + s)] = sg;
+    part[2 * ((int64_t)c * f.slices + s) + 1] = sgx;
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* part, int C, int slices, float* sums,
+                                       float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int s = 0; s < slices; ++s) {
+    sg += part[2 * ((int64_t)c * slices + s)];
+    sgx += part[2 * ((int64_t)c * slices + s) + 1];
+  }
+  sums[2 * c] = (float)sg;
+  sums[2 * c + 1] = (float)sgx;
+  if (dgamma) dgamma[c] = (float)sgx;
+  if (dbeta) dbeta[c] = (float)sg;
+}
+
+// dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)); dx_raw = dz * drop-before scale;
+// partial sums of dx_raw (the conv bias gradient) per (channel, slice)
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a, const float* sums, float* dx,
+                                                           double* part) {
+  __shared__ double red[4];
+  const BNArgs& f = a.f;
+  const int c = blockIdx.x / f.slices, s = blockIdx.x % f.slices;
+  const int64_t N = (int64_t)f.B * f.L;
+  const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
+  const float mu = a.mean[c], rs = a.rstd[c], gm = a.gamma ? a.gamma[c] : 1.f;
+  const float mg = sums[2 * c] / (float)N, mgx = sums[2 * c + 1] / (float)N;
+  double sd = 0.0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int b = (int)(i / f.L), l = (int)(i % f.L);
+    const float ds = pre_drop(f, b, c, l);
+    const float xhat = (f.x[b * f.xs_b + c * f.xs_c + l] * ds - mu) * rs;
+    const float g = bn_g(a, b, c, l, xhat);
+    const float v = gm * rs * (g - mg - xhat * mgx) * ds;
+    dx[((int64_t)b * f.C + c) * f.L + l] = v;
+    sd += v;
+  }
+  sd = block_sum_d(sd, red);
+  if (threadIdx.x == 0) part[(int64_t)c * f.slices + s] = sd;
+}
+
+__global__ void reduce_slices_kernel(const double* part, int C, int slices, float* out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int k = 0; k < slices; ++k) s += part[(int64_t)c * slices + k];
+  out[c] = (float)s;
+}
+
+__global__ void dropout_kernel(const float* x, int64_t n, float p, uint64_t seed, float* y) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = x[i] * drop_scale(seed, (uint64_t)i, p);
+}
+
+// y[c] (+)= scale * sum_{b,t} x[b][c][t]; one workgroup per channel, fixed order
+__global__ __launch_bounds__(256) void sum_bt_kernel(const float* x, int64_t xs_b, int64_t xs_c,
+                                                     int64_t xs_t, int B, int T, float* y,
+                                                     int accumulate) {
+  __shared__ double red[4];
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < (int64_t)B * T; i += blockDim.x) {
+    const int b = (int)(i / T), t = (int)(i % T);
+    s += x[b * xs_b + c * xs_c + t * xs_t];
+  }
+  s = block_sum_d(s, red);
+  if (threadIdx.x == 0) y[c] = (float)(accumulate ? y[c] + s : s);
+}
+
+// LayerNorm backward over rows [R][D]; dy element (r, d) at dy + (r/T)*s_b + d*s_d + (r%T)*s_t.
+// dx = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*w; per-workgroup partials of
+// sum(dy*xhat) and sum(dy) (dw, db) reduced by reduce_cols_kernel.
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* dy, int64_t s_b, int64_t s_d,
+                                                            int64_t s_t, int T, const float* x, int R,
+                                                            int D, const float* w, const float* mean,
+                                                            const float* rstd, float* dx, float* part) {
+  extern __shared__ float lsm[];  // [4 waves][2][D] partials
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* pw = lsm + wv * 2 * D;
+  for (int d = lane; d < 2 * D; d += 64) pw[d] = 0.f;
+  const int rows_per_block = (R + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(R, r0 + rows_per_block);
+  for (int r = r0 + wv; r < r1; r += 4) {
+    const float mu = mean[r], rs = rstd[r];
+    const float* dyr = dy + (int64_t)(r / T) * s_b + (int64_t)(r % T) * s_t;
+    float g[8], xh[8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int d = lane + 64 * q;
+      if (d < D) {
+        const float dv = dyr[d * s_d];
+        xh[q] = (x[(int64_t)r * D + d] - mu) * rs;
+        g[q] = dv * w[d];
+        sg += g[q];
+        sgx += g[q] * xh[q];
+        pw[d] += dv * xh[q];
+        pw[D + d] += dv;
+      } else {
+        g[q] = xh[q] = 0.f;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      sg += __shfl_xor(sg, o);
+      sgx += __shfl_xor(sgx, o);
+    }
+    const float mg = sg / (float)D, mgx = sgx / (float)D;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int d = lane + 64 * q;
+      if (d < D) dx[(int64_t)r * D + d] = rs * (g[q] - mg - xh[q] * mgx);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < 2 * D; d += blockDim.x)
+    part[(int64_t)blockIdx.x * 2 * D + d] = lsm[d] + lsm[2 * D + d] + lsm[4 * D + d] + lsm[6 * D + d];
+}
+
+// out[j] (+)= sum_i part[i*stride + j], i < rows, j < cols (fixed order)
+__global__ void reduce_cols_kernel(const float* part, int rows, int stride, int cols, float* out,
+                                   int accumulate) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols) return;
+  double s = 0.0;
+  for (int i = 0; i < rows; ++i) s += part[(int64_t)i * stride + j];
+  out[j] = (float)(accumulate ? out[j] + s : s);
+}
+
+static int bn_slices(int64_t N) { return (int)cdiv(N, kSlice); }
+
+int reduce_cols(const float* part, int rows, int stride, int cols, float* out, int accumulate,
+                hipStream_t st) {
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(cols, 256)), dim3(256), 0, st, part,
+                     rows, stride, cols, out, accumulate);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+}  // namespace a2m
+
+using namespace a2m;
+
+extern "C" {
+
+int a2m_bn_train_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
+                         int32_t L, const float* gamma, const float* beta, float* running_mean,
+                         float* running_var, float momentum, float eps, float drop_p,
+                         int32_t drop_mode, uint64_t seed, int32_t act, float slope, float* y,
+                         int64_t ys_b, int64_t ys_c, float* save_mean, float* save_rstd,
+                         void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && y && save_mean && save_rstd && B > 0 && C > 0 && L > 0, "bn_train_fwd: bad args");
+  const int64_t N = (int64_t)B * L;
+  const int S = bn_slices(N);
+  const size_t need = sizeof(double) * 2 * (size_t)C * S;
+  if (!ws || ws_bytes < need) { set_error("bn_train_fwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
+  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  hipStream_t st = as_stream(stream);
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C, S, N,
+                     eps, momentum, running_mean, running_var, save_mean, save_rstd);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(C * S), dim3(256), 0, st, a, save_mean, save_rstd, gamma,
+                     beta, act, slope, y, ys_b, ys_c);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x,
+                         int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
+                         const float* gamma, const float* beta, const float* save_mean,
+                         const float* save_rstd, float drop_p, int32_t drop_mode, uint64_t seed,
+                         int32_t act, float slope, float* dx, float* dgamma, float* dbeta,
+                         float* dbias, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(dy && x && dx && save_mean && save_rstd && B > 0 && C > 0 && L > 0, "bn_train_bwd: bad args");
+  const int64_t N = (int64_t)B * L;
+  const int S = bn_slices(N);
+  const size_t need = sizeof(double) * 2 * (size_t)C * S + sizeof(float) * 2 * (size_t)C + 16;
+  if (!ws || ws_bytes < need) { set_error("bn_train_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
+  BNBwdArgs a;
+  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
+  a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
+  hipStream_t st = as_stream(stream);
+  double* part = static_cast<double*>(ws);
+  float* sums = reinterpret_cast<float*>(part + 2 * (size_t)C * S);
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C, S,
+                     sums, dgamma, dbeta);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(C * S), dim3(256), 0, st, a, sums, dx, part);
+  A2M_LAUNCH_CHECK();
+  if (dbias) {
+    hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C,
+                       S, dbias);
+    A2M_LAUNCH_CHECK();
+  }
+  return A2M_OK;
+}
+
+int a2m_dropout_f32(const float* x, int64_t n, float p, uint64_t seed, float* y, void* stream) {
+  A2M_CHECK_ARG(x && y && n >= 0 && p >= 0.f && p < 1.f, "dropout: bad args");
+  if (n == 0) return A2M_OK;
+  const int blocks = (int)std::min<int64_t>(cdiv(n, 256), 8192);
+  hipLaunchKernelGGL(dropout_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, n, p, seed, y);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_sum_bt_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t, int32_t B, int32_t C,
+                   int32_t T, float* y, int32_t accumulate, void* stream) {
+  A2M_CHECK_ARG(x && y && B > 0 && C > 0 && T > 0, "sum_bt: bad args");
+  hipLaunchKernelGGL(sum_bt_kernel, dim3(C), dim3(256), 0, as_stream(stream), x, xs_b, xs_c, xs_t, B,
+                     T, y, accumulate);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_layernorm_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_d, int64_t dys_t, int32_t T,
+                          const float* x, int32_t R, int32_t D, const float* w, const float* mean,
+                          const float* rstd, float* dx, float* dw, float* db, void* ws,
+                          size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(dy && x && w && mean && rstd && dx && dw && db && R > 0 && D > 0 && D <= 512,
+                "layernorm_bwd: bad args");
+  const int blocks = (int)std::min<int64_t>(cdiv(R, 16), 1024);
+  const size_t need = sizeof(float) * (size_t)blocks * 2 * D;
+  if (!ws || ws_bytes < need) { set_error("layernorm_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
+  float* part = static_cast<float*>(ws);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(blocks), dim3(256), sizeof(float) * 8 * D, st, dy,
+                     dys_b, dys_d, dys_t, T, x, R, D, w, mean, rstd, dx, part);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(D, 256)), dim3(256), 0, st, part, blocks,
+                     2 * D, D, dw, 0);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(D, 256)), dim3(256), 0, st, part + D,
+                     blocks, 2 * D, D, db, 0);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+}  // extern "C"

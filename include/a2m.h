@@ -100,11 +100,12 @@ int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t
 int a2m_interp_time_f32(const float* x, int32_t B, int32_t C, int32_t H, int32_t W,
                         float* y, int32_t T, void* stream);
 
-/* Discriminator plumbing (real_motion_model.py:599,609,620): y[b][c] = mean_t x[b][c][t]
- * and y[b][c][t] = x[b][c] (repeat over time into a strided, e.g. concatenated, buffer). */
+/* Discriminator plumbing (real_motion_model.py:599,609,620): y[b][c] = scale * mean_t x[b][c][t]
+ * and y[b][c][t] = scale * x[b][c] (repeat over time into a strided, e.g. concatenated,
+ * buffer).  Each is the other's adjoint up to the scale (used by the backward pass). */
 int a2m_mean_time_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
-                      int32_t T, float* y, void* stream);
-int a2m_repeat_time_f32(const float* x, int32_t B, int32_t C, int32_t T, float* y,
+                      int32_t T, float scale, float* y, void* stream);
+int a2m_repeat_time_f32(const float* x, int32_t B, int32_t C, int32_t T, float scale, float* y,
                         int64_t ys_b, int64_t ys_c, void* stream);
 
 /* ---------------------------------------------------------------- attention blocks
@@ -164,6 +165,120 @@ int a2m_graph_layer_fwd_f32(const float* x, int32_t F, int32_t J, int32_t kind,
 int a2m_pose_losses_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
                         int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float* out,
                         void* ws, size_t ws_bytes, void* stream);
+
+/* ================================================================ training step
+ * Forward-in-train-mode and backward entry points for the per-clip GAN step
+ * (version5_model_train.py:342-405).  Gradients are written (accumulate = 0) or added
+ * (accumulate = 1) into caller buffers; reductions are done in a fixed order. */
+
+/* BatchNorm in training mode (nn.BatchNorm1d/2d forward with batch statistics, running
+ * stats updated in place with `momentum`, unbiased running variance) fused with dropout
+ * and the activation.  x is the raw conv output, element (b, c, l) at b*xs_b + c*xs_c + l.
+ * drop_mode: 0 none, 1 element dropout before BN (ConvNormRelu 1-d, model_layers.py:118),
+ * 2 channel dropout before BN (Dropout2d, 2-d ConvNormRelu), 3 element dropout after the
+ * activation (discriminator blocks, real_motion_model.py:504-551).  Masks are a hash of
+ * (seed, element index) and are regenerated by the backward pass. */
+int a2m_bn_train_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
+                         int32_t L, const float* gamma, const float* beta, float* running_mean,
+                         float* running_var, float momentum, float eps, float drop_p,
+                         int32_t drop_mode, uint64_t seed, int32_t act, float slope, float* y,
+                         int64_t ys_b, int64_t ys_c, float* save_mean, float* save_rstd,
+                         void* ws, size_t ws_bytes, void* stream);
+/* dx (contiguous [B][C][L]) = d(loss)/d(raw conv output); dbias = sum over (b, l) of dx. */
+int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x,
+                         int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
+                         const float* gamma, const float* beta, const float* save_mean,
+                         const float* save_rstd, float drop_p, int32_t drop_mode, uint64_t seed,
+                         int32_t act, float slope, float* dx, float* dgamma, float* dbeta,
+                         float* dbias, void* ws, size_t ws_bytes, void* stream);
+/* nn.Dropout(p) with the hash mask (real_motion_model.py:203,255); backward = same call. */
+int a2m_dropout_f32(const float* x, int64_t n, float p, uint64_t seed, float* y, void* stream);
+/* y[c] (+)= sum_{b,t} x[b][c][t] (conv / linear bias gradients). */
+int a2m_sum_bt_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t, int32_t B,
+                   int32_t C, int32_t T, float* y, int32_t accumulate, void* stream);
+/* LayerNorm backward; dy in the same (permuted) layout the forward wrote. */
+int a2m_layernorm_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_d, int64_t dys_t,
+                          int32_t T, const float* x, int32_t R, int32_t D, const float* w,
+                          const float* mean, const float* rstd, float* dx, float* dw, float* db,
+                          void* ws, size_t ws_bytes, void* stream);
+
+/* Conv2d / Conv1d (H = kh = 1) backward.  dgrad: dy contiguous [B][Co][Ho][Wo] ->
+ * dx (strided) by output-phase decomposed implicit GEMMs (also ConvTranspose1d's forward
+ * algebra); wgrad: dw [Co][Ci][kh][kw] = sum dy (x) im2col(x). */
+int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int32_t Wo,
+                         const float* w, int32_t Ci, int32_t H, int32_t W, int32_t kh, int32_t kw,
+                         int32_t stride_h, int32_t stride_w, int32_t pad_h, int32_t pad_w,
+                         float* dx, int64_t dxs_b, int64_t dxs_c, int64_t dxs_h, int64_t dxs_w,
+                         int32_t accumulate, void* ws, size_t ws_bytes, void* stream);
+int a2m_conv2d_wgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int32_t Wo,
+                         const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_h, int64_t xs_w,
+                         int32_t Ci, int32_t H, int32_t W, int32_t kh, int32_t kw,
+                         int32_t stride_h, int32_t stride_w, int32_t pad_h, int32_t pad_w,
+                         float* dw, int32_t accumulate, void* ws, size_t ws_bytes, void* stream);
+
+/* SelfAttention / ChannelAttention backward (inputs: the forward's saved qkv / attention). */
+size_t a2m_self_attention_bwd_ws_bytes(int32_t B, int32_t C, int32_t T);
+int a2m_self_attention_bwd_f32(const float* dy, const float* x, int64_t bs, int32_t B, int32_t C,
+                               int32_t T, const float* wq, const float* bq, const float* wk,
+                               const float* bk, const float* wv, const float* bv,
+                               const float* gamma, const float* qkv, const float* attn, float* dx,
+                               float* dwq, float* dbq, float* dwk, float* dbk, float* dwv,
+                               float* dbv, float* dgamma, void* ws, size_t ws_bytes, void* stream);
+int a2m_channel_attention_bwd_f32(const float* dy, const float* x, int32_t B, int32_t C, int32_t T,
+                                  const float* w1, const float* b1, int32_t Cr, const float* w2,
+                                  const float* b2, float* dx, float* dw1, float* db1, float* dw2,
+                                  float* db2, void* ws, size_t ws_bytes, void* stream);
+
+/* Skeleton graph layer backward (recomputes the forward from x). */
+int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t F, int32_t J, int32_t kind,
+                            int32_t norm_res, const int32_t* nbr_ptr, const int32_t* nbr_idx,
+                            const float* w0, const float* w1, const float* att_src,
+                            const float* att_dst, const float* bias, const float* ln_w,
+                            const float* ln_b, float slope, float* dx, float* dw0, float* dw1,
+                            float* datt_src, float* datt_dst, float* dbias, float* dln_w,
+                            float* dln_b, void* ws, size_t ws_bytes, void* stream);
+
+/* F.interpolate (time) backward: dx [B][C][H][W] (zeros where the forward read nothing). */
+int a2m_interp_time_bwd_f32(const float* dy, int32_t B, int32_t C, int32_t H, int32_t W,
+                            float* dx, int32_t T, void* stream);
+
+/* Losses of the G / D steps (version5_model_train.py:208-248, 367-403). */
+int a2m_pose_losses_bwd_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
+                            int64_t rs_b, int64_t rs_t, int32_t B, int32_t T,
+                            const float* grad_out, float* dgen, void* ws, size_t ws_bytes,
+                            void* stream);
+/* terms = [L1(diff(real), diff(fake)), mean||accel||, mean||jerk||] on [B][T][Fd] (contiguous).
+ * If grad_terms (device [3], the incoming dL/dterms) and dfake are given, also
+ * dfake = sum_i grad_terms[i] * dterms[i]/dfake (overwritten). */
+int a2m_motion_losses_f32(const float* fake, const float* real, int32_t B, int32_t T, int32_t Fd,
+                          float* terms, const float* grad_terms, float* dfake, void* ws,
+                          size_t ws_bytes, void* stream);
+/* loss = mean (pred - target)^2; dpred (optional) = grad_loss[0] * 2 (pred - target) / n
+ * (grad_loss: device scalar, NULL = 1). */
+int a2m_mse_loss_f32(const float* pred, const float* target, int64_t n, float* loss,
+                     const float* grad_loss, float* dpred, void* ws, size_t ws_bytes, void* stream);
+/* pos_to_motion (version5_model_train.py:208): y[b][t] = x[b][t+1] - x[b][t], and its adjoint. */
+int a2m_diff_time_f32(const float* x, int32_t B, int32_t T, int32_t Fd, float* y, void* stream);
+int a2m_diff_time_bwd_f32(const float* dy, int32_t B, int32_t T, int32_t Fd, float* dx,
+                          int32_t accumulate, void* stream);
+
+/* General strided GEMM on the same MFMA engine (linear layers' backward, 1x1 projections):
+ *   C[m][n] (+)= alpha * sum_k A(m,k) B(n,k) (+ bias[m]), per batch z < batch
+ *   n = n0*N1 + n1, k = k0*K1 + k1 (two-level index spaces cover [B][C][T] row sets)
+ *   A(m,k) = A[z*a_bs + m*a_m + k0*a_k0 + k1*a_k1]
+ *   B(n,k) = B[z*b_bs + n0*b_n0 + n1*b_n1 + k0*b_k0 + k1*b_k1]
+ *   C(m,n) = C[z*c_bs + m*c_m + n0*c_n0 + n1*c_n1]                                        */
+int a2m_gemm_f32(int32_t M, int32_t N, int32_t N1, int32_t K, int32_t K1, int32_t batch,
+                 const float* A, int64_t a_bs, int64_t a_m, int64_t a_k0, int64_t a_k1,
+                 const float* B, int64_t b_bs, int64_t b_n0, int64_t b_n1, int64_t b_k0,
+                 int64_t b_k1, float* C, int64_t c_bs, int64_t c_m, int64_t c_n0, int64_t c_n1,
+                 const float* bias, float alpha, int32_t accumulate, void* ws, size_t ws_bytes,
+                 void* stream);
+
+/* torch.optim.Adam step (no weight decay by default, no amsgrad) over a flat buffer. */
+int a2m_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                 float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
+                 void* stream);
 
 #ifdef __cplusplus
 }

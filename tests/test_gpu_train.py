@@ -1,0 +1,355 @@
+"""GPU parity of the training path: every autograd Function (HIP forward + HIP backward)
+against torch-CPU fp32 autograd of the same op, then one full G-step + D-step against the
+reference's own gradients (tests/golden/train_step_b2t64.npz, produced by running
+version5_model_train.py's step math on the reference modules)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as TF
+
+from conftest import golden, rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+TOL = 1e-4
+GTOL = 2e-4   # gradients: deeper fp32 chains, relative to max |ref|
+
+
+def _r(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).float()
+
+
+def _leaf(t):
+    return t.clone().to(DEV).requires_grad_(True), t.clone().requires_grad_(True)
+
+
+def _check_grads(pairs, tol=GTOL):
+    for name, (gd, gc) in pairs.items():
+        assert gd is not None and gc is not None, name
+        assert rel_err(gd.detach().cpu(), gc.detach()) < tol, (name, rel_err(gd.detach().cpu(), gc.detach()))
+
+
+@pytest.mark.parametrize('two_d', [False, True])
+def test_conv_norm_act_train(two_d):
+    from a2m.model_layers import ConvNormRelu
+    torch.manual_seed(0)
+    if two_d:
+        m = ConvNormRelu(3, 8, type='2d', leaky=True, downsample=True)
+        x = _r(4, 3, 12, 20, seed=1)
+    else:
+        m = ConvNormRelu(6, 10, type='1d', leaky=True, downsample=True)
+        x = _r(3, 6, 17, seed=1)
+    ref = ConvNormRelu(*(3, 8) if two_d else (6, 10), type='2d' if two_d else '1d', leaky=True, downsample=True)
+    ref.load_state_dict(m.state_dict())
+    with torch.no_grad():
+        m.norm.running_var.fill_(1.3)
+        ref.norm.running_var.fill_(1.3)
+    m.to(DEV).train()
+    ref.train()
+    xd, xc = _leaf(x)
+    yd = m(xd)
+    conv = TF.conv2d if two_d else TF.conv1d
+    yc = TF.leaky_relu(TF.batch_norm(conv(xc, ref.conv.weight, ref.conv.bias, stride=2, padding=1),
+                                     ref.norm.running_mean, ref.norm.running_var, ref.norm.weight,
+                                     ref.norm.bias, True, 0.1, 1e-5), 0.2)
+    assert rel_err(yd.detach().cpu(), yc.detach()) < TOL
+    assert rel_err(m.norm.running_mean.cpu(), ref.norm.running_mean) < TOL
+    assert rel_err(m.norm.running_var.cpu(), ref.norm.running_var) < TOL
+    gy = _r(*yc.shape, seed=2)
+    yd.backward(gy.to(DEV))
+    yc.backward(gy)
+    _check_grads({'x': (xd.grad, xc.grad), 'w': (m.conv.weight.grad, ref.conv.weight.grad),
+                  'gamma': (m.norm.weight.grad, ref.norm.weight.grad),
+                  'beta': (m.norm.bias.grad, ref.norm.bias.grad)})
+
+
+def test_convt_bn_relu_train():
+    from a2m.model_layers import ConvTranspose1D
+    torch.manual_seed(0)
+    m = ConvTranspose1D(12, 7)
+    ref = ConvTranspose1D(12, 7)
+    ref.load_state_dict(m.state_dict())
+    m.to(DEV).train()
+    ref.train()
+    xd, xc = _leaf(_r(3, 12, 9, seed=3))
+    yd, yc = m(xd), ref(xc)
+    assert rel_err(yd.detach().cpu(), yc.detach()) < TOL
+    gy = _r(*yc.shape, seed=4)
+    yd.backward(gy.to(DEV))
+    yc.backward(gy)
+    _check_grads({'x': (xd.grad, xc.grad), 'w': (m.conv_transpose.weight.grad, ref.conv_transpose.weight.grad),
+                  'b': (m.bn.weight.grad, ref.bn.weight.grad)})
+
+
+@pytest.mark.parametrize('C,T,res', [(64, 16, False), (256, 64, True), (16, 5, True)])
+def test_self_attention_train(C, T, res):
+    from a2m.model_layers import SelfAttention
+    from oracle import model as OM
+    torch.manual_seed(1)
+    m = SelfAttention(C)
+    with torch.no_grad():
+        m.gamma.fill_(0.4)
+    sd = {'a.' + k: v.clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    m.to(DEV).train()
+    xd, xc = _leaf(_r(2, C, T, seed=5))
+    rd, rc = _leaf(_r(2, C, T, seed=6)) if res else (None, None)
+    yd = m(xd, res=rd)
+    yc = OM.self_attention(OM.Ctx(sd), 'a', xc) + (rc if res else 0)
+    assert rel_err(yd.detach().cpu(), yc.detach()) < TOL
+    gy = _r(2, C, T, seed=7)
+    yd.backward(gy.to(DEV))
+    yc.backward(gy)
+    pairs = {'x': (xd.grad, xc.grad), 'gamma': (m.gamma.grad, sd['a.gamma'].grad)}
+    for k in ('query_conv', 'key_conv', 'value_conv'):
+        pairs[k + '.w'] = (getattr(m, k).weight.grad, sd[f'a.{k}.weight'].grad)
+    pairs['value_conv.b'] = (m.value_conv.bias.grad, sd['a.value_conv.bias'].grad)
+    pairs['query_conv.b'] = (m.query_conv.bias.grad, sd['a.query_conv.bias'].grad)
+    if res:
+        pairs['res'] = (rd.grad, rc.grad)
+    _check_grads(pairs)
+
+
+def test_channel_attention_train():
+    from a2m.model_layers import ChannelAttention
+    from oracle import model as OM
+    torch.manual_seed(2)
+    m = ChannelAttention(64)
+    sd = {'c.' + k: v.clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    m.to(DEV).train()
+    xd, xc = _leaf(_r(3, 64, 20, seed=8))
+    yd, yc = m(xd), OM.channel_attention(OM.Ctx(sd), 'c', xc)
+    assert rel_err(yd.detach().cpu(), yc.detach()) < TOL
+    gy = _r(3, 64, 20, seed=9)
+    yd.backward(gy.to(DEV))
+    yc.backward(gy)
+    _check_grads({'x': (xd.grad, xc.grad), 'w1': (m.fc[0].weight.grad, sd['c.fc.0.weight'].grad),
+                  'b1': (m.fc[0].bias.grad, sd['c.fc.0.bias'].grad),
+                  'w2': (m.fc[2].weight.grad, sd['c.fc.2.weight'].grad),
+                  'b2': (m.fc[2].bias.grad, sd['c.fc.2.bias'].grad)})
+
+
+@pytest.mark.parametrize('kind,J,lo,norm_res', [(0, 10, 0, True), (0, 42, 10, True), (1, 42, 10, True),
+                                                (1, 10, 0, True), (0, 42, 10, False)])
+def test_graph_layer_train(kind, J, lo, norm_res):
+    from a2m import autograd as AG
+    from a2m import skeleton as S
+    from oracle import model as OM
+    Fr = 7
+    ei = S.edge_index(lo, J)
+    ptr, idx = [t.to(DEV) for t in S.in_neighbour_csr(ei, J)]
+    edges = OM.expand_edges(ei, J, Fr)
+    x = _r(Fr * J, 64, seed=10)
+    if kind == 0:
+        params = [_r(256, 64, seed=11, scale=0.15), None, _r(1, 4, 64, seed=12, scale=0.3),
+                  _r(1, 4, 64, seed=13, scale=0.3), _r(64, seed=14, scale=0.1)]
+    else:
+        params = [_r(64, 64, seed=15, scale=0.12), _r(64, 64, seed=16, scale=0.12), None, None,
+                  _r(64, seed=17, scale=0.1)]
+    lnw, lnb = (_r(64, seed=18).abs() + 0.5, _r(64, seed=19, scale=0.1)) if norm_res else (None, None)
+    allp = params + [lnw, lnb]
+    dev_p = [p.clone().to(DEV).requires_grad_(True) if p is not None else None for p in allp]
+    cpu_p = [p.clone().requires_grad_(True) if p is not None else None for p in allp]
+    xd, xc = _leaf(x)
+    yd = AG._GraphLayer.apply(xd, *dev_p, (J, kind, ptr, idx, norm_res))
+    w0, w1, a_s, a_d, b, lw, lb = cpu_p
+    if kind == 0:
+        g = OM._gat_fn(xc, edges, w0, a_s, a_d, b, 4)
+    else:
+        g = OM.graph_conv(OM.Ctx({'g.lin_rel.weight': w0, 'g.lin_rel.bias': b, 'g.lin_root.weight': w1}), 'g',
+                          xc, edges)
+    yc = TF.leaky_relu(TF.layer_norm(g, (64,), lw, lb), 0.2) + xc if norm_res else g
+    assert rel_err(yd.detach().cpu(), yc.detach()) < TOL
+    gy = _r(*yc.shape, seed=20)
+    yd.backward(gy.to(DEV))
+    yc.backward(gy)
+    pairs = {'x': (xd.grad, xc.grad)}
+    for i, name in enumerate(['w0', 'w1', 'att_src', 'att_dst', 'bias', 'ln_w', 'ln_b']):
+        if cpu_p[i] is not None:
+            pairs[name] = (dev_p[i].grad, cpu_p[i].grad)
+    _check_grads(pairs)
+
+
+def test_linear_projin_layernorm_train():
+    from a2m import autograd as AG
+    x = _r(3, 32, 10, seed=21)
+    w, b = _r(40, 32, seed=22, scale=0.2), _r(40, seed=23)
+    xd, xc = _leaf(x)
+    wd, wc = _leaf(w)
+    bd, bc = _leaf(b)
+    yd = AG._ProjIn.apply(xd, wd, bd)
+    yc = TF.linear(xc.permute(0, 2, 1), wc, bc).reshape(30, 40)
+    assert rel_err(yd.detach().cpu(), yc.detach()) < TOL
+    lw, lb = _r(40, seed=24).abs() + .5, _r(40, seed=25)
+    lwd, lwc = _leaf(lw)
+    lbd, lbc = _leaf(lb)
+    w2, b2 = _r(40, 40, seed=26, scale=0.2), _r(40, seed=27)
+    w2d, w2c = _leaf(w2)
+    b2d, b2c = _leaf(b2)
+    zd = AG._LayerNormBCT.apply(AG.linear(yd, w2d, b2d), lwd, lbd, 10)
+    zc = TF.layer_norm(TF.linear(yc, w2c, b2c), (40,), lwc, lbc).view(3, 10, 40).permute(0, 2, 1)
+    assert rel_err(zd.detach().cpu(), zc.detach()) < TOL
+    gz = _r(3, 40, 10, seed=28)
+    zd.backward(gz.to(DEV))
+    zc.backward(gz)
+    _check_grads({'x': (xd.grad, xc.grad), 'w': (wd.grad, wc.grad), 'b': (bd.grad, bc.grad),
+                  'w2': (w2d.grad, w2c.grad), 'b2': (b2d.grad, b2c.grad), 'lw': (lwd.grad, lwc.grad),
+                  'lb': (lbd.grad, lbc.grad)})
+
+
+def test_losses_and_plumbing_train():
+    from a2m import autograd as AG
+    from oracle import model as OM
+    z = golden('losses.npz')
+    gd, gc = _leaf(torch.from_numpy(z['gen']))
+    real = torch.from_numpy(z['real'])
+    ld = AG._PoseLosses.apply(gd, real.to(DEV))
+    lc = torch.stack([OM.bone_length_loss(real, gc), OM.angle_loss(gc)])
+    assert rel_err(ld.detach().cpu(), lc.detach()) < TOL
+    w = torch.tensor([0.7, 1.3])
+    (ld * w.to(DEV)).sum().backward()
+    (lc * w).sum().backward()
+    _check_grads({'gen': (gd.grad, gc.grad)})
+    # motion terms + MSE + diff
+    fd, fc = _leaf(_r(3, 9, 104, seed=30))
+    rp = _r(3, 9, 104, seed=31)
+    td = AG.motion_terms(fd, rp.to(DEV))
+    tc = torch.stack(OM.motion_terms(rp, fc))
+    assert rel_err(td.detach().cpu(), tc.detach()) < TOL
+    md = AG.pos_to_motion(fd)
+    mc = torch.diff(fc, dim=1)
+    tgt = _r(3, 8, 104, seed=32)
+    sd_ = td[0] + 0.1 * td[1] + 0.05 * td[2] + AG.mse_loss(md, tgt.to(DEV))
+    sc_ = tc[0] + 0.1 * tc[1] + 0.05 * tc[2] + TF.mse_loss(mc, tgt)
+    assert rel_err(sd_.detach().cpu(), sc_.detach()) < TOL
+    sd_.backward()
+    sc_.backward()
+    _check_grads({'fake': (fd.grad, fc.grad)})
+    # interp / mean / repeat
+    hd, hc = _leaf(_r(2, 6, 8, 15, seed=33))
+    od = AG._InterpTime.apply(hd, 64)
+    oc = TF.interpolate(hc, size=(64, 1), mode='bilinear').squeeze(-1)
+    assert rel_err(od.detach().cpu(), oc.detach()) < TOL
+    go = _r(2, 6, 64, seed=34)
+    od.backward(go.to(DEV))
+    oc.backward(go)
+    _check_grads({'interp': (hd.grad, hc.grad)})
+    ad, ac = _leaf(_r(2, 6, 5, seed=35))
+    ed = AG._RepeatTime.apply(AG._MeanTime.apply(ad) * 2.0, 5)
+    ec = (ac.mean(2) * 2.0).unsqueeze(2).repeat(1, 1, 5)
+    ge = _r(2, 6, 5, seed=36)
+    ed.backward(ge.to(DEV))
+    ec.backward(ge)
+    _check_grads({'mean/repeat': (ad.grad, ac.grad)})
+
+
+def test_adam_matches_torch():
+    from a2m.optim import FlatAdam
+    ps = [torch.nn.Parameter(_r(7, 5, seed=40)), torch.nn.Parameter(_r(11, seed=41))]
+    pd = [torch.nn.Parameter(p.detach().clone().to(DEV)) for p in ps]
+    ref = torch.optim.Adam(ps, lr=1e-3)
+    opt = FlatAdam(pd, lr=1e-3)
+    for step in range(3):
+        grads = [_r(*p.shape, seed=50 + step * 2 + i) for i, p in enumerate(ps)]
+        ref.zero_grad()
+        opt.zero_grad()
+        for p, q, g in zip(ps, pd, grads):
+            p.grad = g.clone()
+            q.grad.copy_(g.to(DEV))
+        ref.step()
+        opt.step()
+    for p, q in zip(ps, pd):
+        assert rel_err(q.detach().cpu(), p.detach()) < 1e-6
+
+
+def test_dropout_mask_statistics():
+    from a2m import functional as F
+    x = torch.ones(1 << 20, device=DEV)
+    y = F.dropout(x, 0.2, 1234)
+    keep = (y != 0).float().mean().item()
+    assert abs(keep - 0.8) < 0.005
+    assert torch.allclose(y[y != 0], torch.full_like(y[y != 0], 1.25))
+    assert torch.equal(F.dropout(x, 0.2, 1234), y) and not torch.equal(F.dropout(x, 0.2, 99), y)
+
+
+def _bn_cancelled(name):
+    import re
+    return name.endswith(('.conv.bias', '.conv_transpose.bias', '.key_conv.bias')) or \
+        re.fullmatch(r'conv[123](\.\d)?\.(0|4|9)\.bias', name) is not None
+
+
+def _grad_check_vs_golden(module, t, prefix):
+    bad = []
+    for i, n in enumerate(t[f'{prefix}_names']):
+        if _bn_cancelled(n):
+            continue
+        p = dict(module.named_parameters())[n]
+        g = p.grad.detach().double().reshape(-1).cpu().numpy()
+        ix = t[f'{prefix}_idx'][i]
+        ok = ix >= 0
+        ref = t[f'{prefix}_val'][i][ok]
+        scale = max(np.sqrt(t[f'{prefix}_sumsq'][i] / max(g.size, 1)), np.abs(ref).max(), 1e-12)
+        err = np.abs(g[ix[ok]] - ref).max() / scale
+        if err > 2e-3:
+            bad.append((n, err))
+    assert not bad, bad[:10]
+
+
+def test_train_step_vs_reference(g_state, d_state):
+    """One G-step (G + D forward in train mode, all G losses, backward) and one D-step, p=0,
+    fixed labels, against the reference's outputs and sampled gradients."""
+    from a2m import autograd as AG
+    from a2m.real_motion_model import SelfAttention_D, SelfAttention_G
+    z = golden('g_eval_b2t64.npz')
+    t = golden('train_step_b2t64.npz')
+    g = SelfAttention_G(p=0.0)
+    g.load_state_dict(g_state, strict=False)
+    d = SelfAttention_D(out_channels=64, p=0.0)
+    d.load_state_dict(d_state, strict=False)
+    g, d = g.to(DEV).train(), d.to(DEV).train()
+    audio = torch.from_numpy(z['audio']).to(DEV)
+    pose = torch.from_numpy(z['real_pose']).to(DEV)
+    fake_pose, internal = g(audio, real_pose=pose)
+    assert rel_err(fake_pose.detach().cpu(), t['fake_pose']) < TOL
+    fake_d, _ = d(AG.pos_to_motion(fake_pose))
+    assert rel_err(fake_d.detach().cpu(), t['fake_d']) < TOL
+    terms = AG.motion_terms(fake_pose, pose)
+    loss = terms[0] + AG.mse_loss(fake_d, torch.full((2, 4), 0.93, device=DEV)) + 0.1 * terms[1] + \
+        0.05 * terms[2] + internal[0] + internal[1]
+    parts = torch.stack([terms[0], AG.mse_loss(fake_d, torch.full((2, 4), 0.93, device=DEV)), terms[1], terms[2],
+                         internal[0], internal[1]]).detach().cpu().numpy()
+    assert np.abs(parts - t['parts']).max() / np.abs(t['parts']).max() < TOL
+    assert rel_err(loss.detach().cpu(), t['G_loss']) < TOL
+    loss.backward()
+    _grad_check_vs_golden(g, t, 'gG')
+    d.zero_grad()
+    with torch.no_grad():
+        fp2, _ = g(audio)
+    fd2, _ = d(AG.pos_to_motion(fp2))
+    rd2, _ = d(AG.pos_to_motion(pose))
+    dl = AG.mse_loss(rd2, torch.full((2, 4), 0.93, device=DEV)) + AG.mse_loss(fd2, torch.full((2, 4), 0.07, device=DEV))
+    assert rel_err(fd2.detach().cpu(), t['d_fake']) < TOL and rel_err(rd2.detach().cpu(), t['d_real']) < TOL
+    assert rel_err(dl.detach().cpu(), t['D_loss']) < TOL
+    dl.backward()
+    _grad_check_vs_golden(d, t, 'gD')
+
+
+def test_trainer_iteration_runs_and_learns():
+    """GANTrainer: g_freq=3, d_freq=1 with dropout on; losses finite, parameters move."""
+    from a2m.real_motion_model import SelfAttention_D, SelfAttention_G
+    from a2m.training import GANTrainer
+    from oracle import synth
+    from a2m.mel_features import log_mel_batch
+    torch.manual_seed(0)
+    g = SelfAttention_G(p=0.2).to(DEV).train()
+    d = SelfAttention_D(out_channels=64).to(DEV).train()
+    tr = GANTrainer(g, d, lr=1e-4)
+    wav = torch.from_numpy(synth.speech_like(4, synth.samples_for_frames(64), seed=2)).to(DEV)
+    with torch.no_grad():
+        audio = log_mel_batch(wav)
+    pose = torch.from_numpy(synth.pose_targets(4, 64, seed=3)).to(DEV)
+    w0 = g.unet.final_conv.weight.detach().clone()
+    dl, gl = tr.iteration(audio, pose, epoch=0, g_freq=3, d_freq=1)
+    assert torch.isfinite(dl) and torch.isfinite(gl)
+    assert not torch.equal(w0, g.unet.final_conv.weight.detach())
+    assert len(tr.dyn.d_loss_history) == 1
