@@ -12,7 +12,7 @@ from . import _native as N
 
 ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
 
-_NULL = None
+_native_lib = N.lib
 
 
 def _p(t):
@@ -395,9 +395,10 @@ def gemm(M, N, K, A, a_m, a_k, B, b_n, b_k, C, c_m, c_n, N1=1, K1=1, batch=1, a_
     bk0, bk1 = b_k if isinstance(b_k, tuple) else (b_k, 0)
     bn0, bn1 = b_n if isinstance(b_n, tuple) else (b_n, 0)
     cn0, cn1 = c_n if isinstance(c_n, tuple) else (c_n, 0)
-    _with_ws(C.device, lambda wp, wn: N.lib.a2m_gemm_f32(
-        M, N, N1, K, K1, batch, _p(A), a_bs, a_m, ak0, ak1, _p(B), b_bs, bn0, bn1, bk0, bk1, _p(C), c_bs,
-        c_m, cn0, cn1, _p(bias), 1.0, int(accumulate), wp, wn, _stream()))
+    lib, n_cols = _native_lib, N  # the argument N shadows the module alias
+    _with_ws(C.device, lambda wp, wn: lib.a2m_gemm_f32(
+        M, n_cols, N1, K, K1, batch, _p(A), a_bs, a_m, ak0, ak1, _p(B), b_bs, bn0, bn1, bk0, bk1, _p(C),
+        c_bs, c_m, cn0, cn1, _p(bias), 1.0, int(accumulate), wp, wn, _stream()))
     return C
 
 
