@@ -557,3 +557,23 @@ def adam_(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
     _check_dev(param, grad, exp_avg, exp_avg_sq)
     N.check(N.lib.a2m_adam_f32(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), lr, beta1,
                                beta2, eps, weight_decay, step, _stream()))
+
+
+class gemm_timing:
+    """Context manager: HIP-event timing of every implicit-GEMM launch issued inside it
+    (a2m_gemm_timing_begin/_end).  After exit: .launches, .flops, .ms_tile, .ms_reduce,
+    .reduces.  Eager code only (events are not graph-capturable)."""
+
+    def __enter__(self):
+        N.check(N.lib.a2m_gemm_timing_begin())
+        return self
+
+    def __exit__(self, *exc):
+        import ctypes
+        n, r = ctypes.c_int64(), ctypes.c_int64()
+        f, mt, mr = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        N.check(N.lib.a2m_gemm_timing_end(ctypes.byref(n), ctypes.byref(f), ctypes.byref(mt),
+                                          ctypes.byref(mr), ctypes.byref(r)))
+        self.launches, self.flops, self.ms_tile = n.value, f.value, mt.value
+        self.ms_reduce, self.reduces = mr.value, r.value
+        return False

@@ -31,6 +31,22 @@ class _GraphTopology(nn.Module):
     def topology(self, part):
         return getattr(self, f'_{part}_nbr_ptr'), getattr(self, f'_{part}_nbr_idx')
 
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        # A checkpoint's template must hold the skeleton's edges (real_motion_model.py:43-60, any
+        # order): the kernels' neighbour CSR is derived from them once, at construction.
+        for part in ('body', 'hand'):
+            key = f'{prefix}{part}_edge_index_template'
+            if key in state_dict:
+                mine = getattr(self, f'{part}_edge_index_template')
+                theirs = state_dict[key]
+                same = tuple(theirs.shape) == tuple(mine.shape) and \
+                    sorted(map(tuple, theirs.cpu().long().t().tolist())) == sorted(map(tuple, mine.cpu().t().tolist()))
+                if not same:
+                    error_msgs.append(f'{key}: checkpoint edge template differs from the Skeleton2D topology')
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
+
 
 class SelfAttention_G(_GraphTopology):
     def __init__(self, time_steps=64, in_channels=256, out_channels=256, out_feats=104, p=0.2):

@@ -13,6 +13,8 @@
 // barrier per K-step suffices.  Split-K writes fp32 partial slabs to a workspace that a
 // second kernel reduces in a fixed order (bitwise reproducible) and runs the epilogue on.
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #include "a2m_internal.h"
 
@@ -371,6 +373,43 @@ static void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_
 #undef A2M_L
 }
 
+// Optional per-launch timing of the engine (bench.py's live roofline): HIP events recorded on
+// the launch stream around the tile kernel and the split-K reduce.  Off by default; not for
+// use inside graph capture.
+struct GemmTiming {
+  hipEvent_t e0, e1, e2;
+  double flops;
+  bool reduce;
+};
+static std::mutex g_timing_mu;
+static bool g_timing = false;
+static std::vector<GemmTiming> g_timing_recs;
+
+static long timing_open(double flops, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  if (!g_timing) return -1;
+  GemmTiming t{};
+  t.flops = flops;
+  if (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess ||
+      hipEventCreate(&t.e2) != hipSuccess)
+    return -1;
+  (void)hipEventRecord(t.e0, st);
+  g_timing_recs.push_back(t);
+  return (long)g_timing_recs.size() - 1;
+}
+
+static void timing_mark(long i, int which, bool reduce, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  if (i < 0 || i >= (long)g_timing_recs.size()) return;
+  GemmTiming& t = g_timing_recs[i];
+  if (which == 1) {
+    (void)hipEventRecord(t.e1, st);
+  } else {
+    t.reduce = reduce;
+    (void)hipEventRecord(t.e2, st);
+  }
+}
+
 int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int K, int batch,
          void* ws, size_t ws_bytes, hipStream_t stream, int force_split) {
   A2M_CHECK_ARG(M > 0 && N > 0 && K >= 0 && batch > 0, "gemm: bad sizes M=%d N=%d K=%d batch=%d",
@@ -395,16 +434,65 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     a.partial = static_cast<float*>(ws);
   }
   const int ma = operand_mode(A, K), mb = operand_mode(B, K);
+  const long tm = g_timing ? timing_open(2.0 * M * N * (double)K * batch, stream) : -1;
   if (p.bm == 128) launch_tile<128, 128>(a, ma, mb, batch, stream);
   else launch_tile<64, 64>(a, ma, mb, batch, stream);
   A2M_LAUNCH_CHECK();
+  if (tm >= 0) timing_mark(tm, 1, false, stream);
   if (p.splits > 1) {
     const int64_t total = (int64_t)M * N * batch;
     const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, a, batch);
     A2M_LAUNCH_CHECK();
   }
+  if (tm >= 0) timing_mark(tm, 2, p.splits > 1, stream);
   return A2M_OK;
 }
+
+}  // namespace a2m
+
+extern "C" {
+
+int a2m_gemm_timing_begin(void) {
+  std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+  a2m::g_timing_recs.clear();
+  a2m::g_timing = true;
+  return A2M_OK;
+}
+
+int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
+                        int64_t* reduces) {
+  std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+  a2m::g_timing = false;
+  int64_t n = 0, nr = 0;
+  double f = 0, mt = 0, mr = 0;
+  int rc = A2M_OK;
+  for (auto& t : a2m::g_timing_recs) {
+    float a = 0.f, b = 0.f;
+    if (hipEventSynchronize(t.e2) != hipSuccess || hipEventElapsedTime(&a, t.e0, t.e1) != hipSuccess ||
+        hipEventElapsedTime(&b, t.e1, t.e2) != hipSuccess) {
+      a2m::set_error("gemm timing: event query failed");
+      rc = A2M_EHIP;
+    }
+    ++n;
+    f += t.flops;
+    mt += a;
+    if (t.reduce) { mr += b; ++nr; }
+    (void)hipEventDestroy(t.e0);
+    (void)hipEventDestroy(t.e1);
+    (void)hipEventDestroy(t.e2);
+  }
+  a2m::g_timing_recs.clear();
+  if (launches) *launches = n;
+  if (flops) *flops = f;
+  if (ms_tile) *ms_tile = mt;
+  if (ms_reduce) *ms_reduce = mr;
+  if (reduces) *reduces = nr;
+  return rc;
+}
+
+}  // extern "C"
+
+namespace a2m {
 
 }  // namespace a2m

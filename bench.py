@@ -6,8 +6,10 @@ in HBM.  The step is captured once in a HIP graph and replayed.  N GPUs = N inde
 replicas (inference does not shard further: "replicas only", weak scaling), launched one
 process per GPU by torch.distributed.run; max-over-ranks time.
 
-Printed JSON adds `roofline` (the dominant kernel -- the largest UNet implicit-GEMM conv --
-timed with HIP events on its own stream, against the fp32 MFMA peak), `mel_roofline`
+Printed JSON adds `roofline` (the dominant kernel family -- the implicit-GEMM engine's
+gemm_kernel, ~70 % of step time -- every launch of one step timed with HIP events on its
+launch stream, algorithmic FLOPs 2*M*N*K per launch, against the fp32 MFMA peak; `traffic`
+from the committed PMC pass, profiles/traffic_latest.json), `mel_roofline`
 (log-mel kernel vs HBM peak), `path_roofline` (the whole G forward's useful FLOPs) and
 `cpu_baseline` (the torch-CPU oracle port on a bounded sample, rank 0 at N=1 only).
 """
@@ -64,30 +66,28 @@ def g_forward_flops(B, T, C=256):
     return f * B
 
 
-def run_dominant_kernel(dev, iters=20):
-    """Time the largest single implicit-GEMM launch of the step (UNet upsample_layers[1]:
-    Conv1d 2048->1024, k3, T/2=32, B=64, BN + LeakyReLU epilogue) with HIP events."""
+def gemm_engine_timing(step):
+    """Run one eager step with every implicit-GEMM launch bracketed by HIP events on its own
+    stream (a2m_gemm_timing_*): the engine's launches/step, algorithmic FLOPs (2*M*N*K) and
+    summed tile-kernel / split-K-reduce time.  rocprof's gemm_kernel<...> rows of the same
+    command (profiles/) must agree with ms_tile / launches."""
     from a2m import functional as F
-    B, Ci, Co, T = 64, 2048, 1024, 32
-    x = torch.randn(B, Ci, T, device=dev)
-    w = torch.randn(Co, Ci, 3, device=dev) * 0.01
-    b = torch.zeros(Co, device=dev)
-    bn = (torch.ones(Co, device=dev), torch.zeros(Co, device=dev), torch.zeros(Co, device=dev),
-          torch.ones(Co, device=dev), 1e-5)
-    y = torch.empty(B, Co, T, device=dev)
-    s = torch.cuda.Stream(dev)
-    with torch.cuda.stream(s):
-        for _ in range(3):
-            F.conv1d(x, w, b, 1, 1, bn=bn, act=F.ACT_LRELU, out=y)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(iters):
-            F.conv1d(x, w, b, 1, 1, bn=bn, act=F.ACT_LRELU, out=y)
-        e1.record(s)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    flops = 2.0 * Co * Ci * 3 * B * T
-    return ms, flops
+    torch.cuda.synchronize()
+    with F.gemm_timing() as t:
+        step()
+        torch.cuda.synchronize()
+    return t
+
+
+def load_traffic(name):
+    """HBM bytes per launch for a kernel family, from the committed PMC pass
+    (tools/pmc_traffic.py -> profiles/traffic_latest.json), or None."""
+    path = os.path.join(REPO, 'profiles', 'traffic_latest.json')
+    try:
+        with open(path) as f:
+            return json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
 
 
 def run_mel_kernel(dev, wave, iters=50):
@@ -132,6 +132,20 @@ def cpu_baseline(B=8, T=64, max_s=20.0):
     return {'value': round(B * T / med, 1), 'unit': 'pose-frames/s', 'cores': threads, 'kind': 'port',
             'sample': f'{B} clips x {T} frames (numpy fp64 log-mel + torch-CPU fp32 G forward), '
                       f'median of {len(times)} runs, {threads} threads'}
+
+
+def roofline_entry(gt):
+    tf = gt.flops / (gt.ms_tile * 1e-3) / 1e12
+    tr = load_traffic('gemm_kernel')
+    return {'bound': 'mfma', 'kernel': 'gemm_kernel (implicit-GEMM engine: every launch of one step)',
+            'achieved': round(tf, 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+            'traffic': tr['bytes_per_launch'] if tr else None,
+            'traffic_source': tr['source'] if tr else None,
+            'launches_per_step': gt.launches, 'ms_per_launch': round(gt.ms_tile / max(gt.launches, 1), 4),
+            'gflop_per_launch': round(gt.flops / max(gt.launches, 1) / 1e9, 3),
+            'ms_tile_per_step': round(gt.ms_tile, 4),
+            'splitk_reduce_ms_per_step': round(gt.ms_reduce, 4)}
 
 
 def main():
@@ -207,7 +221,7 @@ def main():
 
         ms_step = elapsed / args.steps * 1e3
         value = world * B * T / (elapsed / args.steps)
-        k_ms, k_flops = run_dominant_kernel(dev)
+        gt = gemm_engine_timing(step)
         mel_ms, mel_bytes = run_mel_kernel(dev, wave)
     path_tf = g_forward_flops(B, T) / (ms_step * 1e-3) / 1e12
     result = {
@@ -219,10 +233,7 @@ def main():
         'config': {'workload': 'configs[1]: log-mel + SelfAttention_G forward (eval), batch-64 x 64-frame '
                                'clips per GPU, replicas only', 'global_batch': B * world, 'seq_len': T,
                    'parallelism': f'replicas{world}', 'hip_graph': graph is not None},
-        'roofline': {'bound': 'mfma', 'kernel': 'gemm_kernel (UNet up conv 2048->1024 k3, B64 T32)',
-                     'achieved': round(k_flops / (k_ms * 1e-3) / 1e12, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
-                     'unit': 'TFLOP/s', 'frac': round(k_flops / (k_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
-                     'traffic': None, 'ms_per_launch': round(k_ms, 4)},
+        'roofline': roofline_entry(gt),
         'mel_roofline': {'bound': 'hbm', 'achieved': round(mel_bytes / (mel_ms * 1e-3) / 1e9, 1),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(mel_bytes / (mel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

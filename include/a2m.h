@@ -280,6 +280,14 @@ int a2m_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                  void* stream);
 
+/* Measurement hook (bench.py): while enabled, every launch of the implicit-GEMM engine is
+ * bracketed by HIP events on its stream; _end synchronises them and returns the launch count,
+ * the launches' algorithmic FLOPs (2*M*N*K*batch), the summed tile-kernel time and the summed
+ * split-K reduce time (ms).  Not graph-capturable; no effect when disabled. */
+int a2m_gemm_timing_begin(void);
+int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
+                        int64_t* reduces);
+
 #ifdef __cplusplus
 }
 #endif

@@ -93,6 +93,22 @@ def test_state_dict_keys_match_reference():
             assert list(sd[k].shape) == shp, k
 
 
+def test_edge_template_checked_on_load():
+    """A reference checkpoint's edge template loads; a different topology is refused."""
+    import torch
+    from a2m.real_motion_model import SelfAttention_G
+    g = SelfAttention_G(p=0.0)
+    sd = g.state_dict()
+    g.load_state_dict(sd)
+    bad = dict(sd)
+    g.load_state_dict({**sd, 'body_edge_index_template': sd['body_edge_index_template'].flip(1)})
+    bad['body_edge_index_template'] = sd['body_edge_index_template'].clone()
+    bad['body_edge_index_template'][1, 0] = (bad['body_edge_index_template'][1, 0] + 3) % 10
+    with pytest.raises(RuntimeError, match='edge template'):
+        g.load_state_dict(bad)
+    assert torch.equal(g.body_edge_index_template, sd['body_edge_index_template'])
+
+
 def test_old_pyg_gat_keys_load():
     from a2m.graph_layers import GATConv
     m = GATConv(64, 64, heads=4, concat=False)

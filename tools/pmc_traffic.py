@@ -1,0 +1,73 @@
+"""HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE are too big
+for one pass on gfx950), with the MI355X_MICROARCH.md corrections:
+
+  * counter unit: kilobytes (rocprofv3's derived FETCH_SIZE/WRITE_SIZE divide by 1024);
+  * gfx950 FETCH_SIZE counts exactly half the bytes of wide (16 B/lane) coalesced reads,
+    so it is doubled; WRITE_SIZE is exact for 16 B/lane and dword stores.
+
+    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [--out profiles/traffic_latest.json]
+
+Each DIR is a rocprofv3 `-d` output directory holding a *counter_collection.csv.  Kernel
+families are matched by substring (gemm_kernel, logmel_kernel, graph_layer_kernel, ...).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+FAMILIES = ('gemm_kernel', 'splitk_reduce_kernel', 'logmel_kernel', 'graph_layer_kernel',
+            'graph_att_proj_kernel', 'channel_attention_kernel', 'softmax_rows_kernel', 'layernorm_kernel')
+
+
+def read_counter(d, name):
+    files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
+    if not files:
+        raise SystemExit(f'no counter_collection.csv under {d}')
+    per = defaultdict(lambda: [0, 0.0])       # family -> [dispatches, KB]
+    seen = set()
+    for fn in files:
+        with open(fn, newline='') as f:
+            for row in csv.DictReader(f):
+                if row.get('Counter_Name') != name:
+                    continue
+                kn = row.get('Kernel_Name', '')
+                fam = next((x for x in FAMILIES if x in kn), None)
+                if fam is None:
+                    continue
+                key = (fn, row.get('Dispatch_Id') or row.get('Correlation_Id'))
+                if key not in seen:
+                    seen.add(key)
+                    per[fam][0] += 1
+                per[fam][1] += float(row['Counter_Value'])
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('fetch_dir')
+    ap.add_argument('write_dir')
+    ap.add_argument('--out', default='profiles/traffic_latest.json')
+    ap.add_argument('--tag', default='')
+    a = ap.parse_args()
+    fetch, write = read_counter(a.fetch_dir, 'FETCH_SIZE'), read_counter(a.write_dir, 'WRITE_SIZE')
+    out = {}
+    for fam in FAMILIES:
+        if fam not in fetch or fam not in write:
+            continue
+        nf, kf = fetch[fam]
+        nw, kw = write[fam]
+        rd = 2.0 * kf * 1024 / nf
+        wr = kw * 1024 / nw
+        out[fam] = {'bytes_per_launch': round(rd + wr), 'read_bytes_per_launch': round(rd),
+                    'write_bytes_per_launch': round(wr), 'dispatches': [nf, nw],
+                    'source': f'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes {a.tag}; FETCH x2 (gfx950), KB x1024'}
+    os.makedirs(os.path.dirname(a.out) or '.', exist_ok=True)
+    with open(a.out, 'w') as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == '__main__':
+    main()
