@@ -1,0 +1,143 @@
+"""Data-parallel GAN step on CPU: two gloo ranks, each on half the clips.
+After one GANTrainer iteration the all-reduced G and D gradients must equal the single-process
+whole-batch gradients, and the loss history must match.  After further iterations both ranks
+must hold bitwise-identical parameters and loss histories (so every rank takes the same
+DynamicGANTraining branches).
+
+The HIP kernels cannot run here, so the test swaps the trainer's device ops for their oracle
+equivalents (torch-CPU restatements of version5_model_train.py:208-248 and torch.optim.Adam)
+and uses small torch G/D models with the reference's call contract.  What is under test is
+the host-side DP logic: flat-gradient all-reduce, loss synchronisation, D frozen in the
+G-steps, optimiser bookkeeping.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+B, T, FD = 8, 16, 104
+
+
+class TinyG(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(128, FD)
+
+    def forward(self, audio, real_pose=None):
+        pose = self.lin(audio)
+        internal = [(pose ** 2).mean() * 1e-3]
+        if real_pose is not None:
+            internal.insert(0, (pose - real_pose).abs().mean() * 1e-2)
+        return pose, internal
+
+
+class TinyD(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.lin = torch.nn.Linear(FD, 1)
+
+    def forward(self, x, audio=None, aux_labels=None):
+        y = self.lin(x)                            # [B, T-1, 1]
+        return y[:, :4, 0], []
+
+
+def _patch_ops():
+    """Oracle stand-ins for the trainer's HIP ops (test-only)."""
+    from a2m import autograd as AG
+    from a2m import functional as F
+    from oracle import model as OM
+
+    def motion_terms(fake, real):
+        return torch.stack(OM.motion_terms(real, fake))
+
+    def adam_(p, g, m, v, lr, b1, b2, eps, wd, step):
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (v / (1 - b2 ** step)).sqrt_().add_(eps)
+        p.addcdiv_(m, denom, value=-lr / (1 - b1 ** step))
+
+    AG.pos_to_motion = lambda x: torch.diff(x, dim=1)
+    AG.motion_terms = motion_terms
+    AG.mse_loss = torch.nn.functional.mse_loss
+    F.adam_ = adam_
+
+
+def _data():
+    g = torch.Generator().manual_seed(3)
+    return torch.randn(B, T, 128, generator=g), torch.randn(B, T, FD, generator=g)
+
+
+def _models():
+    torch.manual_seed(11)
+    return TinyG(), TinyD()
+
+
+def _run(rank, world):
+    from a2m.training import GANTrainer
+    _patch_ops()
+    G, D = _models()
+    tr = GANTrainer(G, D, lr=1e-2, fixed_labels=(0.93, 0.07))
+    audio, pose = _data()
+    if world > 1:
+        shard = B // world
+        audio, pose = audio[rank * shard:(rank + 1) * shard], pose[rank * shard:(rank + 1) * shard]
+    tr.iteration(audio, pose, epoch=0, g_freq=1, d_freq=1)
+    grads = (tr.opt_G.flat_grad.clone(), tr.opt_D.flat_grad.clone(),
+             list(tr.dyn.d_loss_history), list(tr.dyn.g_loss_history))
+    for epoch in range(1, 3):
+        tr.iteration(audio, pose, epoch=epoch, g_freq=3, d_freq=1)
+    params = (tr.opt_G.flat.clone(), tr.opt_D.flat.clone(), list(tr.dyn.d_loss_history),
+              list(tr.dyn.g_loss_history))
+    return grads, params
+
+
+def _plain(res):
+    """numpy copies: torch tensors sent through a Queue need the sender alive."""
+    return tuple(tuple(x.numpy() if torch.is_tensor(x) else x for x in part) for part in res)
+
+
+def _worker(rank, world, port, q):
+    if world == 1:                    # single-process reference, no process group
+        q.put(('ref', _plain(_run(0, 1))))
+        return
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        q.put((rank, _plain(_run(rank, world))))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(300)
+def test_dp_two_ranks_matches_single_process():
+    # every run happens in a spawned child: the op stand-ins never leak into this process
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(0, 1, port, q))]
+    procs += [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    ref = res['ref']
+    (rg, rd, rdh, rgh), _ = ref
+    for r in (0, 1):
+        (g, d, dh, gh), _ = res[r]
+        assert abs(g - rg).max() <= 1e-5 * abs(rg).max(), ('G grad', r)
+        assert abs(d - rd).max() <= 1e-5 * abs(rd).max(), ('D grad', r)
+        assert dh == pytest.approx(rdh, rel=1e-5) and gh == pytest.approx(rgh, rel=1e-5)
+    p0, p1 = res[0][1], res[1][1]
+    assert (p0[0] == p1[0]).all() and (p0[1] == p1[1]).all()         # bitwise-identical replicas
+    assert p0[2] == p1[2] and p0[3] == p1[3]                        # identical branch inputs
