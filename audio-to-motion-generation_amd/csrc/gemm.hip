@@ -5,10 +5,10 @@
 // (bias, BatchNorm-eval affine, activation, gamma scale, residual adds, strided store).
 //
 // Tiling: 256 threads = 4 waves in a 2x2 layout, block tile BM x BN (128x128 or 64x64),
-// BK = 16.  Both operands are staged in LDS as [row][k] with a 20-float (80 B) row pitch:
-// a wave64 lane (i = lane&31, h = lane>>5) reads its 8 k-values of row i as two
-// ds_read_b128 (conflict-free at this pitch) and feeds MFMA sub-step s with k = 8h + s --
-// the MFMA's k slot assignment is free as long as A and B agree.  Global loads for tile
+// BK = 16 or 32.  Both operands are staged in LDS as [row][k] with a (BK+4)-float row pitch:
+// a wave64 lane (i = lane&31, h = lane>>5) reads its k-values of row i 8 at a time as two
+// ds_read_b128 (conflict-free at this pitch) and feeds MFMA sub-step s with k = (BK/2)h + s
+// -- the MFMA's k slot assignment is free as long as A and B agree.  Global loads for tile
 // k+1 are issued into registers before the MFMAs of tile k; LDS is double-buffered so one
 // barrier per K-step suffices.  Split-K writes fp32 partial slabs to a workspace that a
 // second kernel reduces in a fixed order (bitwise reproducible) and runs the epilogue on.
@@ -22,8 +22,8 @@ namespace a2m {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 16;
-constexpr int LDK = BK + 4;
+// K-tile depth: 16 or 32 (runtime choice, A2M_GEMM_BK).  LDS row pitch BK+4 floats keeps the
+// per-lane ds_read_b128 fragment reads conflict-free (row*pitch mod 64 banks distinct over 16 rows).
 
 struct GemmArgs {
   Gather A, B;
@@ -31,6 +31,7 @@ struct GemmArgs {
   int M, N, K;
   int splits, kchunk;
   float* partial;
+  int xcd_group;   // >0: XCD-aware block remap with this many M-tiles per group; 0: identity
 };
 
 struct RowInfo {
@@ -94,36 +95,61 @@ __device__ __forceinline__ float gather_elem(const Gather& g, const float* base,
   return v ? base[ri.base + p.k0 * g.sk0 + h * g.sh + w * g.sw] : 0.f;
 }
 
-// MODE 0: dense k-contiguous, float4 loads.  MODE 1: k-contiguous gather (scalar).
-// MODE 2: row-contiguous gather (consecutive lanes -> consecutive rows).
-template <int BR, int MODE>
+typedef float float4u __attribute__((ext_vector_type(4), aligned(4)));
+
+// Operand staging.  The MFMA k-slot order is k = 16*half + 8*h + s (h = lane>>5, s = 0..7,
+// half = 0..BK/16-1) for both operands.
+//   MODE 0: dense k-contiguous rows, float4 loads, LDS [row][k].
+//   MODE 1: k-contiguous gather (scalar loads), LDS [row][k].
+//   MODE 2: row-contiguous gather (scalar loads, lanes along rows), LDS [row][k].
+//   MODE 3: row-contiguous rows loaded 4 at a time (float4 along the row axis: [K][R] matrices
+//           and stride-1 conv im2col over [B][C][T]), LDS [k][row] -- no transpose on the way in;
+//           fragments are read with ds_read_b32 (8 per 32-row tile per half).
+template <int BR, int BK, int MODE>
 struct TileLoader {
-  static constexpr int NPASS = BR / 64;             // k-major maps: 64 rows x 4 quads / pass
+  static constexpr bool KMAJ = MODE == 3;
+  static constexpr int LDK = BK + 4;                // [row][k] pitch
+  static constexpr int LDR = BR + 4;                // [k][row] pitch: 8*LDR = 32 mod 64 banks
+  static constexpr int TILE = KMAJ ? BK * LDR : BR * LDK;
+  static constexpr int QPR = BK / 4;                // k-major maps: float4 quads per row
+  static constexpr int RPP = 256 / QPR;             //   rows per pass
+  static constexpr int NPASS = BR / RPP;
   static constexpr int KPT = BK * BR / 256;         // row-major map: k per thread
   static constexpr int NREG = BK * BR / 256;        // floats per thread
+  static constexpr int QR = BR / 4;                 // mode 3: float4 row groups per k
+  static constexpr int KPP = 256 / QR;              //   k per pass
+  static constexpr int NP3 = BK / KPP;
   const Gather* g;
   const float* base;
   int K;
-  RowInfo ri[MODE == 2 ? 1 : NPASS];
-  int lrow[MODE == 2 ? 1 : NPASS];
+  RowInfo ri[MODE == 2 || MODE == 3 ? 1 : NPASS];
+  int lrow[MODE == 2 || MODE == 3 ? 1 : NPASS];
   int kq;  // k offset of this thread inside the tile
+  int nrow;  // mode 3: rows of this group that exist (0..4)
+  int wstep;  // mode 3: w advance per row (1 for conv rows, 0 for plain [K][R])
   float r[NREG];
 
   __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid) {
     g = &gg;
     base = gg.base + (int64_t)z * gg.bstride;
     K = KK;
-    if (MODE == 2) {
+    if (MODE == 3) {
+      lrow[0] = (tid % QR) * 4;
+      kq = tid / QR;
+      ri[0] = row_info(gg, row0 + lrow[0], R);
+      nrow = min(4, max(0, R - (row0 + lrow[0])));
+      wstep = gg.R2 > 1 ? 1 : 0;
+    } else if (MODE == 2) {
       lrow[0] = tid % BR;
       kq = (tid / BR) * KPT;
       ri[0] = row_info(gg, row0 + lrow[0], R);
     } else {
 #pragma unroll
       for (int p = 0; p < NPASS; ++p) {
-        lrow[p] = tid / 4 + p * 64;
+        lrow[p] = tid / QPR + p * RPP;
         ri[p] = row_info(gg, row0 + lrow[p], R);
       }
-      kq = (tid % 4) * 4;
+      kq = (tid % QPR) * 4;
     }
   }
 
@@ -146,18 +172,54 @@ struct TileLoader {
           kinc(*g, kp);
         }
       }
-    } else {
+    } else if (MODE == 2) {
       KPos kp = kpos(*g, k0 + kq);
 #pragma unroll
       for (int j = 0; j < KPT; ++j) {
         r[j] = gather_elem(*g, base, ri[0], kp, K);
         kinc(*g, kp);
       }
+    } else {
+      // 4 consecutive rows share r0 (host guarantees R2 % 4 == 0 or R2 == 1 with sr0 == 1), so
+      // their elements are consecutive floats starting at w.
+#pragma unroll
+      for (int p = 0; p < NP3; ++p) {
+        const KPos kp = kpos(*g, k0 + kq + p * KPP);
+        const int h = ri[0].h + kp.k1 * g->bk1;
+        const int w = ri[0].w + kp.k2 * g->bk2;
+        bool hv = kp.k < K && h >= 0 && nrow > 0;
+        int hh = h;
+        if (g->divh > 1) {
+          hv = hv && (h % g->divh) == 0;
+          hh = h / g->divh;
+        }
+        hv = hv && hh < g->Lh;
+        const int64_t a = (int64_t)ri[0].base + (int64_t)kp.k0 * g->sk0 + (int64_t)hh * g->sh + w;
+        float4 v;
+        if (hv && nrow == 4 && w >= 0 && w + 3 * wstep < g->Lw) {
+          const float4u u = *reinterpret_cast<const float4u*>(base + a);
+          v = make_float4(u.x, u.y, u.z, u.w);
+        } else {
+          float e[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int wj = w + j * wstep;
+            e[j] = (hv && j < nrow && wj >= 0 && wj < g->Lw) ? base[a + j] : 0.f;
+          }
+          v = make_float4(e[0], e[1], e[2], e[3]);
+        }
+        r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
+      }
     }
   }
 
   __device__ __forceinline__ void store(float* lds) const {
-    if (MODE == 2) {
+    if (MODE == 3) {
+#pragma unroll
+      for (int p = 0; p < NP3; ++p)
+        *reinterpret_cast<float4*>(lds + (kq + p * KPP) * LDR + lrow[0]) =
+            make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
+    } else if (MODE == 2) {
       float* dst = lds + lrow[0] * LDK + kq;
 #pragma unroll
       for (int j = 0; j < KPT; j += 4)
@@ -167,6 +229,21 @@ struct TileLoader {
       for (int p = 0; p < NPASS; ++p)
         *reinterpret_cast<float4*>(lds + lrow[p] * LDK + kq) =
             make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
+    }
+  }
+
+  // The 8 k-values (k = 16*half + 8*lh + s, s = 0..7) of tile row `row` for one lane.
+  __device__ __forceinline__ static void frag(const float* lds, int row, int half, int lh, float* f) {
+    if (KMAJ) {
+      const float* q = lds + (half * 16 + lh * 8) * LDR + row;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) f[s] = q[s * LDR];
+    } else {
+      const float* q = lds + row * LDK + half * 16 + lh * 8;
+      const float4 v0 = *reinterpret_cast<const float4*>(q);
+      const float4 v1 = *reinterpret_cast<const float4*>(q + 4);
+      f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w;
+      f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
     }
   }
 };
@@ -198,22 +275,47 @@ __device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int
   E.out[off] = v;
 }
 
-template <int BM, int BN, int MA, int MB>
+template <int BM, int BN, int BK, int MA, int MB>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
   constexpr int TM = BM / 64, TN = BN / 64;
-  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
+  using LA = TileLoader<BM, BK, MA>;
+  using LB = TileLoader<BN, BK, MB>;
+  constexpr int STAGE = LA::TILE + LB::TILE;
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
-  const int zz = blockIdx.z;
+
+  // Block -> (n-tile, m-tile, batch*split).  With xcd_group > 0 the linear block id, which the
+  // dispatcher deals round-robin over the 8 XCDs, is first made contiguous per XCD (bijective
+  // for any grid size) and then walked in groups of xcd_group M-tiles, so the blocks that share
+  // an XCD's L2 share A panels (weights) and B panels (activations).
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (args.xcd_group > 0) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int q = total / 8, r = total % 8, x = L % 8;
+    const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
+    bz = t / (gx * gy);
+    const int rem = t - bz * gx * gy;
+    const int gm = args.xcd_group;
+    const int group = rem / (gm * gx);
+    const int first_m = group * gm;
+    const int gsz = min(gy - first_m, gm);
+    const int in = rem - group * gm * gx;
+    by = first_m + in % gsz;
+    bx = in / gsz;
+  }
+  const int zz = bz;
   const int batch = zz / args.splits, split = zz % args.splits;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = by * BM, n0 = bx * BN;
   const int kbeg = split * args.kchunk;
   const int kend = min(args.K, kbeg + args.kchunk);
 
-  TileLoader<BM, MA> la;
-  TileLoader<BN, MB> lb;
+  LA la;
+  LB lb;
   la.init(args.A, batch, m0, args.M, args.K, tid);
   lb.init(args.B, batch, n0, args.N, args.K, tid);
 
@@ -229,7 +331,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
     la.load(kbeg);
     lb.load(kbeg);
     la.store(lds);
-    lb.store(lds + BM * LDK);
+    lb.store(lds + LA::TILE);
   }
   __syncthreads();
   int cur = 0;
@@ -239,36 +341,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
       la.load(k + BK);
       lb.load(k + BK);
     }
-    const float* As = lds + cur * (BM + BN) * LDK;
-    const float* Bs = As + BM * LDK;
-    float af[TM][8], bf[TN][8];
+    const float* As = lds + cur * STAGE;
+    const float* Bs = As + LA::TILE;
 #pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      const float* p = As + (wm * (BM / 2) + t * 32 + li) * LDK + lh * 8;
-      float4 v0 = *reinterpret_cast<const float4*>(p);
-      float4 v1 = *reinterpret_cast<const float4*>(p + 4);
-      af[t][0] = v0.x; af[t][1] = v0.y; af[t][2] = v0.z; af[t][3] = v0.w;
-      af[t][4] = v1.x; af[t][5] = v1.y; af[t][6] = v1.z; af[t][7] = v1.w;
+    for (int half = 0; half < BK / 16; ++half) {
+      float af[TM][8], bf[TN][8];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) LA::frag(As, wm * (BM / 2) + t * 32 + li, half, lh, af[t]);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) LB::frag(Bs, wn * (BN / 2) + u * 32 + li, half, lh, bf[u]);
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+#pragma unroll
+          for (int u = 0; u < TN; ++u)
+            acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][s], bf[u][s], acc[t][u], 0, 0, 0);
     }
-#pragma unroll
-    for (int u = 0; u < TN; ++u) {
-      const float* p = Bs + (wn * (BN / 2) + u * 32 + li) * LDK + lh * 8;
-      float4 v0 = *reinterpret_cast<const float4*>(p);
-      float4 v1 = *reinterpret_cast<const float4*>(p + 4);
-      bf[u][0] = v0.x; bf[u][1] = v0.y; bf[u][2] = v0.z; bf[u][3] = v0.w;
-      bf[u][4] = v1.x; bf[u][5] = v1.y; bf[u][6] = v1.z; bf[u][7] = v1.w;
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int u = 0; u < TN; ++u)
-          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][s], bf[u][s], acc[t][u], 0, 0, 0);
     if (has_next) {
-      float* nxt = lds + (cur ^ 1) * (BM + BN) * LDK;
+      float* nxt = lds + (cur ^ 1) * STAGE;
       la.store(nxt);
-      lb.store(nxt + BM * LDK);
+      lb.store(nxt + LA::TILE);
     }
     __syncthreads();
     cur ^= 1;
@@ -316,8 +409,20 @@ __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
   }
 }
 
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
 static int operand_mode(const Gather& g, int K) {
-  if (!g.kcontig) return 2;
+  if (!g.kcontig) {
+    // rows 4-at-a-time contiguous: plain [K][R] (rows via r0, unit stride) or stride-1 im2col
+    // rows along w within an r0 block whose length is a multiple of 4
+    const bool plain = g.R1 == 1 && g.R2 == 1 && g.sr0 == 1;
+    const bool conv = g.R1 == 1 && g.R2 > 1 && g.R2 % 4 == 0 && g.ar2 == 1 && g.sw == 1 && g.divw == 1;
+    static const int allow = env_int("A2M_GEMM_MODE3", 1);
+    return allow && (plain || conv) ? 3 : 2;
+  }
   const bool dense = g.K1 == 1 && g.K2 == 1 && g.sk0 == 1 && g.Lh == 1 && g.Lw == 1 &&
                      g.sh == 0 && g.sw == 0 && g.ch == 0 && g.cw == 0 && g.divh == 1 && g.divw == 1;
   const bool aligned = (reinterpret_cast<uintptr_t>(g.base) % 16 == 0) && (g.sr0 % 4 == 0) &&
@@ -326,19 +431,26 @@ static int operand_mode(const Gather& g, int K) {
 }
 
 struct Plan {
-  int bm, splits, kchunk;
+  int bm, bk, splits, kchunk;
 };
 
-static int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : dflt;
+// Tile / split-K choice: fill the 256 CUs with >= ~2 workgroups each while keeping every
+// K-slice >= 256 deep.  A2M_GEMM_TILE=64|128, A2M_GEMM_SPLIT=n, A2M_GEMM_BK=16|32 and
+// A2M_GEMM_XCD=g (XCD-aware remap, g M-tiles per group; 0 = off) override (experiments).
+static int gemm_bk() {
+  static const int bk = env_int("A2M_GEMM_BK", 32) == 16 ? 16 : 32;
+  return bk;
 }
 
-// Tile / split-K choice: fill the 256 CUs with >= ~2 workgroups each while keeping every
-// K-slice >= 256 deep.  A2M_GEMM_TILE=64|128 and A2M_GEMM_SPLIT=n override (experiments).
+static int gemm_xcd_group() {
+  static const int g = env_int("A2M_GEMM_XCD", 0);
+  return g < 0 ? 0 : g;
+}
+
 static Plan plan_for(int M, int N, int K, int batch) {
   static const int force_tile = env_int("A2M_GEMM_TILE", 0);
   static const int force_split = env_int("A2M_GEMM_SPLIT", 0);
+  const int BK = gemm_bk();
   auto splits_for = [&](int64_t tiles) {
     int s = 1;
     while (s < 64 && tiles * s < 512 && K / (s * 2) >= 256) s *= 2;
@@ -352,6 +464,7 @@ static Plan plan_for(int M, int N, int K, int batch) {
   if (force_tile == 64 || force_tile == 128) p.bm = force_tile;
   int splits = p.bm == 128 ? s128 : s64;
   if (force_split > 0) splits = force_split;
+  p.bk = BK;
   p.kchunk = (int)(cdiv(cdiv(K, splits), BK) * BK);
   p.splits = (int)cdiv(K, p.kchunk);
   return p;
@@ -362,14 +475,15 @@ size_t gemm_ws_bytes(int M, int N, int K, int batch) {
   return p.splits > 1 ? (size_t)p.splits * batch * M * N * sizeof(float) : 0;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BK>
 static void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
-  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, MA_, MB_>), grid, dim3(256), 0, st, a); return; }
-  A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2)
-  A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2)
-  A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2)
+  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_>), grid, dim3(256), 0, st, a); return; }
+  A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3)
+  A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2) A2M_L(1, 3)
+  A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3)
+  A2M_L(3, 0) A2M_L(3, 1) A2M_L(3, 2) A2M_L(3, 3)
 #undef A2M_L
 }
 
@@ -418,13 +532,14 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   a.A = A; a.B = B; a.E = E; a.M = M; a.N = N; a.K = K;
   Plan p = plan_for(M, N, K, batch);
   if (force_split > 0) {
-    p.kchunk = (int)(cdiv(cdiv(K, force_split), BK) * BK);
+    p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk) * p.bk);
     p.splits = (int)cdiv(K, p.kchunk);
   }
-  if (K == 0) { p.splits = 1; p.kchunk = BK; }
+  if (K == 0) { p.splits = 1; p.kchunk = p.bk; }
   a.splits = p.splits;
   a.kchunk = p.kchunk;
   a.partial = nullptr;
+  a.xcd_group = gemm_xcd_group();
   if (p.splits > 1) {
     const size_t need = (size_t)p.splits * batch * M * N * sizeof(float);
     if (ws == nullptr || ws_bytes < need) {
@@ -435,8 +550,13 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   }
   const int ma = operand_mode(A, K), mb = operand_mode(B, K);
   const long tm = g_timing ? timing_open(2.0 * M * N * (double)K * batch, stream) : -1;
-  if (p.bm == 128) launch_tile<128, 128>(a, ma, mb, batch, stream);
-  else launch_tile<64, 64>(a, ma, mb, batch, stream);
+  if (p.bk == 32) {
+    if (p.bm == 128) launch_tile<128, 128, 32>(a, ma, mb, batch, stream);
+    else launch_tile<64, 64, 32>(a, ma, mb, batch, stream);
+  } else {
+    if (p.bm == 128) launch_tile<128, 128, 16>(a, ma, mb, batch, stream);
+    else launch_tile<64, 64, 16>(a, ma, mb, batch, stream);
+  }
   A2M_LAUNCH_CHECK();
   if (tm >= 0) timing_mark(tm, 1, false, stream);
   if (p.splits > 1) {

@@ -67,6 +67,23 @@ def graph_case(J, lo, kind, B=64, T=64):
     return us, 2.0 * x.shape[0] * 64 * (256 if kind == 0 else 128)
 
 
+def dense_case(M, N, K):
+    A = torch.randn(M, K, device=dev)
+    Bm = torch.randn(N, K, device=dev)
+    C = torch.empty(M, N, device=dev)
+    us = timeit(lambda: F.gemm(M, N, K, A, K, 1, Bm, K, 1, C, N, 1), iters=10)
+    return us, 2.0 * M * N * K
+
+
+def dense_nn_case(M, N, K):
+    """B stored [K][N] (row-contiguous operand, the [B,C,T] activation orientation)."""
+    A = torch.randn(M, K, device=dev)
+    Bm = torch.randn(K, N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    us = timeit(lambda: F.gemm(M, N, K, A, K, 1, Bm, 1, N, C, N, 1), iters=10)
+    return us, 2.0 * M * N * K
+
+
 CASES = {
     'unet.d0 256->512 k3 T64': lambda: conv_case(64, 256, 512, 64, 3, 1, 1),
     'unet.d1 512->512 k4s2 T64': lambda: conv_case(64, 512, 512, 64, 4, 2, 1),
@@ -81,6 +98,14 @@ CASES = {
     'attn C2048 T16': lambda: attn_case(64, 2048, 16),
     'attn C2048 T32': lambda: attn_case(64, 2048, 32),
     'attn C256 T64': lambda: attn_case(64, 256, 64),
+    'dense 4096^3': lambda: dense_case(4096, 4096, 4096),
+    'dense up1 1024x2048x6144': lambda: dense_case(1024, 2048, 6144),
+    'denseNN up1 1024x2048x6144': lambda: dense_nn_case(1024, 2048, 6144),
+    'denseNN up3 512x4096x3072': lambda: dense_nn_case(512, 4096, 3072),
+    'dense bott 2048x1024x3072': lambda: dense_case(2048, 1024, 3072),
+    'dense up3 512x4096x3072': lambda: dense_case(512, 4096, 3072),
+    'dense d2 1024x2048x1536': lambda: dense_case(1024, 2048, 1536),
+    'dense dec 256x4096x768': lambda: dense_case(256, 4096, 768),
     'gat body': lambda: graph_case(10, 0, 0),
     'gat hand': lambda: graph_case(42, 10, 0),
     'gconv hand': lambda: graph_case(42, 10, 1),
@@ -88,7 +113,7 @@ CASES = {
 
 if __name__ == '__main__':
     flt = sys.argv[1] if len(sys.argv) > 1 else ''
-    tag = os.environ.get('A2M_GEMM_TILE', '-') + '/' + os.environ.get('A2M_GEMM_SPLIT', '-')
+    tag = '/'.join(os.environ.get(k, '-') for k in ('A2M_GEMM_TILE', 'A2M_GEMM_SPLIT', 'A2M_GEMM_BK', 'A2M_GEMM_XCD'))
     for name, fn in CASES.items():
         if flt not in name:
             continue
