@@ -126,7 +126,7 @@ struct TileLoader {
   int lrow[MODE == 2 || MODE == 3 ? 1 : NPASS];
   int kq;  // k offset of this thread inside the tile
   int nrow;  // mode 3: rows of this group that exist (0..4)
-  int wstep;  // mode 3: w advance per row (1 for conv rows, 0 for plain [K][R])
+  int rdim;   // mode 3: 0 rows via r0, 1 rows along h, 2 rows along w
   float r[NREG];
 
   __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid) {
@@ -138,7 +138,7 @@ struct TileLoader {
       kq = tid / QR;
       ri[0] = row_info(gg, row0 + lrow[0], R);
       nrow = min(4, max(0, R - (row0 + lrow[0])));
-      wstep = gg.R2 > 1 ? 1 : 0;
+      rdim = gg.R2 > 1 ? 2 : (gg.R1 > 1 ? 1 : 0);
     } else if (MODE == 2) {
       lrow[0] = tid % BR;
       kq = (tid / BR) * KPT;
@@ -180,31 +180,32 @@ struct TileLoader {
         kinc(*g, kp);
       }
     } else {
-      // 4 consecutive rows share r0 (host guarantees R2 % 4 == 0 or R2 == 1 with sr0 == 1), so
-      // their elements are consecutive floats starting at w.
+      // 4 consecutive rows differ only in the row axis (host guarantees it): rdim 0 = rows via
+      // r0 with unit stride, 1 = rows along h (sh == 1), 2 = rows along w (sw == 1), so their
+      // elements are consecutive floats.
+      const int dh = rdim == 1, dw = rdim == 2;
 #pragma unroll
       for (int p = 0; p < NP3; ++p) {
         const KPos kp = kpos(*g, k0 + kq + p * KPP);
-        const int h = ri[0].h + kp.k1 * g->bk1;
+        int h = ri[0].h + kp.k1 * g->bk1;
         const int w = ri[0].w + kp.k2 * g->bk2;
-        bool hv = kp.k < K && h >= 0 && nrow > 0;
-        int hh = h;
-        if (g->divh > 1) {
-          hv = hv && (h % g->divh) == 0;
-          hh = h / g->divh;
+        bool kv = kp.k < K && nrow > 0;
+        if (g->divh > 1) {  // only with rdim != 1
+          kv = kv && h >= 0 && (h % g->divh) == 0;
+          h = h / g->divh;
         }
-        hv = hv && hh < g->Lh;
-        const int64_t a = (int64_t)ri[0].base + (int64_t)kp.k0 * g->sk0 + (int64_t)hh * g->sh + w;
+        const int64_t a = (int64_t)ri[0].base + (int64_t)kp.k0 * g->sk0 + (int64_t)h * g->sh +
+                          (int64_t)w * g->sw;
         float4 v;
-        if (hv && nrow == 4 && w >= 0 && w + 3 * wstep < g->Lw) {
+        if (kv && nrow == 4 && h >= 0 && h + 3 * dh < g->Lh && w >= 0 && w + 3 * dw < g->Lw) {
           const float4u u = *reinterpret_cast<const float4u*>(base + a);
           v = make_float4(u.x, u.y, u.z, u.w);
         } else {
           float e[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int wj = w + j * wstep;
-            e[j] = (hv && j < nrow && wj >= 0 && wj < g->Lw) ? base[a + j] : 0.f;
+            const int hj = h + j * dh, wj = w + j * dw;
+            e[j] = (kv && j < nrow && hj >= 0 && hj < g->Lh && wj >= 0 && wj < g->Lw) ? base[a + j] : 0.f;
           }
           v = make_float4(e[0], e[1], e[2], e[3]);
         }
@@ -416,12 +417,14 @@ static int env_int(const char* name, int dflt) {
 
 static int operand_mode(const Gather& g, int K) {
   if (!g.kcontig) {
-    // rows 4-at-a-time contiguous: plain [K][R] (rows via r0, unit stride) or stride-1 im2col
-    // rows along w within an r0 block whose length is a multiple of 4
+    // rows 4-at-a-time contiguous: plain [K][R] (rows via r0, unit stride), or stride-1 im2col
+    // rows along w (R2 % 4 == 0) or along h (R2 == 1, R1 % 4 == 0), unit element stride
     const bool plain = g.R1 == 1 && g.R2 == 1 && g.sr0 == 1;
-    const bool conv = g.R1 == 1 && g.R2 > 1 && g.R2 % 4 == 0 && g.ar2 == 1 && g.sw == 1 && g.divw == 1;
+    const bool along_w = g.R2 > 1 && g.R2 % 4 == 0 && g.ar2 == 1 && g.sw == 1 && g.divw == 1;
+    const bool along_h = g.R2 == 1 && g.R1 > 1 && g.R1 % 4 == 0 && g.ar1 == 1 && g.sh == 1 &&
+                         g.divh == 1;
     static const int allow = env_int("A2M_GEMM_MODE3", 1);
-    return allow && (plain || conv) ? 3 : 2;
+    return allow && (plain || along_w || along_h) ? 3 : 2;
   }
   const bool dense = g.K1 == 1 && g.K2 == 1 && g.sk0 == 1 && g.Lh == 1 && g.Lw == 1 &&
                      g.sh == 0 && g.sw == 0 && g.ch == 0 && g.cw == 0 && g.divh == 1 && g.divw == 1;
@@ -549,6 +552,10 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     a.partial = static_cast<float*>(ws);
   }
   const int ma = operand_mode(A, K), mb = operand_mode(B, K);
+  static const int log_launches = env_int("A2M_GEMM_LOG", 0);
+  if (log_launches)
+    std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d\n", M, N,
+                 K, batch, p.bm, p.bk, p.splits, ma, mb);
   const long tm = g_timing ? timing_open(2.0 * M * N * (double)K * batch, stream) : -1;
   if (p.bk == 32) {
     if (p.bm == 128) launch_tile<128, 128, 32>(a, ma, mb, batch, stream);

@@ -43,22 +43,26 @@ __global__ __launch_bounds__(512) void graph_att_proj_kernel(const float* __rest
   Ug[threadIdx.x] = s;
 }
 
-__global__ __launch_bounds__(256, 2) void graph_layer_kernel(
+// One workgroup = whole frames (<= 128 node rows), 4 waves; wave w owns rows 32w..32w+31 of
+// the layer GEMM out[128 x 64] = sum_seg A_seg[128 x 64] . W_seg^T.  The A fragments are built
+// straight in registers by the lane that feeds them to the MFMA (lane (li, lh) holds row 32w+li,
+// k = 16kc + 8lh + s), so the aggregation needs no LDS tile and no barrier: per segment each lane
+// computes its row's edge softmax (GAT head `seg`) from the block's logits, gathers its
+// neighbours' 8-float k-slices from the LDS node tile and issues the MFMAs.  LayerNorm(64),
+// LeakyReLU and the residual run on the accumulators (row reductions = 32-lane shuffles).
+// LDS = node tile + logits + lists (~40 KB): several workgroups per CU hide the HBM latency.
+__global__ __launch_bounds__(256, 3) void graph_layer_kernel(
     const float* __restrict__ x, int F, int J, int kind, int norm_res, const int* __restrict__ nbr_ptr,
     const int* __restrict__ nbr_idx, const float* __restrict__ w0, const float* __restrict__ w1,
     const float* __restrict__ att_src, const float* __restrict__ att_dst,
     const float* __restrict__ bias, const float* __restrict__ ln_w, const float* __restrict__ ln_b,
     float slope, const float* __restrict__ Ug, float* __restrict__ y, float* __restrict__ pre_ln) {
   __shared__ __attribute__((aligned(16))) float xs[GMAXN * ZP];
-  __shared__ __attribute__((aligned(16))) float ys[GMAXN * ZP];
-  // U (attention projections) is only needed before the segment loop, the per-head edge
-  // weights ew only inside it: they share one 4 KB array so two workgroups fit per CU.
-  __shared__ __attribute__((aligned(16))) float u_ew[GMAXN * GMAXDEG];
-  float (*U)[GF] = reinterpret_cast<float (*)[GF]>(u_ew);
-  float (*ew)[GMAXDEG] = reinterpret_cast<float (*)[GMAXDEG]>(u_ew);
-  __shared__ float al[GMAXN][2 * GHEADS];
-  __shared__ unsigned char nbl[GMAXN][GMAXDEG];
+  __shared__ __attribute__((aligned(16))) float Uk[GF][2 * GHEADS];   // k-major attention projections
+  __shared__ float al[2 * GHEADS][GMAXN];                              // logits, q-major
+  __shared__ __attribute__((aligned(8))) unsigned char nbl[GMAXN][GMAXDEG];
   __shared__ unsigned char ndeg[GMAXN];
+  __shared__ int csr[2 * GMAXN];
 
   const int fpb = GMAXN / J;
   const int NBmax = fpb * J;
@@ -68,6 +72,8 @@ __global__ __launch_bounds__(256, 2) void graph_layer_kernel(
   const int lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
 
+  // ---- prologue: node tile, U, CSR (independent loads, one barrier)
+  const int ne = min(nbr_ptr[J], 2 * GMAXN - (J + 1));
   for (int i = tid; i < GMAXN * (GF / 4); i += blockDim.x) {
     const int n = i / (GF / 4), q = i % (GF / 4);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -75,28 +81,53 @@ __global__ __launch_bounds__(256, 2) void graph_layer_kernel(
     *reinterpret_cast<float4*>(xs + n * ZP + q * 4) = v;
   }
   if (kind == 0)
-    for (int i = tid; i < 2 * GHEADS * GF; i += blockDim.x) (&U[0][0])[i] = Ug[i];
-  // block-local neighbour lists: in-edges in edge order, then (GAT) the PyG self loop
-  for (int n = tid; n < NB; n += blockDim.x) {
-    const int f0 = (n / J) * J, ln = n % J;
-    const int e0 = nbr_ptr[ln], e1 = nbr_ptr[ln + 1];
+    for (int i = tid; i < 2 * GHEADS * GF; i += blockDim.x) Uk[i % GF][i / GF] = Ug[i];
+  for (int i = tid; i < J + 1 + ne; i += blockDim.x) csr[i] = i <= J ? nbr_ptr[i] : nbr_idx[i - (J + 1)];
+  __syncthreads();
+  // block-local neighbour lists (in-edges in edge order, then the GAT self loop) and logits
+  for (int n = tid; n < GMAXN; n += blockDim.x) {
     int d = 0;
-    for (int e = e0; e < e1 && d < GMAXDEG; ++e) nbl[n][d++] = f0 + nbr_idx[e];
-    if (kind == 0 && d < GMAXDEG) nbl[n][d++] = n;
+    if (n < NB) {
+      const int f0 = (n / J) * J, ln = n % J;
+      for (int e = csr[ln]; e < csr[ln + 1] && d < GMAXDEG; ++e) nbl[n][d++] = f0 + csr[J + 1 + e];
+      if (kind == 0 && d < GMAXDEG) nbl[n][d++] = n;
+    }
+    for (int q = d; q < GMAXDEG; ++q) nbl[n][q] = 0;
     ndeg[n] = d;
   }
-  __syncthreads();
   if (kind == 0) {
-    for (int i = tid; i < NB * 2 * GHEADS; i += blockDim.x) {
-      const int n = i >> 3, q = i & 7;
+    for (int n = tid; n < NB; n += blockDim.x) {
       const float* xr = xs + n * ZP;
-      float s = 0.f;
-      for (int k = 0; k < GF; ++k) s += xr[k] * U[q][k];
-      al[n][q] = s;
+      float sacc[2 * GHEADS];
+#pragma unroll
+      for (int q = 0; q < 2 * GHEADS; ++q) sacc[q] = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < GF; k += 4) {
+        const float4 xv = *reinterpret_cast<const float4*>(xr + k);
+        const float xk[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 u0 = *reinterpret_cast<const float4*>(&Uk[k + j][0]);
+          const float4 u1 = *reinterpret_cast<const float4*>(&Uk[k + j][4]);
+          sacc[0] += xk[j] * u0.x; sacc[1] += xk[j] * u0.y; sacc[2] += xk[j] * u0.z; sacc[3] += xk[j] * u0.w;
+          sacc[4] += xk[j] * u1.x; sacc[5] += xk[j] * u1.y; sacc[6] += xk[j] * u1.z; sacc[7] += xk[j] * u1.w;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2 * GHEADS; ++q) al[q][n] = sacc[q];
     }
-    __syncthreads();
   }
+  __syncthreads();
 
+  // ---- segments: register-built A fragments -> MFMA
+  const int row = wave * 32 + li;
+  const int d = ndeg[row];
+  int ids[GMAXDEG];
+  {
+    const uint2 nb = *reinterpret_cast<const uint2*>(&nbl[row][0]);
+#pragma unroll
+    for (int q = 0; q < GMAXDEG; ++q) ids[q] = ((q < 4 ? nb.x : nb.y) >> (8 * (q & 3))) & 0xff;
+  }
   floatx16 acc[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -104,119 +135,113 @@ __global__ __launch_bounds__(256, 2) void graph_layer_kernel(
     for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
 
   const int nseg = kind == 0 ? GHEADS : 2;
-  const int arow = wave * 32 + li;
   for (int seg = 0; seg < nseg; ++seg) {
     const float* W = kind == 0 ? w0 + (int64_t)seg * GF * GF : (seg == 0 ? w0 : w1);
-    // B fragments: lane (li, lh) needs W[t*32 + li][kc*16 + 8*lh .. +8]; issue before the build
-    float4 bw[2][4][2];
+    const bool agg = kind == 0 || seg == 0;
+    float wq[GMAXDEG];
+    if (kind == 0) {  // edge softmax of head `seg` for this lane's row (PyG: LeakyReLU 0.2)
+      const float ad = al[GHEADS + seg][row];
+      float mx = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int kc = 0; kc < 4; ++kc) {
-        const float* p = W + (t * 32 + li) * GF + kc * 16 + lh * 8;
-        bw[t][kc][0] = *reinterpret_cast<const float4*>(p);
-        bw[t][kc][1] = *reinterpret_cast<const float4*>(p + 4);
+      for (int q = 0; q < GMAXDEG; ++q) {
+        const float sv = al[seg][ids[q]] + ad;
+        wq[q] = sv > 0.f ? sv : sv * 0.2f;
+        if (q < d) mx = fmaxf(mx, wq[q]);
       }
-    const float* A = ys;
-    if (kind == 0 || seg == 0) {
-      if (kind == 0) {  // edge softmax of head `seg`, one thread per target node
-        for (int n = tid; n < NB; n += blockDim.x) {
-          const int d = ndeg[n];
-          const float ad = al[n][GHEADS + seg];
-          float e[GMAXDEG];
-          float mx = -INFINITY;
+      float den = 0.f;
 #pragma unroll
-          for (int q = 0; q < GMAXDEG; ++q) {
-            if (q < d) {
-              float s = al[nbl[n][q]][seg] + ad;
-              e[q] = s > 0.f ? s : s * 0.2f;
-              mx = fmaxf(mx, e[q]);
-            }
-          }
-          float den = 0.f;
-#pragma unroll
-          for (int q = 0; q < GMAXDEG; ++q)
-            if (q < d) { e[q] = expf(e[q] - mx); den += e[q]; }
-          const float inv = 1.f / (den + 1e-16f);
-#pragma unroll
-          for (int q = 0; q < GMAXDEG; ++q) ew[n][q] = q < d ? e[q] * inv : 0.f;
-        }
-        __syncthreads();
+      for (int q = 0; q < GMAXDEG; ++q) {
+        wq[q] = q < d ? expf(wq[q] - mx) : 0.f;
+        den += wq[q];
       }
-      // 16 threads per node row, 4 features each: ys[n] = sum_q w_q x[nbl[n][q]]
-      for (int i = tid; i < GMAXN * 16; i += blockDim.x) {
-        const int n = i >> 4, cg = i & 15;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int d = n < NB ? ndeg[n] : 0;
-        for (int q = 0; q < d; ++q) {
-          const float w = kind == 0 ? ew[n][q] : 1.f;
-          const float4 v = *reinterpret_cast<const float4*>(xs + nbl[n][q] * ZP + cg * 4);
-          a.x += w * v.x; a.y += w * v.y; a.z += w * v.z; a.w += w * v.w;
-        }
-        *reinterpret_cast<float4*>(ys + n * ZP + cg * 4) = a;
-      }
-      __syncthreads();
+      const float inv = 1.f / (den + 1e-16f);
+#pragma unroll
+      for (int q = 0; q < GMAXDEG; ++q) wq[q] *= inv;
     } else {
-      A = xs;  // GraphConv root term
+#pragma unroll
+      for (int q = 0; q < GMAXDEG; ++q) wq[q] = q < d ? 1.f : 0.f;
     }
 #pragma unroll
     for (int kc = 0; kc < 4; ++kc) {
-      const float* p = A + arow * ZP + kc * 16 + lh * 8;
-      const float4 a0 = *reinterpret_cast<const float4*>(p);
-      const float4 a1 = *reinterpret_cast<const float4*>(p + 4);
-      const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      // B fragments for this k-chunk: lane (li, lh) needs W[t*32 + li][kc*16 + 8*lh .. +8]
+      // (L2-resident weights, requested before the gather below)
+      float4 bw[2][2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const float bf[8] = {bw[t][kc][0].x, bw[t][kc][0].y, bw[t][kc][0].z, bw[t][kc][0].w,
-                             bw[t][kc][1].x, bw[t][kc][1].y, bw[t][kc][1].z, bw[t][kc][1].w};
+        const float* p = W + (t * 32 + li) * GF + kc * 16 + lh * 8;
+        bw[t][0] = *reinterpret_cast<const float4*>(p);
+        bw[t][1] = *reinterpret_cast<const float4*>(p + 4);
+      }
+      float af[8];
+      if (agg) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) af[s] = 0.f;
+#pragma unroll
+        for (int q = 0; q < GMAXDEG; ++q) {
+          if (q < d) {
+            const float* p = xs + ids[q] * ZP + kc * 16 + lh * 8;
+            const float4 v0 = *reinterpret_cast<const float4*>(p);
+            const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
+            const float w = wq[q];
+            af[0] += w * v0.x; af[1] += w * v0.y; af[2] += w * v0.z; af[3] += w * v0.w;
+            af[4] += w * v1.x; af[5] += w * v1.y; af[6] += w * v1.z; af[7] += w * v1.w;
+          }
+        }
+      } else {  // GraphConv root term
+        const float* p = xs + row * ZP + kc * 16 + lh * 8;
+        const float4 v0 = *reinterpret_cast<const float4*>(p);
+        const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
+        af[0] = v0.x; af[1] = v0.y; af[2] = v0.z; af[3] = v0.w;
+        af[4] = v1.x; af[5] = v1.y; af[6] = v1.z; af[7] = v1.w;
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float bf[8] = {bw[t][0].x, bw[t][0].y, bw[t][0].z, bw[t][0].w,
+                             bw[t][1].x, bw[t][1].y, bw[t][1].z, bw[t][1].w};
 #pragma unroll
         for (int s = 0; s < 8; ++s)
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
       }
     }
-    __syncthreads();  // ys is rebuilt by the next segment
   }
 
-  // accumulators -> ys (pre-LayerNorm layer output)
+  // ---- epilogue on the accumulators: acc[t][q] = out[r][t*32 + li],
+  //      r = 32*wave + (q & 3) + 8*(q >> 2) + 4*lh
   const float scale = kind == 0 ? 1.f / GHEADS : 1.f;
+  const float b0 = bias[li], b1 = bias[32 + li];
+  float lw0 = 1.f, lw1 = 1.f, lb0 = 0.f, lb1 = 0.f;
+  if (norm_res) {
+    lw0 = ln_w[li]; lw1 = ln_w[32 + li];
+    lb0 = ln_b[li]; lb1 = ln_b[32 + li];
+  }
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int r = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-      const int c = t * 32 + li;
-      ys[r * ZP + c] = kind == 0 ? acc[t][q] * scale + bias[c] : acc[t][q] + bias[c];
-    }
-  __syncthreads();
-
-  // 16 lanes per node row: LayerNorm(64) by shuffles, LeakyReLU, residual, float4 stores
-  const int cg = tid & 15;
-  for (int n = tid >> 4; n < GMAXN; n += 16) {
-    const float4 o4 = *reinterpret_cast<const float4*>(ys + n * ZP + cg * 4);
-    const float o[4] = {o4.x, o4.y, o4.z, o4.w};
+  for (int q = 0; q < 16; ++q) {
+    const int r = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+    const float o0 = acc[0][q] * scale + b0, o1 = acc[1][q] * scale + b1;
+    float* yr = y + (node0 + r) * GF;
     if (!norm_res) {
-      if (n < NB) *reinterpret_cast<float4*>(y + (node0 + n) * GF + cg * 4) = o4;
+      if (r < NB) { yr[li] = o0; yr[32 + li] = o1; }
       continue;
     }
-    float s = o[0] + o[1] + o[2] + o[3];
-    for (int m = 1; m < 16; m <<= 1) s += __shfl_xor(s, m);
-    const float mean = s * (1.f / GF);
-    float ss = 0.f;
+    float sm = o0 + o1;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ss += (o[q] - mean) * (o[q] - mean);
-    for (int m = 1; m < 16; m <<= 1) ss += __shfl_xor(ss, m);
-    const float rstd = 1.f / sqrtf(ss * (1.f / GF) + 1e-5f);
-    if (n >= NB) continue;
-    float v[4];
+    for (int m = 1; m < 32; m <<= 1) sm += __shfl_xor(sm, m);
+    const float mean = sm * (1.f / GF);
+    float sv = (o0 - mean) * (o0 - mean) + (o1 - mean) * (o1 - mean);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = cg * 4 + q;
-      float t = (o[q] - mean) * rstd * ln_w[c] + ln_b[c];
-      t = t > 0.f ? t : t * slope;
-      v[q] = t + xs[n * ZP + c];
+    for (int m = 1; m < 32; m <<= 1) sv += __shfl_xor(sv, m);
+    const float rstd = 1.f / sqrtf(sv * (1.f / GF) + 1e-5f);
+    if (r >= NB) continue;
+    float u0 = (o0 - mean) * rstd * lw0 + lb0, u1 = (o1 - mean) * rstd * lw1 + lb1;
+    u0 = u0 > 0.f ? u0 : u0 * slope;
+    u1 = u1 > 0.f ? u1 : u1 * slope;
+    yr[li] = u0 + xs[r * ZP + li];
+    yr[32 + li] = u1 + xs[r * ZP + 32 + li];
+    if (pre_ln) {
+      float* pr = pre_ln + (node0 + r) * GF;
+      pr[li] = o0;
+      pr[32 + li] = o1;
     }
-    *reinterpret_cast<float4*>(y + (node0 + n) * GF + cg * 4) = make_float4(v[0], v[1], v[2], v[3]);
-    if (pre_ln) *reinterpret_cast<float4*>(pre_ln + (node0 + n) * GF + cg * 4) = o4;
   }
 }
 

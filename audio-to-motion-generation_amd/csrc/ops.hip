@@ -77,18 +77,17 @@ __global__ void interp_time_kernel(const float* x, int B, int C, int H, int W, f
 }
 
 // ---------------------------------------------------------------------- channel attention
-// One workgroup per batch element: avg/max pooling over T (one wave per channel), the
-// shared 2-layer MLP for both pooled vectors, sigmoid-sum, then the channel rescale.
-__global__ __launch_bounds__(256) void channel_attention_kernel(const float* x, int C, int T,
-                                                                const float* w1, const float* b1,
-                                                                int Cr, const float* w2,
-                                                                const float* b2, float* y,
-                                                                float* att_out) {
+// Channel weights, one workgroup per batch element: avg/max pooling over T (one wave per
+// channel, lanes along T), the shared MLP's first layer as wave-cooperative dot products over C
+// (coalesced weight rows), the second layer one thread per channel; att[b][c] out.
+__global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x, int C, int T,
+                                                                  const float* w1, const float* b1,
+                                                                  int Cr, const float* w2,
+                                                                  const float* b2, float* att) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* pavg = sm;
   float* pmax = pavg + C;
   float* hid = pmax + C;  // [2][Cr]
-  float* att = hid + 2 * Cr;
   const int b = blockIdx.x;
   const float* xb = x + (int64_t)b * C * T;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -110,13 +109,17 @@ __global__ __launch_bounds__(256) void channel_attention_kernel(const float* x, 
     }
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < 2 * Cr; j += blockDim.x) {
+  for (int j = wv; j < 2 * Cr; j += 4) {
     const int r = j % Cr;
     const float* in = j < Cr ? pavg : pmax;
     const float* wr = w1 + (int64_t)r * C;
-    float a = b1[r];
-    for (int c = 0; c < C; ++c) a += wr[c] * in[c];
-    hid[j] = a > 0.f ? a : 0.f;
+    float a = 0.f;
+    for (int c = lane; c < C; c += 64) a += wr[c] * in[c];
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    if (lane == 0) {
+      a += b1[r];
+      hid[j] = a > 0.f ? a : 0.f;
+    }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -126,13 +129,26 @@ __global__ __launch_bounds__(256) void channel_attention_kernel(const float* x, 
       a0 += wr[r] * hid[r];
       a1 += wr[r] * hid[Cr + r];
     }
-    const float s = 1.f / (1.f + expf(-a0)) + 1.f / (1.f + expf(-a1));
-    att[c] = s;
-    if (att_out) att_out[(int64_t)b * C + c] = s;
+    att[(int64_t)b * C + c] = 1.f / (1.f + expf(-a0)) + 1.f / (1.f + expf(-a1));
   }
-  __syncthreads();
-  float* yb = y + (int64_t)b * C * T;
-  for (int64_t i = threadIdx.x; i < (int64_t)C * T; i += blockDim.x) yb[i] = xb[i] * att[i / T];
+}
+
+// y[b][c][t] = x[b][c][t] * att[b][c], float4 along T when T % 4 == 0.
+__global__ void channel_scale_kernel(const float* x, const float* att, int T, int64_t n, float* y) {
+  if ((T & 3) == 0) {
+    const int64_t n4 = n >> 2;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const float a = att[(i << 2) / T];
+      float4 v = reinterpret_cast<const float4*>(x)[i];
+      v.x *= a; v.y *= a; v.z *= a; v.w *= a;
+      reinterpret_cast<float4*>(y)[i] = v;
+    }
+  } else {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+      y[i] = x[i] * att[i / T];
+  }
 }
 
 // ------------------------------------------------------------------------------ LayerNorm
@@ -484,12 +500,17 @@ int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t 
 int a2m_channel_attention_fwd_f32(const float* x, int32_t B, int32_t C, int32_t T,
                                   const float* w1, const float* b1, int32_t Cr, const float* w2,
                                   const float* b2, float* y, float* att_out, void* stream) {
-  A2M_CHECK_ARG(x && w1 && b1 && w2 && b2 && y && B > 0 && C > 0 && Cr > 0 && T > 0,
+  A2M_CHECK_ARG(x && w1 && b1 && w2 && b2 && y && att_out && B > 0 && C > 0 && Cr > 0 && T > 0,
                 "channel_attention: bad args");
-  const size_t lds = sizeof(float) * (3 * (size_t)C + 2 * Cr);
+  const size_t lds = sizeof(float) * (2 * (size_t)C + 2 * Cr);
   A2M_CHECK_ARG(lds <= 64 * 1024, "channel_attention: C too large");
-  hipLaunchKernelGGL(channel_attention_kernel, dim3(B), dim3(256), lds, as_stream(stream), x, C,
-                     T, w1, b1, Cr, w2, b2, y, att_out);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(channel_att_weights_kernel, dim3(B), dim3(256), lds, st, x, C, T, w1, b1, Cr,
+                     w2, b2, att_out);
+  A2M_LAUNCH_CHECK();
+  const int64_t n = (int64_t)B * C * T;
+  const int blocks = (int)std::min<int64_t>(cdiv(n / 4 + 1, 256), 2048);
+  hipLaunchKernelGGL(channel_scale_kernel, dim3(blocks), dim3(256), 0, st, x, att_out, T, n, y);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

@@ -94,6 +94,11 @@ int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
       }
       int rc = gemm(A, Bg, E, Ci, B * nuh * nuw, K, 1, static_cast<char*>(ws) + pack_bytes,
                     ws_bytes - pack_bytes, st);
+      if (rc == A2M_EWS) {
+        set_error("conv_dgrad: workspace too small (%zu < %zu bytes)", ws_bytes,
+                  pack_bytes + gemm_ws_bytes(Ci, B * nuh * nuw, K, 1));
+        return rc;
+      }
       if (rc) return rc;
     }
   }

@@ -124,7 +124,7 @@ size_t a2m_self_attention_ws_bytes(int32_t B, int32_t C, int32_t T);
 
 /* ChannelAttention (model_layers.py:149-174): y = x * (mlp(avg_T x) + mlp(max_T x)),
  * mlp = Linear(C, C/r) -> ReLU -> Linear(C/r, C) -> Sigmoid.  x, y contiguous [B][C][T];
- * att_out [B][C] receives the channel weights. */
+ * att_out [B][C] (required) receives the channel weights; y may alias x. */
 int a2m_channel_attention_fwd_f32(const float* x, int32_t B, int32_t C, int32_t T,
                                   const float* w1, const float* b1, int32_t Cr,
                                   const float* w2, const float* b2,
