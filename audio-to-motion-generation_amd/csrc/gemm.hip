@@ -67,6 +67,21 @@ __device__ __forceinline__ KPos kpos(const Gather& g, int k) {
   return p;
 }
 
+// p += d in the mixed radix (k0, K1, K2) with d.k1 < K1, d.k2 < K2: branch-free, no division
+// (the loaders advance their k positions by BK per k-step this way).
+__device__ __forceinline__ void kadd(const Gather& g, KPos& p, const KPos& d) {
+  p.k += d.k;
+  int k2 = p.k2 + d.k2;
+  const int c2 = k2 >= g.K2;
+  k2 -= c2 ? g.K2 : 0;
+  int k1 = p.k1 + d.k1 + c2;
+  const int c1 = k1 >= g.K1;
+  k1 -= c1 ? g.K1 : 0;
+  p.k0 += d.k0 + c1;
+  p.k1 = k1;
+  p.k2 = k2;
+}
+
 __device__ __forceinline__ void kinc(const Gather& g, KPos& p) {
   ++p.k;
   if (++p.k2 == g.K2) {
@@ -127,9 +142,14 @@ struct TileLoader {
   int kq;  // k offset of this thread inside the tile
   int nrow;  // mode 3: rows of this group that exist (0..4)
   int rdim;   // mode 3: 0 rows via r0, 1 rows along h, 2 rows along w
+  int rstep;  // mode 3: element step between consecutive rows (1, or 2 for stride-2 convs)
+  static constexpr int NKP = MODE == 3 ? NP3 : 1;
+  KPos kp[NKP];   // k position of each of this thread's k groups at the next load (modes 1-3)
+  KPos kstep;     // BK in (k0, k1, k2) digits
   float r[NREG];
 
-  __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid) {
+  __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid,
+                                       int kbeg) {
     g = &gg;
     base = gg.base + (int64_t)z * gg.bstride;
     K = KK;
@@ -139,6 +159,7 @@ struct TileLoader {
       ri[0] = row_info(gg, row0 + lrow[0], R);
       nrow = min(4, max(0, R - (row0 + lrow[0])));
       rdim = gg.R2 > 1 ? 2 : (gg.R1 > 1 ? 1 : 0);
+      rstep = rdim == 2 ? gg.ar2 : (rdim == 1 ? gg.ar1 : 1);
     } else if (MODE == 2) {
       lrow[0] = tid % BR;
       kq = (tid / BR) * KPT;
@@ -150,6 +171,11 @@ struct TileLoader {
         ri[p] = row_info(gg, row0 + lrow[p], R);
       }
       kq = (tid % QPR) * 4;
+    }
+    if (MODE != 0) {
+      kstep = kpos(gg, BK);
+#pragma unroll
+      for (int p = 0; p < NKP; ++p) kp[p] = kpos(gg, kbeg + kq + (MODE == 3 ? p * KPP : 0));
     }
   }
 
@@ -165,47 +191,56 @@ struct TileLoader {
     } else if (MODE == 1) {
 #pragma unroll
       for (int p = 0; p < NPASS; ++p) {
-        KPos kp = kpos(*g, k0 + kq);
+        KPos q = kp[0];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          r[p * 4 + j] = gather_elem(*g, base, ri[p], kp, K);
-          kinc(*g, kp);
+          r[p * 4 + j] = gather_elem(*g, base, ri[p], q, K);
+          kinc(*g, q);
         }
       }
+      kadd(*g, kp[0], kstep);
     } else if (MODE == 2) {
-      KPos kp = kpos(*g, k0 + kq);
+      KPos q = kp[0];
 #pragma unroll
       for (int j = 0; j < KPT; ++j) {
-        r[j] = gather_elem(*g, base, ri[0], kp, K);
-        kinc(*g, kp);
+        r[j] = gather_elem(*g, base, ri[0], q, K);
+        kinc(*g, q);
       }
+      kadd(*g, kp[0], kstep);
     } else {
       // 4 consecutive rows differ only in the row axis (host guarantees it): rdim 0 = rows via
       // r0 with unit stride, 1 = rows along h (sh == 1), 2 = rows along w (sw == 1), so their
-      // elements are consecutive floats.
-      const int dh = rdim == 1, dw = rdim == 2;
+      // elements are consecutive floats (rstep 1) or every other float (stride-2 convs).
+      const int dh = rdim == 1 ? rstep : 0, dw = rdim == 2 ? rstep : 0;
 #pragma unroll
       for (int p = 0; p < NP3; ++p) {
-        const KPos kp = kpos(*g, k0 + kq + p * KPP);
-        int h = ri[0].h + kp.k1 * g->bk1;
-        const int w = ri[0].w + kp.k2 * g->bk2;
-        bool kv = kp.k < K && nrow > 0;
+        const KPos q = kp[p];
+        kadd(*g, kp[p], kstep);
+        int h = ri[0].h + q.k1 * g->bk1;
+        const int w = ri[0].w + q.k2 * g->bk2;
+        bool kv = q.k < K && nrow > 0;
         if (g->divh > 1) {  // only with rdim != 1
           kv = kv && h >= 0 && (h % g->divh) == 0;
           h = h / g->divh;
         }
-        const int64_t a = (int64_t)ri[0].base + (int64_t)kp.k0 * g->sk0 + (int64_t)h * g->sh +
+        const int64_t a = (int64_t)ri[0].base + (int64_t)q.k0 * g->sk0 + (int64_t)h * g->sh +
                           (int64_t)w * g->sw;
         float4 v;
         if (kv && nrow == 4 && h >= 0 && h + 3 * dh < g->Lh && w >= 0 && w + 3 * dw < g->Lw) {
           const float4u u = *reinterpret_cast<const float4u*>(base + a);
-          v = make_float4(u.x, u.y, u.z, u.w);
+          if (rstep == 1) {
+            v = make_float4(u.x, u.y, u.z, u.w);
+          } else {  // stride-2 rows: elements a, a+2 | a+4, a+6 (second load ends at a+6)
+            const float4u u1 = *reinterpret_cast<const float4u*>(base + a + 3);
+            v = make_float4(u.x, u.z, u1.y, u1.w);
+          }
         } else {
           float e[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int hj = h + j * dh, wj = w + j * dw;
-            e[j] = (kv && j < nrow && hj >= 0 && hj < g->Lh && wj >= 0 && wj < g->Lw) ? base[a + j] : 0.f;
+            e[j] = (kv && j < nrow && hj >= 0 && hj < g->Lh && wj >= 0 && wj < g->Lw)
+                       ? base[a + j * rstep] : 0.f;
           }
           v = make_float4(e[0], e[1], e[2], e[3]);
         }
@@ -317,8 +352,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
 
   LA la;
   LB lb;
-  la.init(args.A, batch, m0, args.M, args.K, tid);
-  lb.init(args.B, batch, n0, args.N, args.K, tid);
+  la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
+  lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
 
   floatx16 acc[TM][TN];
 #pragma unroll
@@ -395,17 +430,53 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
   }
 }
 
+// Fixed-order (s = 0, 1, ...) sum of the split-K slabs + epilogue.  Four consecutive n per
+// thread (float4) when N % 4 == 0, and the slab loads of four splits are issued before their
+// adds, so the pass is bandwidth- rather than latency-bound.
 __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
   const int64_t MN = (int64_t)args.M * args.N;
+  const int S = args.splits;
+  if ((args.N & 3) == 0) {
+    const int64_t total4 = MN * batch / 4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t e = i * 4;
+      const int z = (int)(e / MN);
+      const int64_t mn = e - (int64_t)z * MN;
+      const int m = (int)(mn / args.N), n = (int)(mn - (int64_t)m * args.N);
+      const float* p = args.partial + (int64_t)z * S * MN + mn;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      int s = 0;
+      for (; s + 4 <= S; s += 4) {
+        const float4 a0 = *reinterpret_cast<const float4*>(p + (s + 0) * MN);
+        const float4 a1 = *reinterpret_cast<const float4*>(p + (s + 1) * MN);
+        const float4 a2 = *reinterpret_cast<const float4*>(p + (s + 2) * MN);
+        const float4 a3 = *reinterpret_cast<const float4*>(p + (s + 3) * MN);
+        v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
+        v.x += a1.x; v.y += a1.y; v.z += a1.z; v.w += a1.w;
+        v.x += a2.x; v.y += a2.y; v.z += a2.z; v.w += a2.w;
+        v.x += a3.x; v.y += a3.y; v.z += a3.z; v.w += a3.w;
+      }
+      for (; s < S; ++s) {
+        const float4 a = *reinterpret_cast<const float4*>(p + s * MN);
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      }
+      epi_store(args.E, z, v.x, m, epi_addr(args.E, m, n));
+      epi_store(args.E, z, v.y, m, epi_addr(args.E, m, n + 1));
+      epi_store(args.E, z, v.z, m, epi_addr(args.E, m, n + 2));
+      epi_store(args.E, z, v.w, m, epi_addr(args.E, m, n + 3));
+    }
+    return;
+  }
   const int64_t total = MN * batch;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int z = (int)(i / MN);
     const int64_t mn = i - (int64_t)z * MN;
     const int m = (int)(mn / args.N), n = (int)(mn - (int64_t)m * args.N);
-    const float* p = args.partial + (int64_t)z * args.splits * MN + mn;
+    const float* p = args.partial + (int64_t)z * S * MN + mn;
     float v = 0.f;
-    for (int s = 0; s < args.splits; ++s) v += p[s * MN];
+    for (int s = 0; s < S; ++s) v += p[s * MN];
     epi_store(args.E, z, v, m, epi_addr(args.E, m, n));
   }
 }
@@ -420,9 +491,10 @@ static int operand_mode(const Gather& g, int K) {
     // rows 4-at-a-time contiguous: plain [K][R] (rows via r0, unit stride), or stride-1 im2col
     // rows along w (R2 % 4 == 0) or along h (R2 == 1, R1 % 4 == 0), unit element stride
     const bool plain = g.R1 == 1 && g.R2 == 1 && g.sr0 == 1;
-    const bool along_w = g.R2 > 1 && g.R2 % 4 == 0 && g.ar2 == 1 && g.sw == 1 && g.divw == 1;
-    const bool along_h = g.R2 == 1 && g.R1 > 1 && g.R1 % 4 == 0 && g.ar1 == 1 && g.sh == 1 &&
-                         g.divh == 1;
+    const bool along_w = g.R2 > 1 && g.R2 % 4 == 0 && (g.ar2 == 1 || g.ar2 == 2) && g.sw == 1 &&
+                         g.divw == 1;
+    const bool along_h = g.R2 == 1 && g.R1 > 1 && g.R1 % 4 == 0 && (g.ar1 == 1 || g.ar1 == 2) &&
+                         g.sh == 1 && g.divh == 1;
     static const int allow = env_int("A2M_GEMM_MODE3", 1);
     return allow && (plain || along_w || along_h) ? 3 : 2;
   }
@@ -567,8 +639,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   A2M_LAUNCH_CHECK();
   if (tm >= 0) timing_mark(tm, 1, false, stream);
   if (p.splits > 1) {
-    const int64_t total = (int64_t)M * N * batch;
-    const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+    const int64_t total = (int64_t)M * N * batch / ((N & 3) == 0 ? 4 : 1);
+    const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, a, batch);
     A2M_LAUNCH_CHECK();
   }
