@@ -134,6 +134,70 @@ def cpu_baseline(B=8, T=64, max_s=20.0):
                       f'median of {len(times)} runs, {threads} threads'}
 
 
+# dense FLOPs of one training iteration at T=64 measured with torch's
+# FlopCounter on the reference modules: 3 G-steps x 891.7 GF + 1 D-step x 382.8 GF per 64 clips.
+TRAIN_GFLOP_PER_CLIP_T64 = (3 * 891.7 + 382.8) / 64
+
+
+def run_train(args, world, rank, dev):
+    """configs[2]: one version5_model_train.py iteration (3 G-steps + 1 D-step, Adam) over a
+    global batch split across ranks (strong scaling), DP gradient all-reduce over RCCL."""
+    from a2m.real_motion_model import SelfAttention_D, SelfAttention_G
+    from a2m.training import GANTrainer
+    Bg, T = args.batch, args.frames
+    assert Bg % world == 0, 'global batch must divide by the number of GPUs'
+    B = Bg // world
+    torch.manual_seed(1234)                           # identical initial weights on every rank
+    g = SelfAttention_G(time_steps=T, p=0.2).to(dev).train()
+    d = SelfAttention_D(out_channels=64).to(dev).train()
+    tr = GANTrainer(g, d, lr=10e-4)
+    gen = torch.Generator(device='cpu').manual_seed(100 + rank)
+    audio = torch.randn(B, T, 128, generator=gen).to(dev)
+    pose = torch.randn(B, T, 104, generator=gen).to(dev)
+
+    def step(epoch):
+        tr.iteration(audio, pose, epoch=epoch, g_freq=3, d_freq=1)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms = elapsed / args.steps * 1e3
+    flops = TRAIN_GFLOP_PER_CLIP_T64 * 1e9 * B * T / 64           # per rank
+    tf = flops * world / (ms * 1e-3) / 1e12
+    result = {
+        'metric': 'pose-frames/sec (whole node), PATS 64-frame clips batch 64, training iteration',
+        'value': round(Bg * T / (ms * 1e-3), 1), 'unit': 'pose-frames/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
+        'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32',
+        'data': 'synthetic mel/pose tensors, random-init weights',
+        'config': {'workload': 'configs[2]: version5_model_train.py iteration (G x3 + D x1, Adam, '
+                               'smoothed noisy labels), DP over ranks, per-rank BatchNorm statistics',
+                   'global_batch': Bg, 'seq_len': T, 'parallelism': f'dp{world}'},
+        'path_roofline': {'bound': 'mfma', 'achieved': round(tf, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
+                          'unit': 'TFLOP/s', 'frac': round(tf / FP32_MFMA_PEAK_TFLOPS / world, 4),
+                          'gflop_per_iteration': round(flops * world / 1e9, 1),
+                          'flop_source': 'SURVEY.md 8(d) FlopCounter count, dense'},
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def roofline_entry(gt):
     tf = gt.flops / (gt.ms_tile * 1e-3) / 1e12
     tr = load_traffic('gemm_kernel')
@@ -157,6 +221,7 @@ def main():
     ap.add_argument('--frames', type=int, default=64)
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--mode', choices=('infer', 'train'), default='infer')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -166,6 +231,8 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
+    if args.mode == 'train':
+        return run_train(args, world, rank, dev)
 
     from a2m.mel_features import log_mel_batch
     from a2m.real_motion_model import SelfAttention_G
