@@ -32,6 +32,9 @@ SIGNATURES = {
                                           P, P, P, P, F32, I32, F32, P, I64, I64, I64, P, SZ, P]),
     'a2m_convt1d_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, I32, I32, I32, I32, I32,
                                            P, P, P, P, F32, I32, F32, P, I64, I64, P, SZ, P]),
+    'a2m_convt1d_packed_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, I32, I32, I32, I32, I32,
+                                           P, P, P, P, F32, I32, F32, P, I64, I64, P, SZ, P]),
+    'a2m_convt1d_pack_f32': (ctypes.c_int, [P, I32, I32, I32, I32, I32, P, P]),
     'a2m_conv2d_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, I32,
                                           P, P, P, P, F32, I32, F32, P, I32, I32, I32, I32, P, SZ, P]),
     'a2m_mean_time_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, F32, P, P]),
@@ -40,6 +43,9 @@ SIGNATURES = {
     'a2m_self_attention_fwd_f32': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, P, P, P, P, P,
                                                   I64, P, P, P, SZ, P]),
     'a2m_self_attention_ws_bytes': (SZ, [I32, I32, I32]),
+    'a2m_stack_qkv_f32': (ctypes.c_int, [P, P, P, P, P, P, I32, P, P, P]),
+    'a2m_self_attention_packed_fwd_f32': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, P, I64, P, P, P,
+                                                         SZ, P]),
     'a2m_channel_attention_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, P, P, I32, P, P, P, P, P]),
     'a2m_layernorm_fwd_f32': (ctypes.c_int, [P, I32, I32, P, P, F32, P, I32, I64, I64, I64, P, P, P]),
     'a2m_graph_layer_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32, P, P,

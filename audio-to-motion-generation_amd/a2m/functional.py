@@ -105,8 +105,22 @@ def linear(x, w, b=None, out=None):
     return y
 
 
-def convt1d(x, w, b=None, stride=2, pad=1, out_pad=1, bn=None, act=ACT_NONE, slope=0.2, out=None):
-    """x: [B, Ci, Tin] (t contiguous), w: [Ci, Co, k]."""
+def convt_packed(w, stride, pad, cache=None):
+    """Phase-packed ConvTranspose1d weights (a2m_convt1d_pack_f32), cached in `cache`."""
+    key = _wkey((w,)) + (stride, pad)
+    if cache is not None and cache.get('key') == key:
+        return cache['w']
+    Ci, Co, ks = w.shape
+    packed = torch.empty(Ci * Co * ks, device=w.device)
+    N.check(N.lib.a2m_convt1d_pack_f32(_p(w), Ci, Co, ks, stride, pad, _p(packed), _stream()))
+    if cache is not None:
+        cache.update(key=key, w=packed)
+    return packed
+
+
+def convt1d(x, w, b=None, stride=2, pad=1, out_pad=1, bn=None, act=ACT_NONE, slope=0.2, out=None,
+            cache=None):
+    """x: [B, Ci, Tin] (t contiguous), w: [Ci, Co, k]; `cache` keeps the packed weights."""
     _check_dev(x, w, b, out)
     B, Ci, Tin = x.shape
     assert x.stride(2) == 1 and w.is_contiguous() and w.shape[0] == Ci
@@ -115,8 +129,9 @@ def convt1d(x, w, b=None, stride=2, pad=1, out_pad=1, bn=None, act=ACT_NONE, slo
     if out is None:
         out = torch.empty(B, Co, Tout, device=x.device, dtype=x.dtype)
     assert tuple(out.shape) == (B, Co, Tout) and out.stride(2) == 1
-    _with_ws(x.device, lambda wp, wn: N.lib.a2m_convt1d_fwd_f32(
-        _p(x), x.stride(0), x.stride(1), B, Ci, Tin, _p(w), _p(b), Co, ks, stride, pad, out_pad,
+    packed = convt_packed(w, stride, pad, cache)
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_convt1d_packed_fwd_f32(
+        _p(x), x.stride(0), x.stride(1), B, Ci, Tin, _p(packed), _p(b), Co, ks, stride, pad, out_pad,
         *_bn_args(bn), act, slope, _p(out), out.stride(0), out.stride(1), wp, wn, _stream()))
     return out
 
@@ -171,9 +186,39 @@ def repeat_time(x, out, scale=1.0):
 
 
 # ------------------------------------------------------------------------- attention
-def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=None):
+# Parameters updated outside torch's in-place ops (FlatAdam's HIP kernel) do not bump
+# torch's version counters; the optimiser bumps this epoch instead.  Derived weight layouts
+# (stacked QKV, phase-packed convT) are cached under (epoch, data_ptr, _version) keys.
+WEIGHTS_EPOCH = [0]
+
+
+def bump_weights_epoch():
+    WEIGHTS_EPOCH[0] += 1
+
+
+def _wkey(ts):
+    return (WEIGHTS_EPOCH[0],) + tuple(None if t is None else (t.data_ptr(), t._version) for t in ts)
+
+
+def stacked_qkv(wq, bq, wk, bk, wv, bv, cache=None):
+    """[C/4 + C][C] stacked q/k/v weights and [C/4 + C] biases (cached in `cache` if given)."""
+    key = _wkey((wq, bq, wk, bk, wv, bv))
+    if cache is not None and cache.get('key') == key:
+        return cache['w'], cache['b']
+    C = wq.shape[1]
+    w = torch.empty(C // 4 + C, C, device=wq.device)
+    b = torch.empty(C // 4 + C, device=wq.device)
+    N.check(N.lib.a2m_stack_qkv_f32(_p(wq), _p(bq), _p(wk), _p(bk), _p(wv), _p(bv), C, _p(w), _p(b),
+                                    _stream()))
+    if cache is not None:
+        cache.update(key=key, w=w, b=b)
+    return w, b
+
+
+def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=None, cache=None):
     """SelfAttention forward.  x, res, out: [B, C, T] with t contiguous and channel stride T.
-    `save`, if a dict, receives the qkv and attention intermediates."""
+    `save`, if a dict, receives the qkv and attention intermediates; `cache` (a dict owned by
+    the module) keeps the stacked QKV weights between calls."""
     _check_dev(x, wq, wk, wv, gamma, res, out)
     B, C, T = x.shape
     assert x.stride(2) == 1 and x.stride(1) == T
@@ -184,8 +229,9 @@ def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=No
         assert res.stride() == out.stride()
     qkv = torch.empty(B, C // 4 + C, T, device=x.device, dtype=x.dtype)
     attn = torch.empty(B, T, T, device=x.device, dtype=x.dtype)
-    _with_ws(x.device, lambda wp, wn: N.lib.a2m_self_attention_fwd_f32(
-        _p(x), x.stride(0), B, C, T, _p(wq), _p(bq), _p(wk), _p(bk), _p(wv), _p(bv), _p(gamma),
+    wqkv, bqkv = stacked_qkv(wq, bq, wk, bk, wv, bv, cache)
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_self_attention_packed_fwd_f32(
+        _p(x), x.stride(0), B, C, T, _p(wqkv), _p(bqkv), _p(gamma),
         _p(res), _p(out), out.stride(0), _p(qkv), _p(attn), wp, wn, _stream()))
     if save is not None:
         save['qkv'], save['attn'] = qkv, attn

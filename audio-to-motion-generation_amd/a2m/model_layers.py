@@ -97,6 +97,7 @@ class SelfAttention(nn.Module):
         self.key_conv = nn.Conv1d(in_channels, in_channels // 8, kernel_size=1)
         self.value_conv = nn.Conv1d(in_channels, in_channels, kernel_size=1)
         self.gamma = nn.Parameter(torch.zeros(1))
+        self._pack = {}   # stacked QKV weights for the eval path (functional.stacked_qkv)
 
     def weights(self):
         return (self.query_conv.weight, self.query_conv.bias, self.key_conv.weight,
@@ -106,7 +107,7 @@ class SelfAttention(nn.Module):
         """gamma * softmax-attention(x) + x (+ res): res fuses ResBlock's outer residual."""
         if _grad_path(self, x, res):
             return _autograd().self_attention(self, x, res=res, out=out)
-        return F.self_attention(x, *self.weights(), res=res, out=out)
+        return F.self_attention(x, *self.weights(), res=res, out=out, cache=self._pack)
 
 
 class ChannelAttention(nn.Module):
@@ -145,6 +146,7 @@ class ConvTranspose1D(nn.Module):
                                                  padding, output_padding)
         self.bn = nn.BatchNorm1d(out_channels)
         self.relu = nn.ReLU(inplace=True)
+        self._pack = {}   # phase-packed weights for the eval path (functional.convt_packed)
 
     def forward(self, x, out=None):
         if _grad_path(self, x):
@@ -152,7 +154,7 @@ class ConvTranspose1D(nn.Module):
         c, n = self.conv_transpose, self.bn
         return F.convt1d(x, c.weight, c.bias, c.stride[0], c.padding[0], c.output_padding[0],
                          bn=(n.weight, n.bias, n.running_mean, n.running_var, n.eps),
-                         act=F.ACT_RELU, out=out)
+                         act=F.ACT_RELU, out=out, cache=self._pack)
 
 
 class AudioEncoder(nn.Module):

@@ -54,6 +54,7 @@ class FlatAdam:
         g = self.param_groups[0]
         F.adam_(self.flat, self.flat_grad, self.exp_avg, self.exp_avg_sq, g['lr'], g['betas'][0],
                 g['betas'][1], g['eps'], g['weight_decay'], self.step_count)
+        F.bump_weights_epoch()   # the HIP update is invisible to torch's version counters
 
     def state_dict(self):
         return {'step': self.step_count, 'exp_avg': self.exp_avg.clone(), 'exp_avg_sq': self.exp_avg_sq.clone(),

@@ -77,9 +77,10 @@ __global__ void interp_time_kernel(const float* x, int B, int C, int H, int W, f
 }
 
 // ---------------------------------------------------------------------- channel attention
-// Channel weights, one workgroup per batch element: avg/max pooling over T (one wave per
-// channel, lanes along T), the shared MLP's first layer as wave-cooperative dot products over C
-// (coalesced weight rows), the second layer one thread per channel; att[b][c] out.
+// Channel weights, one workgroup per batch element, every global load independent (no
+// dependent chains): avg/max pooling one thread per channel over T, the shared MLP's first
+// layer as 4-lane partial dot products over C, the second layer one thread per channel;
+// att[b][c] = sigmoid(mlp(avg)) + sigmoid(mlp(max)).
 __global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x, int C, int T,
                                                                   const float* w1, const float* b1,
                                                                   int Cr, const float* w2,
@@ -90,33 +91,36 @@ __global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x
   float* hid = pmax + C;  // [2][Cr]
   const int b = blockIdx.x;
   const float* xb = x + (int64_t)b * C * T;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int c = wv; c < C; c += 4) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const float* p = xb + (int64_t)c * T;
     float s = 0.f, mx = -INFINITY;
-    for (int t = lane; t < T; t += 64) {
-      const float v = p[t];
-      s += v;
-      mx = fmaxf(mx, v);
+    if ((T & 3) == 0 && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+      for (int t = 0; t < T; t += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(p + t);
+        s += v.x + v.y + v.z + v.w;
+        mx = fmaxf(fmaxf(mx, fmaxf(v.x, v.y)), fmaxf(v.z, v.w));
+      }
+    } else {
+      for (int t = 0; t < T; ++t) {
+        s += p[t];
+        mx = fmaxf(mx, p[t]);
+      }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      s += __shfl_xor(s, o);
-      mx = fmaxf(mx, __shfl_xor(mx, o));
-    }
-    if (lane == 0) {
-      pavg[c] = s / (float)T;
-      pmax[c] = mx;
-    }
+    pavg[c] = s / (float)T;
+    pmax[c] = mx;
   }
   __syncthreads();
-  for (int j = wv; j < 2 * Cr; j += 4) {
+  // layer 1: output j (2*Cr of them) by 4 consecutive lanes, each over a quarter of C
+  for (int i = threadIdx.x; i < 8 * Cr; i += blockDim.x) {
+    const int j = i >> 2, part = i & 3;
     const int r = j % Cr;
     const float* in = j < Cr ? pavg : pmax;
     const float* wr = w1 + (int64_t)r * C;
     float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += wr[c] * in[c];
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-    if (lane == 0) {
+    for (int c = part; c < C; c += 4) a += wr[c] * in[c];
+    a += __shfl_xor(a, 1);
+    a += __shfl_xor(a, 2);
+    if (part == 0) {
       a += b1[r];
       hid[j] = a > 0.f ? a : 0.f;
     }
@@ -126,8 +130,9 @@ __global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x
     const float* wr = w2 + (int64_t)c * Cr;
     float a0 = b2[c], a1 = b2[c];
     for (int r = 0; r < Cr; ++r) {
-      a0 += wr[r] * hid[r];
-      a1 += wr[r] * hid[Cr + r];
+      const float w = wr[r];
+      a0 += w * hid[r];
+      a1 += w * hid[Cr + r];
     }
     att[(int64_t)b * C + c] = 1.f / (1.f + expf(-a0)) + 1.f / (1.f + expf(-a1));
   }
@@ -319,13 +324,13 @@ int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t,
   return gemm(A, Bg, E, Co, B * Tout, Ci * ks, 1, ws, ws_bytes, as_stream(stream));
 }
 
-int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
-                        int32_t Tin, const float* w, const float* bias, int32_t Co, int32_t ks,
+int a2m_convt1d_packed_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
+                        int32_t Tin, const float* packed, const float* bias, int32_t Co, int32_t ks,
                         int32_t stride, int32_t pad, int32_t out_pad, const float* bn_w,
                         const float* bn_b, const float* bn_rm, const float* bn_rv, float bn_eps,
                         int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
                         void* ws, size_t ws_bytes, void* stream) {
-  A2M_CHECK_ARG(x && w && y, "convt1d: null pointer");
+  A2M_CHECK_ARG(x && packed && y, "convt1d: null pointer");
   const int Tout = (Tin - 1) * stride - 2 * pad + ks + out_pad;
   A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && Tout > 0 && stride > 0 && pad >= 0,
                 "convt1d: bad shape");
@@ -334,18 +339,9 @@ int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, i
                 "convt1d: too large");
   // Output-phase decomposition: out[s*u + r] only sees the taps kk with
   // (r + pad - kk) % s == 0, at input u + (r + pad - kk)/s.  Each phase is a dense GEMM over
-  // K = taps_r * Ci (no zero-inserted work); weights are packed per phase as
-  // P_r[co][tap*Ci + ci] = W[ci][co][kk_tap] into the head of the workspace.
-  const size_t pack_bytes = ((size_t)Ci * Co * ks * sizeof(float) + 255) & ~size_t(255);
-  if (!ws || ws_bytes < pack_bytes) {
-    set_error("convt1d: workspace too small (%zu < %zu bytes)", ws_bytes, pack_bytes);
-    return A2M_EWS;
-  }
-  float* packed = static_cast<float*>(ws);
+  // K = taps_r * Ci (no zero-inserted work); weights packed per phase by a2m_convt1d_pack_f32
+  // as P_r[co][tap*Ci + ci] = W[ci][co][kk_tap], phases back to back.
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(convt_pack_kernel, dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Ci * Co * ks, 256), 8192)),
-                     dim3(256), 0, st, w, Ci, Co, ks, stride, pad, packed);
-  A2M_LAUNCH_CHECK();
   size_t off = 0;
   for (int r = 0; r < stride; ++r) {
     int kk0 = -1, ntap = 0;
@@ -371,12 +367,45 @@ int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, i
     Bg.divh = Bg.divw = 1; Bg.Lh = Tin; Bg.Lw = Ci; Bg.sh = 1; Bg.sw = (int)xs_c; Bg.kcontig = 0;
     Epilogue E = epi_bn(yr, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
     E.N1 = 1; E.N2 = nu; E.so0 = (int)ys_b; E.so2 = stride; E.som = (int)ys_c;
-    int rc = gemm(A, Bg, E, Co, B * nu, ntap * Ci, 1, static_cast<char*>(ws) + pack_bytes,
-                  ws_bytes - pack_bytes, st);
+    int rc = gemm(A, Bg, E, Co, B * nu, ntap * Ci, 1, ws, ws_bytes, st);
     if (rc) return rc;
     off += (size_t)Co * ntap * Ci;
   }
   return A2M_OK;
+}
+
+int a2m_convt1d_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int32_t stride,
+                         int32_t pad, float* packed, void* stream) {
+  A2M_CHECK_ARG(w && packed && Ci > 0 && Co > 0 && ks > 0 && stride > 0 && pad >= 0,
+                "convt1d_pack: bad args");
+  A2M_CHECK_ARG(fits32((int64_t)Ci * Co * ks), "convt1d_pack: too large");
+  hipLaunchKernelGGL(convt_pack_kernel,
+                     dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Ci * Co * ks, 256), 8192)),
+                     dim3(256), 0, as_stream(stream), w, Ci, Co, ks, stride, pad, packed);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
+                        int32_t Tin, const float* w, const float* bias, int32_t Co, int32_t ks,
+                        int32_t stride, int32_t pad, int32_t out_pad, const float* bn_w,
+                        const float* bn_b, const float* bn_rm, const float* bn_rv, float bn_eps,
+                        int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
+                        void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && w && y, "convt1d: null pointer");
+  // weights packed per output phase into the workspace head, then the packed path
+  const size_t pack_bytes = ((size_t)Ci * Co * ks * sizeof(float) + 255) & ~size_t(255);
+  if (!ws || ws_bytes < pack_bytes) {
+    set_error("convt1d: workspace too small (%zu < %zu bytes)", ws_bytes, pack_bytes);
+    return A2M_EWS;
+  }
+  float* packed = static_cast<float*>(ws);
+  int rc = a2m_convt1d_pack_f32(w, Ci, Co, ks, stride, pad, packed, stream);
+  if (rc) return rc;
+  return a2m_convt1d_packed_fwd_f32(x, xs_b, xs_c, B, Ci, Tin, packed, bias, Co, ks, stride, pad,
+                                    out_pad, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope, y, ys_b,
+                                    ys_c, static_cast<char*>(ws) + pack_bytes,
+                                    ws_bytes - pack_bytes, stream);
 }
 
 int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
@@ -446,12 +475,19 @@ size_t a2m_self_attention_ws_bytes(int32_t B, int32_t C, int32_t T) {
   return s;
 }
 
-int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
-                               const float* wq, const float* bq, const float* wk, const float* bk,
-                               const float* wv, const float* bv, const float* gamma,
-                               const float* res, float* y, int64_t y_bs, float* qkv,
-                               float* attn, void* ws, size_t ws_bytes, void* stream) {
-  A2M_CHECK_ARG(x && wq && wk && wv && gamma && y && qkv && attn, "self_attention: null pointer");
+int a2m_stack_qkv_f32(const float* wq, const float* bq, const float* wk, const float* bk,
+                      const float* wv, const float* bv, int32_t C, float* wqkv, float* bqkv,
+                      void* stream) {
+  A2M_CHECK_ARG(wq && wk && wv && wqkv && bqkv && C >= 8 && C % 8 == 0, "stack_qkv: bad args");
+  return stack_qkv(wq, bq, wk, bk, wv, bv, C, wqkv, bqkv, as_stream(stream));
+}
+
+int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t C,
+                                      int32_t T, const float* wqkv, const float* bqkv,
+                                      const float* gamma, const float* res, float* y, int64_t y_bs,
+                                      float* qkv, float* attn, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  A2M_CHECK_ARG(x && wqkv && bqkv && gamma && y && qkv && attn, "self_attention: null pointer");
   A2M_CHECK_ARG(B > 0 && C >= 8 && C % 8 == 0 && T > 0, "self_attention: bad shape C=%d T=%d", C, T);
   A2M_CHECK_ARG(x_bs == y_bs, "self_attention: x and y must share a layout");
   A2M_CHECK_ARG(fits32((int64_t)B * x_bs) && fits32((int64_t)B * (C + C / 4) * T) &&
@@ -460,24 +496,10 @@ int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t 
   hipStream_t st = as_stream(stream);
   const int Cq = C / 8, Cqkv = C / 4 + C;
   const int64_t qs_b = (int64_t)Cqkv * T;
-  int rc;
-  // q, k, v as ONE 1x1 convolution with the three weights stacked in the workspace head:
-  // qkv[b][0:Cq | Cq:2Cq | 2Cq:2Cq+C][t]
-  const size_t wcat_bytes = (((size_t)Cqkv * C + Cqkv) * sizeof(float) + 255) & ~size_t(255);
-  if (!ws || ws_bytes < wcat_bytes) {
-    set_error("self_attention: workspace too small (%zu < %zu bytes)", ws_bytes, wcat_bytes);
-    return A2M_EWS;
-  }
-  float* wcat = static_cast<float*>(ws);
-  float* bcat = wcat + (size_t)Cqkv * C;
-  hipLaunchKernelGGL(stack_qkv_kernel, dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Cqkv * C, 256), 8192)),
-                     dim3(256), 0, st, wq, bq, wk, bk, wv, bv, C, wcat, bcat);
-  A2M_LAUNCH_CHECK();
-  ws = static_cast<char*>(ws) + wcat_bytes;
-  ws_bytes -= wcat_bytes;
-  rc = a2m_conv1d_fwd_f32(x, x_bs, T, 1, B, C, T, wcat, bcat, Cqkv, 1, 1, 0, nullptr, nullptr,
-                          nullptr, nullptr, 0.f, A2M_ACT_NONE, 0.f, qkv, qs_b, T, 1, ws, ws_bytes,
-                          stream);
+  // q, k, v as ONE 1x1 convolution with the stacked weights: qkv[b][0:Cq | Cq:2Cq | 2Cq:][t]
+  int rc = a2m_conv1d_fwd_f32(x, x_bs, T, 1, B, C, T, wqkv, bqkv, Cqkv, 1, 1, 0, nullptr, nullptr,
+                              nullptr, nullptr, 0.f, A2M_ACT_NONE, 0.f, qkv, qs_b, T, 1, ws,
+                              ws_bytes, stream);
   if (rc) return rc;
   // scores[b][i][j] = sum_c q[b][c][i] k[b][c][j]
   Gather Aq = dense_kr(qkv, T, qs_b);
@@ -495,6 +517,29 @@ int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t 
   Eo.res1 = x;
   Eo.res2 = res;
   return gemm(Av, Ba, Eo, C, T, T, B, ws, ws_bytes, st);
+}
+
+int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
+                               const float* wq, const float* bq, const float* wk, const float* bk,
+                               const float* wv, const float* bv, const float* gamma,
+                               const float* res, float* y, int64_t y_bs, float* qkv,
+                               float* attn, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && wq && wk && wv && gamma && y && qkv && attn, "self_attention: null pointer");
+  A2M_CHECK_ARG(C >= 8 && C % 8 == 0, "self_attention: bad shape C=%d T=%d", C, T);
+  // the three weights stacked in the workspace head, then the packed path
+  const int Cqkv = C / 4 + C;
+  const size_t wcat_bytes = (((size_t)Cqkv * C + Cqkv) * sizeof(float) + 255) & ~size_t(255);
+  if (!ws || ws_bytes < wcat_bytes) {
+    set_error("self_attention: workspace too small (%zu < %zu bytes)", ws_bytes, wcat_bytes);
+    return A2M_EWS;
+  }
+  float* wcat = static_cast<float*>(ws);
+  float* bcat = wcat + (size_t)Cqkv * C;
+  int rc = stack_qkv(wq, bq, wk, bk, wv, bv, C, wcat, bcat, as_stream(stream));
+  if (rc) return rc;
+  return a2m_self_attention_packed_fwd_f32(x, x_bs, B, C, T, wcat, bcat, gamma, res, y, y_bs, qkv,
+                                           attn, static_cast<char*>(ws) + wcat_bytes,
+                                           ws_bytes - wcat_bytes, stream);
 }
 
 int a2m_channel_attention_fwd_f32(const float* x, int32_t B, int32_t C, int32_t T,

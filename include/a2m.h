@@ -83,6 +83,16 @@ int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, i
                         const float* bn_rv, float bn_eps, int32_t act, float slope,
                         float* y, int64_t ys_b, int64_t ys_c,
                         void* ws, size_t ws_bytes, void* stream);
+/* The same split in two: the per-phase weight packing (packed: Ci*Co*k floats) and the
+ * forward on packed weights (callers cache the packing while the weights are unchanged). */
+int a2m_convt1d_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int32_t stride,
+                         int32_t pad, float* packed, void* stream);
+int a2m_convt1d_packed_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
+                               int32_t Tin, const float* packed, const float* bias, int32_t Co,
+                               int32_t ks, int32_t stride, int32_t pad, int32_t out_pad,
+                               const float* bn_w, const float* bn_b, const float* bn_rm,
+                               const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
+                               int64_t ys_b, int64_t ys_c, void* ws, size_t ws_bytes, void* stream);
 
 /* AudioEncoder's Conv2d ConvNormRelu layers (model_layers.py:219-276) on contiguous
  * [B][Ci][H][W] -> [B][Co][Hout][Wout].  Only output columns [w_lo, w_hi) are computed
@@ -121,6 +131,16 @@ int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t 
                                float* y, int64_t y_bs, float* qkv_out, float* attn_out,
                                void* ws, size_t ws_bytes, void* stream);
 size_t a2m_self_attention_ws_bytes(int32_t B, int32_t C, int32_t T);
+/* The same with the q/k/v 1x1-conv weights pre-stacked by a2m_stack_qkv_f32 into
+ * wqkv [C/4 + C][C] and bqkv [C/4 + C] (callers cache these while the weights are unchanged). */
+int a2m_stack_qkv_f32(const float* wq, const float* bq, const float* wk, const float* bk,
+                      const float* wv, const float* bv, int32_t C, float* wqkv, float* bqkv,
+                      void* stream);
+int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t C,
+                                      int32_t T, const float* wqkv, const float* bqkv,
+                                      const float* gamma, const float* res, float* y, int64_t y_bs,
+                                      float* qkv_out, float* attn_out, void* ws, size_t ws_bytes,
+                                      void* stream);
 
 /* ChannelAttention (model_layers.py:149-174): y = x * (mlp(avg_T x) + mlp(max_T x)),
  * mlp = Linear(C, C/r) -> ReLU -> Linear(C/r, C) -> Sigmoid.  x, y contiguous [B][C][T];

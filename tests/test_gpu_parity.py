@@ -138,6 +138,50 @@ def test_self_attention(B, C, T):
     assert rel_err(out.cpu(), ref) < TOL
 
 
+def test_derived_weight_caches_follow_updates():
+    """The eval path caches stacked QKV and phase-packed convT weights; torch in-place updates
+    (version counters) and FlatAdam's HIP update (weights epoch) must both invalidate them."""
+    from a2m.model_layers import ConvTranspose1D, SelfAttention
+    from a2m.optim import FlatAdam
+    from oracle import model as OM
+    torch.manual_seed(3)
+    att, ct = SelfAttention(32), ConvTranspose1D(16, 8)
+    with torch.no_grad():
+        att.gamma.fill_(0.5)
+    att, ct = att.to(DEV).eval(), ct.to(DEV).eval()
+    x, xc = _rand(2, 32, 12, seed=60).to(DEV), _rand(2, 16, 6, seed=61).to(DEV)
+
+    def refs():
+        sd = {'a.' + k: v.detach().cpu() for k, v in att.state_dict().items()}
+        ra = OM.self_attention(OM.Ctx(sd), 'a', x.cpu())
+        c, n = ct.conv_transpose, ct.bn
+        rc = torch.nn.functional.conv_transpose1d(xc.cpu(), c.weight.detach().cpu(), c.bias.detach().cpu(),
+                                                  stride=2, padding=1, output_padding=1)
+        rc = torch.relu(torch.nn.functional.batch_norm(rc, n.running_mean.cpu(), n.running_var.cpu(),
+                                                       n.weight.detach().cpu(), n.bias.detach().cpu(),
+                                                       False, 0.0, 1e-5))
+        return ra, rc
+
+    with torch.no_grad():
+        for step in range(3):
+            ra, rc = refs()
+            assert rel_err(att(x).cpu(), ra) < TOL and rel_err(ct(xc).cpu(), rc) < TOL, step
+            if step == 0:   # torch in-place update
+                att.value_conv.weight.mul_(-1.5)
+                att.key_conv.weight.add_(0.05)
+                ct.conv_transpose.weight.mul_(2.0)
+    opt_a, opt_c = FlatAdam(att.parameters(), lr=0.05), FlatAdam(ct.parameters(), lr=0.05)
+    with torch.no_grad():   # re-seated parameters: caches rebuilt on the flat buffers
+        ra, rc = refs()
+        assert rel_err(att(x).cpu(), ra) < TOL and rel_err(ct(xc).cpu(), rc) < TOL
+    for o in (opt_a, opt_c):   # the HIP update leaves data_ptr and _version unchanged
+        o.flat_grad.copy_(torch.randn_like(o.flat_grad))
+        o.step()
+    with torch.no_grad():
+        ra, rc = refs()
+        assert rel_err(att(x).cpu(), ra) < TOL and rel_err(ct(xc).cpu(), rc) < TOL
+
+
 def test_channel_attention_layernorm_mean_repeat():
     from a2m import functional as F
     from oracle import model as OM
