@@ -121,4 +121,10 @@ inline Gather gather_bct(const float* x, int64_t bs, int cs, int T) {  // rows n
   return g;
 }
 
+// Fused attention core for T <= 64, C/8 <= 64 (attn_core.hip).
+bool attn_core_fits(int C, int T);
+int attn_core(const float* qkv, int64_t qs_b, int B, int C, int T, const float* gamma,
+              const float* x, int64_t x_bs, const float* res, float* y, float* attn_out,
+              hipStream_t st);
+
 }  // namespace a2m

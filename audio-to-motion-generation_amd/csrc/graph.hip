@@ -74,11 +74,20 @@ __global__ __launch_bounds__(256, 3) void graph_layer_kernel(
 
   // ---- prologue: node tile, U, CSR (independent loads, one barrier)
   const int ne = min(nbr_ptr[J], 2 * GMAXN - (J + 1));
-  for (int i = tid; i < GMAXN * (GF / 4); i += blockDim.x) {
-    const int n = i / (GF / 4), q = i % (GF / 4);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (n < NB) v = *reinterpret_cast<const float4*>(x + (node0 + n) * GF + q * 4);
-    *reinterpret_cast<float4*>(xs + n * ZP + q * 4) = v;
+  {  // node tile: all 8 float4 loads of this thread in flight before the LDS writes
+    constexpr int NL = GMAXN * (GF / 4) / 256;
+    float4 v[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * 256, n = i / (GF / 4), q = i % (GF / 4);
+      v[j] = n < NB ? *reinterpret_cast<const float4*>(x + (node0 + n) * GF + q * 4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * 256, n = i / (GF / 4), q = i % (GF / 4);
+      *reinterpret_cast<float4*>(xs + n * ZP + q * 4) = v[j];
+    }
   }
   if (kind == 0)
     for (int i = tid; i < 2 * GHEADS * GF; i += blockDim.x) Uk[i % GF][i / GF] = Ug[i];

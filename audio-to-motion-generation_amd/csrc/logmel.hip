@@ -100,7 +100,22 @@ __global__ __launch_bounds__(256) void logmel_kernel(const float* __restrict__ w
   const int clip = blockIdx.x / n_frames;
   const float* src = wave + clip * clip_stride + (int64_t)frame * hop;
   float* xs = reinterpret_cast<float*>(buf0);
-  for (int n = threadIdx.x; n < nfft; n += blockDim.x) xs[n] = n < win ? src[n] * window[n] : 0.f;
+  // all of this thread's sample (and window) loads are issued before the first LDS write
+  // (a blockDim-strided loop would wait for each load in turn)
+  constexpr int PF = 16;  // fft_len <= 4096 (host check)
+  float sv[PF], wv[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    const int n = threadIdx.x + j * 256;
+    const bool in = n < win && n < nfft;
+    sv[j] = in ? src[n] : 0.f;
+    wv[j] = in ? window[n] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    const int n = threadIdx.x + j * 256;
+    if (n < nfft) xs[n] = sv[j] * wv[j];
+  }
   __syncthreads();
 
   // Stockham autosort FFT of size M (complex), out-of-place ping-pong buffer0 <-> buffer1.
@@ -156,6 +171,7 @@ __global__ __launch_bounds__(256) void logmel_kernel(const float* __restrict__ w
     const int s = mstart[m], len = mlen[m];
     const float* wp = mw + mwoff[m];
     float acc = 0.f;
+#pragma unroll 8
     for (int q = 0; q < len; ++q) acc += wp[q] * mag[s + q];
     dst[m] = logf(acc + log_offset);
   }
@@ -254,6 +270,7 @@ int a2m_logmel_f32(const float* wave, int64_t n_clips, int64_t clip_stride, int6
   if (nf == 0 || n_clips == 0) return A2M_OK;  // empty output, like the reference's (0, n_mels)
   A2M_CHECK_ARG(wave && out && dev_plan, "logmel: null pointer");
   A2M_CHECK_ARG(n_clips * nf < (1LL << 31), "logmel: too many frames");
+  A2M_CHECK_ARG(fft_len <= 4096, "logmel: fft_len %d > 4096", fft_len);
   const size_t lds = sizeof(float) * (2 * (size_t)fft_len + fft_len / 2 + 1 + 3);
   A2M_CHECK_ARG(lds <= 160 * 1024, "logmel: fft_len %d too large for LDS", fft_len);
   hipLaunchKernelGGL(logmel_kernel, dim3((unsigned)(n_clips * nf)), dim3(256), lds,

@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cstring>
 
+#include <cstdlib>
+
 #include "a2m_internal.h"
 
 namespace a2m {
@@ -95,6 +97,7 @@ __global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x
     const float* p = xb + (int64_t)c * T;
     float s = 0.f, mx = -INFINITY;
     if ((T & 3) == 0 && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
+#pragma unroll 8
       for (int t = 0; t < T; t += 4) {
         const float4 v = *reinterpret_cast<const float4*>(p + t);
         s += v.x + v.y + v.z + v.w;
@@ -117,6 +120,7 @@ __global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x
     const float* in = j < Cr ? pavg : pmax;
     const float* wr = w1 + (int64_t)r * C;
     float a = 0.f;
+#pragma unroll 8
     for (int c = part; c < C; c += 4) a += wr[c] * in[c];
     a += __shfl_xor(a, 1);
     a += __shfl_xor(a, 2);
@@ -129,6 +133,7 @@ __global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const float* wr = w2 + (int64_t)c * Cr;
     float a0 = b2[c], a1 = b2[c];
+#pragma unroll 8
     for (int r = 0; r < Cr; ++r) {
       const float w = wr[r];
       a0 += w * hid[r];
@@ -501,6 +506,9 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
                               nullptr, nullptr, 0.f, A2M_ACT_NONE, 0.f, qkv, qs_b, T, 1, ws,
                               ws_bytes, stream);
   if (rc) return rc;
+  static const int fused_ok = std::getenv("A2M_ATTN_FUSED") ? std::atoi(std::getenv("A2M_ATTN_FUSED")) : 1;
+  if (fused_ok && attn_core_fits(C, T))
+    return attn_core(qkv, qs_b, B, C, T, gamma, x, x_bs, res, y, attn, st);
   // scores[b][i][j] = sum_c q[b][c][i] k[b][c][j]
   Gather Aq = dense_kr(qkv, T, qs_b);
   Gather Bk = dense_kr(qkv + (int64_t)Cq * T, T, qs_b);

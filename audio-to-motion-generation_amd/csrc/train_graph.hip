@@ -97,11 +97,20 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
   const int arow = wave * 32 + li;
   const int ywidth = kind == 0 ? BH * BF : BF;
 
-  for (int i = tid; i < BMAXN * (BF / 4); i += blockDim.x) {
-    const int n = i / (BF / 4), q = i % (BF / 4);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (n < NB) v = *reinterpret_cast<const float4*>(x + (node0 + n) * BF + q * 4);
-    *reinterpret_cast<float4*>(xs + n * BZP + q * 4) = v;
+  {  // node tile: all loads of this thread in flight before the LDS writes
+    constexpr int NL = BMAXN * (BF / 4) / 256;
+    float4 v[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * 256, n = i / (BF / 4), q = i % (BF / 4);
+      v[j] = n < NB ? *reinterpret_cast<const float4*>(x + (node0 + n) * BF + q * 4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * 256, n = i / (BF / 4), q = i % (BF / 4);
+      *reinterpret_cast<float4*>(xs + n * BZP + q * 4) = v[j];
+    }
   }
   if (kind == 0)
     for (int i = tid; i < 2 * BH * BF; i += blockDim.x) (&U[0][0])[i] = Ug[i];
