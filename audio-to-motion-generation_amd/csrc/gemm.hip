@@ -120,9 +120,15 @@ typedef float float4u __attribute__((ext_vector_type(4), aligned(4)));
 //   MODE 3: row-contiguous rows loaded 4 at a time (float4 along the row axis: [K][R] matrices
 //           and stride-1 conv im2col over [B][C][T]), LDS [k][row] -- no transpose on the way in;
 //           fragments are read with ds_read_b32 (8 per 32-row tile per half).
+#ifndef A2M_M3_TRANSPOSE
+#define A2M_M3_TRANSPOSE 1
+#endif
 template <int BR, int BK, int MODE>
 struct TileLoader {
-  static constexpr bool KMAJ = MODE == 3;
+  // MODE 3 with A2M_M3_TRANSPOSE: the float4 of 4 rows is written as 4 scalars into the
+  // [row][k] layout (lanes spread over k so the writes stay conflict-free), and fragments are
+  // the same two ds_read_b128 as the other modes.
+  static constexpr bool KMAJ = MODE == 3 && !A2M_M3_TRANSPOSE;
   static constexpr int LDK = BK + 4;                // [row][k] pitch
   static constexpr int LDR = BR + 4;                // [k][row] pitch: 8*LDR = 32 mod 64 banks
   static constexpr int TILE = KMAJ ? BK * LDR : BR * LDK;
@@ -154,8 +160,13 @@ struct TileLoader {
     base = gg.base + (int64_t)z * gg.bstride;
     K = KK;
     if (MODE == 3) {
-      lrow[0] = (tid % QR) * 4;
-      kq = tid / QR;
+      if (KMAJ) {
+        lrow[0] = (tid % QR) * 4;
+        kq = tid / QR;
+      } else {
+        lrow[0] = (tid / KPP) * 4;
+        kq = tid % KPP;
+      }
       ri[0] = row_info(gg, row0 + lrow[0], R);
       nrow = min(4, max(0, R - (row0 + lrow[0])));
       rdim = gg.R2 > 1 ? 2 : (gg.R1 > 1 ? 1 : 0);
@@ -250,11 +261,16 @@ struct TileLoader {
   }
 
   __device__ __forceinline__ void store(float* lds) const {
-    if (MODE == 3) {
+    if (MODE == 3 && KMAJ) {
 #pragma unroll
       for (int p = 0; p < NP3; ++p)
         *reinterpret_cast<float4*>(lds + (kq + p * KPP) * LDR + lrow[0]) =
             make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
+    } else if (MODE == 3) {
+#pragma unroll
+      for (int p = 0; p < NP3; ++p)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lds[(lrow[0] + j) * LDK + kq + p * KPP] = r[p * 4 + j];
     } else if (MODE == 2) {
       float* dst = lds + lrow[0] * LDK + kq;
 #pragma unroll
