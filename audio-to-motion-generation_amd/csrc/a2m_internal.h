@@ -121,6 +121,51 @@ inline Gather gather_bct(const float* x, int64_t bs, int cs, int T) {  // rows n
   return g;
 }
 
+// ---------------------------------------------------------------------------------------
+// Wave reductions.  __shfl_xor lowers to ds_bpermute (an LDS round trip per step, each
+// waited for); within a 16-lane row the DPP forms below are register-to-register.  After
+// xor1 + xor2 every lane of a quad holds the quad's value, so the mirror patterns (which pair
+// lane i with 7-i / 15-i) combine whole groups exactly like xor 4 / xor 8 would.
+// ---------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+
+__device__ __forceinline__ float quad_sum(float v) {
+  v += dpp_f<DPP_XOR1>(v);
+  return v + dpp_f<DPP_XOR2>(v);
+}
+__device__ __forceinline__ float quad_max(float v) {
+  v = fmaxf(v, dpp_f<DPP_XOR1>(v));
+  return fmaxf(v, dpp_f<DPP_XOR2>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v = quad_sum(v);
+  v += dpp_f<DPP_HALF_MIRROR>(v);
+  return v + dpp_f<DPP_MIRROR>(v);
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = quad_max(v);
+  v = fmaxf(v, dpp_f<DPP_HALF_MIRROR>(v));
+  return fmaxf(v, dpp_f<DPP_MIRROR>(v));
+}
+// sum over the 32 lanes of each wave half (lanes l and l^16 combined by one bpermute)
+__device__ __forceinline__ float half32_sum(float v) {
+  v = row16_sum(v);
+  return v + __shfl_xor(v, 16);
+}
+__device__ __forceinline__ float wave64_sum(float v) {
+  v = half32_sum(v);
+  return v + __shfl_xor(v, 32);
+}
+__device__ __forceinline__ float wave64_max(float v) {
+  v = row16_max(v);
+  v = fmaxf(v, __shfl_xor(v, 16));
+  return fmaxf(v, __shfl_xor(v, 32));
+}
+
 // Fused attention core for T <= 64, C/8 <= 64 (attn_core.hip).
 bool attn_core_fits(int C, int T);
 int attn_core(const float* qkv, int64_t qs_b, int B, int C, int T, const float* gamma,

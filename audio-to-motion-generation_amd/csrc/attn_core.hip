@@ -82,18 +82,42 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
   }
   __syncthreads();
 
-  // row softmax over j < T: one wave per 16 rows, lane = j
-  for (int i = wave * 16; i < wave * 16 + 16; ++i) {
-    const float sv = lane < T ? ss[i * AP + lane] : -INFINITY;
-    float mx = sv;
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    const float e = lane < T ? expf(sv - mx) : 0.f;
-    float sum = e;
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    const float a = i < T ? e * (1.f / sum) : 0.f;
-    ss[i * AP + lane] = a;
-    if (attn_out && blockIdx.x == 0 && i < T && lane < T)
-      attn_out[((int64_t)b * T + i) * T + lane] = a;
+  // row softmax over j < T: four lanes per row (16 columns each), quad reductions in DPP
+  {
+    const int i = tid >> 2, part = tid & 3;
+    float* rowp = ss + i * AP + part * 16;
+    float e[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const float4 v4 = *reinterpret_cast<const float4*>(rowp + 4 * q4);
+      e[4 * q4] = v4.x; e[4 * q4 + 1] = v4.y; e[4 * q4 + 2] = v4.z; e[4 * q4 + 3] = v4.w;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (part * 16 + q >= T) e[q] = -INFINITY;
+      mx = fmaxf(mx, e[q]);
+    }
+    mx = quad_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      e[q] = part * 16 + q < T ? expf(e[q] - mx) : 0.f;
+      sum += e[q];
+    }
+    sum = quad_sum(sum);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) e[q] = i < T ? e[q] * inv : 0.f;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4)
+      *reinterpret_cast<float4*>(rowp + 4 * q4) = make_float4(e[4 * q4], e[4 * q4 + 1], e[4 * q4 + 2], e[4 * q4 + 3]);
+    if (attn_out && blockIdx.x == 0 && i < T) {
+      float* ar = attn_out + ((int64_t)b * T + i) * T;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (part * 16 + q < T) ar[part * 16 + q] = e[q];
+    }
   }
   __syncthreads();
 

@@ -232,13 +232,8 @@ __global__ __launch_bounds__(256, 3) void graph_layer_kernel(
       if (r < NB) { yr[li] = o0; yr[32 + li] = o1; }
       continue;
     }
-    float sm = o0 + o1;
-#pragma unroll
-    for (int m = 1; m < 32; m <<= 1) sm += __shfl_xor(sm, m);
-    const float mean = sm * (1.f / GF);
-    float sv = (o0 - mean) * (o0 - mean) + (o1 - mean) * (o1 - mean);
-#pragma unroll
-    for (int m = 1; m < 32; m <<= 1) sv += __shfl_xor(sv, m);
+    const float mean = half32_sum(o0 + o1) * (1.f / GF);
+    const float sv = half32_sum((o0 - mean) * (o0 - mean) + (o1 - mean) * (o1 - mean));
     const float rstd = 1.f / sqrtf(sv * (1.f / GF) + 1e-5f);
     if (r >= NB) continue;
     float u0 = (o0 - mean) * rstd * lw0 + lb0, u1 = (o1 - mean) * rstd * lw1 + lb1;
