@@ -31,14 +31,14 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(float* x, int rows, i
   float* p = x + (int64_t)row * n;
   float mx = -INFINITY;
   for (int j = lane; j < n; j += 64) mx = fmaxf(mx, p[j]);
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  mx = wave64_max(mx);
   float s = 0.f;
   for (int j = lane; j < n; j += 64) {
     const float e = expf(p[j] - mx);
     p[j] = e;
     s += e;
   }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave64_sum(s);
   const float inv = 1.f / s;
   for (int j = lane; j < n; j += 64) p[j] *= inv;
 }
@@ -122,8 +122,7 @@ __global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x
     float a = 0.f;
 #pragma unroll 8
     for (int c = part; c < C; c += 4) a += wr[c] * in[c];
-    a += __shfl_xor(a, 1);
-    a += __shfl_xor(a, 2);
+    a = quad_sum(a);
     if (part == 0) {
       a += b1[r];
       hid[j] = a > 0.f ? a : 0.f;
@@ -180,7 +179,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int R, i
     v[q] = d < D ? p[d] : 0.f;
     s += v[q];
   }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave64_sum(s);
   const float mean = s / (float)D;
   float ss = 0.f;
 #pragma unroll
@@ -189,7 +188,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int R, i
     const float c = d < D ? v[q] - mean : 0.f;
     ss += c * c;
   }
-  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  ss = wave64_sum(ss);
   const float rstd = 1.f / sqrtf(ss / (float)D + eps);
   float* yr = y + (int64_t)(row / T) * ys_b + (int64_t)(row % T) * ys_t;
 #pragma unroll
@@ -211,7 +210,7 @@ __global__ void mean_time_kernel(const float* x, int64_t xs_b, int64_t xs_c, int
   const float* p = x + (int64_t)(i / C) * xs_b + (int64_t)(i % C) * xs_c;
   float s = 0.f;
   for (int t = lane; t < T; t += 64) s += p[t];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave64_sum(s);
   if (lane == 0) y[i] = scale * (s / (float)T);
 }
 

@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void attn_softmax_bwd_kernel(const float* attn
   float* gr = g + (int64_t)row * T;
   float s = 0.f;
   for (int j = lane; j < T; j += 64) s += a[j] * gr[j];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave64_sum(s);
   const float gm = gamma[0];
   for (int j = lane; j < T; j += 64) gr[j] = gm * a[j] * (gr[j] - s);
   if (lane == 0) rowdot[row] = s;

@@ -207,12 +207,12 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
     float dov[4];
     if (norm_res) {
       float s = o[0] + o[1] + o[2] + o[3];
-      for (int m = 1; m < 16; m <<= 1) s += __shfl_xor(s, m);
+      s = row16_sum(s);
       const float mean = s * (1.f / BF);
       float ss = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) ss += (o[q] - mean) * (o[q] - mean);
-      for (int m = 1; m < 16; m <<= 1) ss += __shfl_xor(ss, m);
+      ss = row16_sum(ss);
       const float rstd = 1.f / sqrtf(ss * (1.f / BF) + 1e-5f);
       float sg = 0.f, sgx = 0.f, oh[4];
 #pragma unroll
@@ -227,10 +227,8 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
         sg += g4[q];
         sgx += g4[q] * oh[q];
       }
-      for (int m = 1; m < 16; m <<= 1) {
-        sg += __shfl_xor(sg, m);
-        sgx += __shfl_xor(sgx, m);
-      }
+      sg = row16_sum(sg);
+      sgx = row16_sum(sgx);
       const float mg = sg * (1.f / BF), mgx = sgx * (1.f / BF);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -275,7 +273,7 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
             const float4 xv = *reinterpret_cast<const float4*>(xs + nbl[n][q] * BZP + c4 * 4);
             v = g.x * xv.x + g.y * xv.y + g.z * xv.z + g.w * xv.w;
           }
-          for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m);
+          v = row16_sum(v);
           if (c4 == 0) dsb[n][q] = v;
         }
       }

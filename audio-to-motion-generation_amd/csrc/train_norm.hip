@@ -266,10 +266,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* dy, int
         g[q] = xh[q] = 0.f;
       }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      sg += __shfl_xor(sg, o);
-      sgx += __shfl_xor(sgx, o);
-    }
+    sg = wave64_sum(sg);
+    sgx = wave64_sum(sgx);
     const float mg = sg / (float)D, mgx = sgx / (float)D;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
