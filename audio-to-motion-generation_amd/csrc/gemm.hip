@@ -22,7 +22,7 @@ namespace a2m {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// K-tile depth: 16 or 32 (runtime choice, A2M_GEMM_BK).  LDS row pitch BK+4 floats keeps the
+// K-tile depth BK = 32 (the kernels are templated on it).  LDS row pitch BK+4 floats keeps the
 // per-lane ds_read_b128 fragment reads conflict-free (row*pitch mod 64 banks distinct over 16 rows).
 
 struct GemmArgs {
@@ -118,8 +118,10 @@ typedef float float4u __attribute__((ext_vector_type(4), aligned(4)));
 //   MODE 1: k-contiguous gather (scalar loads), LDS [row][k].
 //   MODE 2: row-contiguous gather (scalar loads, lanes along rows), LDS [row][k].
 //   MODE 3: row-contiguous rows loaded 4 at a time (float4 along the row axis: [K][R] matrices
-//           and stride-1 conv im2col over [B][C][T]), LDS [k][row] -- no transpose on the way in;
-//           fragments are read with ds_read_b32 (8 per 32-row tile per half).
+//           and stride-1/2 conv im2col over [B][C][T]); written transposed into LDS [row][k]
+//           (A2M_M3_TRANSPOSE, default) or kept k-major with ds_read_b32 fragments.
+//   MODE 4: k-contiguous runs (the inner k digit has unit stride, K2 % 4 == 0: wgrad operands
+//           over [B][C][T]) loaded 4 k at a time, LDS [row][k].
 #ifndef A2M_M3_TRANSPOSE
 #define A2M_M3_TRANSPOSE 1
 #endif
@@ -199,6 +201,38 @@ struct TileLoader {
         if (ri[p].valid && k < K) v = *reinterpret_cast<const float4*>(base + ri[p].base + k);
         r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
       }
+    } else if (MODE == 4) {
+      // k-contiguous runs: the 4 k of a quad share k0, k1 (host: K2 % 4 == 0) and sit at
+      // consecutive addresses (bk2 * sw == 1), so one float4 unless the quad crosses an edge
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p) {
+        const KPos q = kp[0];
+        int h = ri[p].h + q.k1 * g->bk1;
+        const int w = ri[p].w + q.k2;
+        bool hv = ri[p].valid && h >= 0;
+        if (g->divh > 1) {
+          hv = hv && (h % g->divh) == 0;
+          h = h / g->divh;
+        }
+        hv = hv && h < g->Lh;
+        float4 v;
+        if (hv && q.k + 3 < K && w >= 0 && w + 3 < g->Lw) {
+          const float4u u = *reinterpret_cast<const float4u*>(
+              base + ri[p].base + (int64_t)q.k0 * g->sk0 + (int64_t)h * g->sh + w);
+          v = make_float4(u.x, u.y, u.z, u.w);
+        } else {
+          KPos qq = q;
+          float e[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            e[j] = gather_elem(*g, base, ri[p], qq, K);
+            kinc(*g, qq);
+          }
+          v = make_float4(e[0], e[1], e[2], e[3]);
+        }
+        r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
+      }
+      kadd(*g, kp[0], kstep);
     } else if (MODE == 1) {
 #pragma unroll
       for (int p = 0; p < NPASS; ++p) {
@@ -518,7 +552,10 @@ static int operand_mode(const Gather& g, int K) {
                      g.sh == 0 && g.sw == 0 && g.ch == 0 && g.cw == 0 && g.divh == 1 && g.divw == 1;
   const bool aligned = (reinterpret_cast<uintptr_t>(g.base) % 16 == 0) && (g.sr0 % 4 == 0) &&
                        (g.bstride % 4 == 0) && (K % 4 == 0);
-  return dense && aligned ? 0 : 1;
+  if (dense && aligned) return 0;
+  static const int allow4 = env_int("A2M_GEMM_MODE4", 1);
+  const bool runs = g.K2 % 4 == 0 && g.bk2 == 1 && g.sw == 1 && g.divw == 1;
+  return allow4 && runs ? 4 : 1;
 }
 
 struct Plan {
@@ -526,12 +563,9 @@ struct Plan {
 };
 
 // Tile / split-K choice: fill the 256 CUs with >= ~2 workgroups each while keeping every
-// K-slice >= 256 deep.  A2M_GEMM_TILE=64|128, A2M_GEMM_SPLIT=n, A2M_GEMM_BK=16|32 and
+// K-slice >= 256 deep.  A2M_GEMM_TILE=64|128, A2M_GEMM_SPLIT=n and
 // A2M_GEMM_XCD=g (XCD-aware remap, g M-tiles per group; 0 = off) override (experiments).
-static int gemm_bk() {
-  static const int bk = env_int("A2M_GEMM_BK", 32) == 16 ? 16 : 32;
-  return bk;
-}
+static int gemm_bk() { return 32; }   // (BK = 16 measured slower end to end; not instantiated)
 
 static int gemm_xcd_group() {
   static const int g = env_int("A2M_GEMM_XCD", 0);
@@ -571,10 +605,11 @@ static void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
   if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_>), grid, dim3(256), 0, st, a); return; }
-  A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3)
-  A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2) A2M_L(1, 3)
-  A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3)
-  A2M_L(3, 0) A2M_L(3, 1) A2M_L(3, 2) A2M_L(3, 3)
+  A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3) A2M_L(0, 4)
+  A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2) A2M_L(1, 3) A2M_L(1, 4)
+  A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3) A2M_L(2, 4)
+  A2M_L(3, 0) A2M_L(3, 1) A2M_L(3, 2) A2M_L(3, 3) A2M_L(3, 4)
+  A2M_L(4, 0) A2M_L(4, 1) A2M_L(4, 2) A2M_L(4, 3) A2M_L(4, 4)
 #undef A2M_L
 }
 
@@ -645,13 +680,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d\n", M, N,
                  K, batch, p.bm, p.bk, p.splits, ma, mb);
   const long tm = g_timing ? timing_open(2.0 * M * N * (double)K * batch, stream) : -1;
-  if (p.bk == 32) {
-    if (p.bm == 128) launch_tile<128, 128, 32>(a, ma, mb, batch, stream);
-    else launch_tile<64, 64, 32>(a, ma, mb, batch, stream);
-  } else {
-    if (p.bm == 128) launch_tile<128, 128, 16>(a, ma, mb, batch, stream);
-    else launch_tile<64, 64, 16>(a, ma, mb, batch, stream);
-  }
+  if (p.bm == 128) launch_tile<128, 128, 32>(a, ma, mb, batch, stream);
+  else launch_tile<64, 64, 32>(a, ma, mb, batch, stream);
   A2M_LAUNCH_CHECK();
   if (tm >= 0) timing_mark(tm, 1, false, stream);
   if (p.splits > 1) {

@@ -281,20 +281,34 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* dy, int
 }
 
 // out[j] (+)= sum_i part[i*stride + j], i < rows, j < cols (fixed order)
-__global__ void reduce_cols_kernel(const float* part, int rows, int stride, int cols, float* out,
-                                   int accumulate) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= cols) return;
+// out[j] (+)= sum_i part[i*stride + j] in double.  One 1024-thread workgroup per 64 columns:
+// 16 row groups per column, each summing rows g, g+16, ... with 8 loads in flight, then the 16
+// partials combined in a fixed order (bitwise reproducible).
+__global__ __launch_bounds__(1024) void reduce_cols_kernel(const float* part, int rows, int stride,
+                                                           int cols, float* out, int accumulate) {
+  __shared__ double red[16][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + c;
   double s = 0.0;
-  for (int i = 0; i < rows; ++i) s += part[(int64_t)i * stride + j];
-  out[j] = (float)(accumulate ? out[j] + s : s);
+  if (j < cols) {
+#pragma unroll 8
+    for (int i = g; i < rows; i += 16) s += part[(int64_t)i * stride + j];
+  }
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && j < cols) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][c];
+    out[j] = (float)(accumulate ? out[j] + t : t);
+  }
 }
 
 static int bn_slices(int64_t N) { return (int)cdiv(N, kSlice); }
 
 int reduce_cols(const float* part, int rows, int stride, int cols, float* out, int accumulate,
                 hipStream_t st) {
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(cols, 256)), dim3(256), 0, st, part,
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(cols, 64)), dim3(1024), 0, st, part,
                      rows, stride, cols, out, accumulate);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
@@ -396,10 +410,10 @@ int a2m_layernorm_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_d, int64_t
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(blocks), dim3(256), sizeof(float) * 8 * D, st, dy,
                      dys_b, dys_d, dys_t, T, x, R, D, w, mean, rstd, dx, part);
   A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(D, 256)), dim3(256), 0, st, part, blocks,
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(D, 64)), dim3(1024), 0, st, part, blocks,
                      2 * D, D, dw, 0);
   A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(D, 256)), dim3(256), 0, st, part + D,
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(D, 64)), dim3(1024), 0, st, part + D,
                      blocks, 2 * D, D, db, 0);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
