@@ -280,6 +280,52 @@ int stack_qkv(const float* wq, const float* bq, const float* wk, const float* bk
   return A2M_OK;
 }
 
+// im2col for conv1d over [B][C][T] (t contiguous): col[b*Tout + t][ci*ks + tap] =
+// x[b][ci][t*s + tap - pad] (0 outside).  One workgroup per (64 output steps, 16 channels,
+// clip): the input window is staged through LDS with coalesced row loads, and every output row
+// segment (16*ks contiguous floats) is written by consecutive lanes.  The dense [N][K] result is
+// the engine's fastest operand form (mode 0), which the [B][C][T] gather cannot match.
+constexpr int I2C_T = 64, I2C_C = 16, I2C_SPAN = 2 * (I2C_T - 1) + 8;
+__global__ __launch_bounds__(256) void im2col1d_kernel(const float* __restrict__ x, int64_t xs_b,
+                                                       int64_t xs_c, int Ci, int Tin, int Tout,
+                                                       int ks, int stride, int pad,
+                                                       float* __restrict__ col) {
+  __shared__ float win[I2C_C][I2C_SPAN + 1];
+  const int t0 = blockIdx.x * I2C_T, ci0 = blockIdx.y * I2C_C, b = blockIdx.z;
+  const int span = (I2C_T - 1) * stride + ks;
+  const int tin0 = t0 * stride - pad;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* xb = x + (int64_t)b * xs_b;
+  // wave w stages channels w, w+4, w+8, w+12 (lanes along t): all loads issued first
+  float v[4][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = wave + 4 * j;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int u = lane + 64 * q, ti = tin0 + u;
+      v[j][q] = (u < span && ci0 + c < Ci && ti >= 0 && ti < Tin) ? xb[(int64_t)(ci0 + c) * xs_c + ti] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (lane + 64 * q < span) win[wave + 4 * j][lane + 64 * q] = v[j][q];
+  __syncthreads();
+  // wave w writes rows w, w+4, ...; lane owns the fixed k offsets kk = lane, lane + 64
+  const int K = Ci * ks, seg = min(I2C_C, Ci - ci0) * ks;
+  const int nt = min(I2C_T, Tout - t0);
+  const int kk0 = lane, kk1 = lane + 64;
+  const int c0 = kk0 / ks, tap0 = kk0 - c0 * ks, c1 = kk1 / ks, tap1 = kk1 - c1 * ks;
+  float* base = col + ((int64_t)b * Tout + t0) * K + (int64_t)ci0 * ks;
+  for (int tt = wave; tt < nt; tt += 4) {
+    float* row = base + (int64_t)tt * K;
+    if (kk0 < seg) row[kk0] = win[c0][tt * stride + tap0];
+    if (kk1 < seg) row[kk1] = win[c1][tt * stride + tap1];
+  }
+}
+
 int softmax_rows(float* x, int rows, int n, hipStream_t st) {
   if (rows == 0) return A2M_OK;
   hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, st, x,
@@ -311,6 +357,30 @@ int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t,
                 "conv1d: tensor too large for 32-bit offsets");
   Gather A = dense_rk(w, Ci * ks);
   Gather Bg{};
+  static const int im2col_on = std::getenv("A2M_CONV_IM2COL") ? std::atoi(std::getenv("A2M_CONV_IM2COL")) : 1;
+  const int64_t K = (int64_t)Ci * ks, N = (int64_t)B * Tout;
+  static const int im2col_min_co = std::getenv("A2M_CONV_IM2COL_MINCO") ? std::atoi(std::getenv("A2M_CONV_IM2COL_MINCO")) : 128;
+  if (im2col_on && ks > 1 && ks <= 8 && stride <= 2 && Co >= im2col_min_co && xs_t == 1 && K % 4 == 0 &&
+      N * K < (1LL << 31)) {
+    // explicit im2col into the workspace head, then a dense x dense GEMM
+    const size_t col_bytes = ((size_t)(N * K) * sizeof(float) + 255) & ~size_t(255);
+    const size_t need = col_bytes + gemm_ws_bytes(Co, (int)N, (int)K, 1);
+    if (!ws || ws_bytes < need) {
+      set_error("conv1d: workspace too small (%zu < %zu bytes)", ws_bytes, need);
+      return A2M_EWS;
+    }
+    float* col = static_cast<float*>(ws);
+    hipStream_t st = as_stream(stream);
+    dim3 grid((unsigned)cdiv(Tout, I2C_T), (unsigned)cdiv(Ci, I2C_C), (unsigned)B);
+    hipLaunchKernelGGL(im2col1d_kernel, grid, dim3(256), 0, st, x, xs_b, xs_c, Ci, Tin, Tout, ks,
+                       stride, pad, col);
+    A2M_LAUNCH_CHECK();
+    Bg = dense_rk(col, (int)K);
+    Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+    E.N1 = 1; E.N2 = Tout; E.so0 = (int)ys_b; E.so1 = 0; E.so2 = (int)ys_t; E.som = (int)ys_c;
+    return gemm(A, Bg, E, Co, (int)N, (int)K, 1, static_cast<char*>(ws) + col_bytes,
+                ws_bytes - col_bytes, st);
+  }
   if (ks == 1 && pad == 0 && stride == 1 && xs_b == (int64_t)Tin * xs_t) {
     // rows n = b*T + t are uniformly strided: plain [N][Ci] (k-major when xs_c == 1)
     Bg = xs_c == 1 ? dense_rk(x, (int)xs_t) : dense_kr(x, (int)xs_c);
