@@ -360,7 +360,8 @@ int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t,
   static const int im2col_on = std::getenv("A2M_CONV_IM2COL") ? std::atoi(std::getenv("A2M_CONV_IM2COL")) : 1;
   const int64_t K = (int64_t)Ci * ks, N = (int64_t)B * Tout;
   static const int im2col_min_co = std::getenv("A2M_CONV_IM2COL_MINCO") ? std::atoi(std::getenv("A2M_CONV_IM2COL_MINCO")) : 128;
-  if (im2col_on && ks > 1 && ks <= 8 && stride <= 2 && Co >= im2col_min_co && xs_t == 1 && K % 4 == 0 &&
+  static const int im2col_1x1 = std::getenv("A2M_CONV_IM2COL_1X1") ? std::atoi(std::getenv("A2M_CONV_IM2COL_1X1")) : 0;
+  if (im2col_on && (ks > 1 || im2col_1x1) && ks <= 8 && stride <= 2 && Co >= im2col_min_co && xs_t == 1 && K % 4 == 0 &&
       N * K < (1LL << 31)) {
     // explicit im2col into the workspace head, then a dense x dense GEMM
     const size_t col_bytes = ((size_t)(N * K) * sizeof(float) + 255) & ~size_t(255);
