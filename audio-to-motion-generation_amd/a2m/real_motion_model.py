@@ -238,3 +238,8 @@ class SelfAttention_D(_GraphTopology):
         F.repeat_time(g, cat[:, C:])
         lg = F.conv1d(cat, self.logits.weight, self.logits.bias, 1, 1)
         return lg.transpose(-1, -2).squeeze(-1), []
+
+
+# generate_motion_video.py:18 imports `Speech2Gesture_G` from a module absent from the reference;
+# the generator it loads (MODEL_PATH_G, saved by version5_model_train.py:510-516) is this one.
+Speech2Gesture_G = SelfAttention_G

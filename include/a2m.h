@@ -300,6 +300,24 @@ int a2m_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                  void* stream);
 
+/* ---- Pose normalisation and evaluation ----
+ * Poses are [n_frames][104] planar (x of 52 joints, then y), neck = joint 0.
+ * a2m_pose_moments_f32: acc[0:104] += mean over the frames of (x - neck) (necksub = 1) or x,
+ * acc[104:208] += mean of squares, fp64 -- one batch of normalization_tools.get_mean_std[_necksub]
+ * (normalization_tools.py:7-45); the caller averages over batches.
+ * a2m_pose_normalize_f32: ((x - neck) - mean) / std  (version5_model_train.py:298-304).
+ * a2m_pose_denormalize_f32: x * std + mean  (generate_motion_video.py:259-260).
+ * a2m_pck_f32: pred, gt [N][2][K] -> out[N] = fraction of keypoints with
+ * |gt - pred| <= alpha * max(x extent, y extent) of gt (motion_evaluation.py:4-22). */
+int a2m_pose_moments_f32(const float* pose, int64_t n_frames, int32_t necksub, double* acc,
+                         void* stream);
+int a2m_pose_normalize_f32(const float* pose, int64_t n_frames, const float* mean, const float* std_,
+                           float* out, void* stream);
+int a2m_pose_denormalize_f32(const float* pose, int64_t n_frames, const float* mean,
+                             const float* std_, float* out, void* stream);
+int a2m_pck_f32(const float* pred, const float* gt, int32_t N, int32_t K, double alpha,
+                double* out, void* stream);
+
 /* Measurement hook (bench.py): while enabled, every launch of the implicit-GEMM engine is
  * bracketed by HIP events on its stream; _end synchronises them and returns the launch count,
  * the launches' algorithmic FLOPs (2*M*N*K*batch), the summed tile-kernel time and the summed

@@ -1,0 +1,76 @@
+"""GPU parity of the normalisation and PCK rows against the
+reference's own outputs (tests/golden/eval_norm.npz, made by oracle/make_fixtures_eval.py)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+class _Loader:
+    def __init__(self, batches):
+        self.train = [{'pose/data': b} for b in batches]
+
+
+@pytest.mark.parametrize('on_device', [False, True])
+def test_mean_std_vs_reference(on_device):
+    from a2m import normalization as NZ
+    z = golden('eval_norm.npz')
+    batches = [torch.from_numpy(z[f'batch{i}']) for i in range(int(z['n_batches']))]
+    if on_device:
+        batches = [b.cuda() for b in batches]
+    for fn, tag in ((NZ.get_mean_std_necksub, 'necksub'), (NZ.get_mean_std, 'plain')):
+        mean, std = fn(_Loader(batches))
+        rm, rs = z[f'mean_{tag}'], z[f'std_{tag}']
+        assert np.abs(mean.cpu().numpy() - rm).max() <= 1e-5 * np.abs(rm).max(), tag
+        assert np.abs(std.cpu().numpy() - rs).max() <= 1e-5 * np.abs(rs).max(), tag
+
+
+def test_normalize_denormalize():
+    from a2m import normalization as NZ
+    z = golden('eval_norm.npz')
+    mean, std = torch.from_numpy(z['mean_necksub']).cuda(), torch.from_numpy(z['std_necksub']).cuda()
+    pose = torch.from_numpy(z['batch0']).cuda()
+    nrm = NZ.necksub_normalize(pose, mean, std)
+    assert np.abs(nrm.cpu().numpy() - z['normalized0']).max() <= 1e-5
+    assert np.abs(nrm.cpu().numpy()[..., [0, 52]]).max() <= 1e-6 * np.abs(z['mean_necksub']).max() + 1e-6
+    den = NZ.denormalize(nrm, mean, std)
+    assert np.abs(den.cpu().numpy() - z['denormalized0']).max() <= 1e-4
+
+
+@pytest.mark.parametrize('K', [52, 48])
+def test_pck_vs_reference(K):
+    from a2m.evaluation import compute_pck
+    z = golden('eval_norm.npz')
+    for alpha, tag in ((0.2, 'a02'), (0.1, 'a01')):
+        out = compute_pck(z[f'pck{K}_pred'], z[f'pck{K}_gt'], alpha)
+        assert isinstance(out, np.ndarray) and np.array_equal(out, z[f'pck{K}_{tag}']), (K, tag)
+    dev = compute_pck(torch.from_numpy(z[f'pck{K}_pred']).cuda(), torch.from_numpy(z[f'pck{K}_gt']).cuda())
+    assert dev.is_cuda and np.array_equal(dev.cpu().numpy(), z[f'pck{K}_a02'])
+    with pytest.raises(ValueError):
+        compute_pck(z[f'pck{K}_pred'][:, :1], z[f'pck{K}_gt'][:, :1])
+
+
+def test_inference_surface(tmp_path, g_state):
+    """generate_motion_video.py's flow: Speech2Gesture_G, checkpoint round trip, generate with
+    de-normalisation == generator output * std + mean."""
+    from a2m import inference
+    from a2m.real_motion_model import SelfAttention_G, Speech2Gesture_G
+    assert Speech2Gesture_G is SelfAttention_G
+    g = Speech2Gesture_G(p=0.0)
+    g.load_state_dict(g_state, strict=False)
+    path = tmp_path / 'gen.pth'
+    torch.save(g.state_dict(), path)
+    g2 = inference.load_generator(str(path), p=0.0)
+    z = golden('g_eval_b2t64.npz')
+    audio = torch.from_numpy(z['audio']).cuda()
+    raw = inference.generate(g2, audio)
+    assert np.abs(raw.cpu().numpy() - z['pose']).max() <= 1e-4 * np.abs(z['pose']).max()
+    zn = golden('eval_norm.npz')
+    mean, std = torch.from_numpy(zn['mean_necksub']), torch.from_numpy(zn['std_necksub'])
+    den = inference.generate(g2, audio, mean, std)
+    ref = z['pose'].astype(np.float64) * zn['std_necksub'] + zn['mean_necksub']
+    assert np.abs(den.cpu().numpy() - ref).max() <= 1e-4 * np.abs(ref).max()
+    assert tuple(inference.planar_frames(den).shape) == (2, 64, 2, 52)

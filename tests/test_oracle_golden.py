@@ -113,3 +113,18 @@ def test_train_step_oracle(g_state, d_state):
         ref = t['gG_val'][i][ok]
         scale = max(np.sqrt(t['gG_sumsq'][i] / max(g.size, 1)), np.abs(ref).max(), 1e-12)
         assert np.abs(g[ix[ok]] - ref).max() / scale < 2e-3, n
+
+
+def test_eval_norm_oracle_vs_reference():
+    """oracle/evaluation.py against the reference's normalization_tools and compute_pck
+    outputs (tests/golden/eval_norm.npz, oracle/make_fixtures_eval.py)."""
+    from oracle import evaluation as OE
+    z = golden('eval_norm.npz')
+    batches = [z[f'batch{i}'] for i in range(int(z['n_batches']))]
+    mean, std = OE.mean_std_necksub(batches)
+    assert np.abs(mean - z['mean_necksub']).max() <= 1e-5 * np.abs(z['mean_necksub']).max()
+    assert np.abs(std - z['std_necksub']).max() <= 1e-5 * np.abs(z['std_necksub']).max()
+    assert std[0] == 1.0 and std[52] == 1.0
+    for K in (52, 48):
+        for alpha, tag in ((0.2, 'a02'), (0.1, 'a01')):
+            assert np.array_equal(OE.compute_pck(z[f'pck{K}_pred'], z[f'pck{K}_gt'], alpha), z[f'pck{K}_{tag}'])

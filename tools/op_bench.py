@@ -84,6 +84,23 @@ def dense_nn_case(M, N, K):
     return us, 2.0 * M * N * K
 
 
+def norm_case(B=256, T=64):
+    from a2m import normalization as NZ
+    pose = torch.randn(B, T, 104, device=dev)
+    mean, std = torch.randn(104, device=dev), torch.rand(104, device=dev) + 0.5
+    out = torch.empty_like(pose)
+    us = timeit(lambda: NZ.necksub_normalize(pose, mean, std, out=out))
+    return us, 2.0 * pose.numel() * 4 / 1e6 * 1e6  # bytes moved (reported as 'TFLOP/s' column = MB/us)
+
+
+def pck_case(N=4096, K=52):
+    from a2m.evaluation import compute_pck
+    gt = torch.randn(N, 2, K, device=dev)
+    pred = gt + 0.1 * torch.randn_like(gt)
+    us = timeit(lambda: compute_pck(pred, gt))
+    return us, 2.0 * gt.numel() * 4
+
+
 CASES = {
     'unet.d0 256->512 k3 T64': lambda: conv_case(64, 256, 512, 64, 3, 1, 1),
     'unet.d1 512->512 k4s2 T64': lambda: conv_case(64, 512, 512, 64, 4, 2, 1),
@@ -107,6 +124,8 @@ CASES = {
     'dense d2 1024x2048x1536': lambda: dense_case(1024, 2048, 1536),
     'dense dec 256x4096x768': lambda: dense_case(256, 4096, 768),
     'gat body': lambda: graph_case(10, 0, 0),
+    'bytes: pose normalize B256 T64': norm_case,
+    'bytes: pck N4096 K52': pck_case,
     'gat hand': lambda: graph_case(42, 10, 0),
     'gconv hand': lambda: graph_case(42, 10, 1),
 }
