@@ -5,6 +5,7 @@
 //   normalize    version5_model_train.py:298-304: ((x - neck) - mean) / std, planar [2][52]
 //   denormalize  generate_motion_video.py:259-260: x * std + mean (separate roundings, as torch)
 //   pck          motion_evaluation.py:4-22 / pose_video/evaluation.py:4-21
+//   windows      dataUtils.py:585-665 (PATS sample windows gathered from HBM-resident sequences)
 // All bandwidth-trivial element work; the moments pass is a fixed-order fp64 reduction.
 #include "a2m_internal.h"
 
@@ -140,3 +141,45 @@ int a2m_pck_f32(const float* pred, const float* gt, int32_t N, int32_t K, double
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------- windowing
+// PATS sample windows (dataUtils.py:585-624, :646-665): out[w][j][c] = data[starts[w] +
+// j*interval][c] for j < ceil(window / interval), optionally standardised as (x - mean[c]) /
+// (std[c] < 1e-7 ? 1 : std[c]) -- the loader's cached normalisation (:656-662).
+namespace a2m {
+__global__ void window_gather_kernel(const float* __restrict__ data, int C, const int64_t* starts,
+                                     int nw, int nj, int interval, const float* mean,
+                                     const float* std_, float* __restrict__ out) {
+  const int64_t total = (int64_t)nw * nj * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const int64_t wj = i / C;
+    const int j = (int)(wj % nj), w = (int)(wj / nj);
+    float v = data[(starts[w] + (int64_t)j * interval) * C + c];
+    if (mean) {
+      const float s = std_[c] < 1e-7f ? 1.f : std_[c];
+      v = __fdiv_rn(__fsub_rn(v, mean[c]), s);
+    }
+    out[i] = v;
+  }
+}
+}  // namespace a2m
+
+extern "C" int a2m_window_gather_f32(const float* data, int64_t length, int32_t C,
+                                     const int64_t* starts, int32_t n_windows, int32_t window,
+                                     int32_t interval, const float* mean, const float* std_,
+                                     float* out, void* stream) {
+  A2M_CHECK_ARG(data && starts && out && C > 0 && n_windows >= 0 && window > 0 && interval > 0 &&
+                    (mean == nullptr) == (std_ == nullptr),
+                "window_gather: bad args");
+  (void)length;  // the host computed starts < length - window (dataUtils.py:611-618)
+  if (n_windows == 0) return A2M_OK;
+  const int nj = (window + interval - 1) / interval;
+  const int64_t total = (int64_t)n_windows * nj * C;
+  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+  hipLaunchKernelGGL(window_gather_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), data, C, starts,
+                     n_windows, nj, interval, mean, std_, out);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}

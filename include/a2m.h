@@ -318,6 +318,13 @@ int a2m_pose_denormalize_f32(const float* pose, int64_t n_frames, const float* m
 int a2m_pck_f32(const float* pred, const float* gt, int32_t N, int32_t K, double alpha,
                 double* out, void* stream);
 
+/* PATS windowing (dataUtils.py:585-665): out[w][j][c] =
+ * data[starts[w] + j*interval][c], j < ceil(window/interval), data [length][C] in HBM; with
+ * mean/std (both or neither) each value is standardised as (x - mean[c]) / (std[c] < 1e-7 ? 1 : std[c]). */
+int a2m_window_gather_f32(const float* data, int64_t length, int32_t C, const int64_t* starts,
+                          int32_t n_windows, int32_t window, int32_t interval, const float* mean,
+                          const float* std_, float* out, void* stream);
+
 /* Measurement hook (bench.py): while enabled, every launch of the implicit-GEMM engine is
  * bracketed by HIP events on its stream; _end synchronises them and returns the launch count,
  * the launches' algorithmic FLOPs (2*M*N*K*batch), the summed tile-kernel time and the summed

@@ -143,3 +143,19 @@ def test_ops_refuse_cpu_tensors():
     w = torch.zeros(4, 4, 3)
     with pytest.raises(RuntimeError, match='no CPU fallback'):
         F.conv1d(x, w)
+
+
+def test_pats_window_index_geometry():
+    """dataUtils.update_idx_list arithmetic (dataUtils.py:585-624; restated -- the reference
+    loader does not import, so no reference run pins it): 4.3 s windows give 64 pose frames at
+    15 fps and 64 audio frames from log_mel_512 at fs 89 with stride round(89/15) = 6."""
+    from a2m.windowing import FS, window_index
+    assert FS['audio/log_mel_512'] == 89 and FS['pose/data'] == 15
+    s_p, w_p, i_p = window_index(1000, 'pose/data', 15, 4.3, 5)
+    assert (w_p, i_p) == (64, 1) and s_p[1] - s_p[0] == 5 and s_p[-1] < 1000 - 64
+    s_a, w_a, i_a = window_index(6000, 'audio/log_mel_512', 15, 4.3, 5)
+    assert (w_a, i_a) == (382, 6) and s_a[1] - s_a[0] == 30 and len(range(0, w_a, i_a)) == 64
+    s0, w0, _ = window_index(200, 'pose/data', 15, 4.3, 0)
+    assert list(s0) == list(range(0, 200 - 64, 64))
+    with pytest.raises(AssertionError):
+        window_index(200, 'pose/data', 15, 4.3, 64)

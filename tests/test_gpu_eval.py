@@ -74,3 +74,28 @@ def test_inference_surface(tmp_path, g_state):
     ref = z['pose'].astype(np.float64) * zn['std_necksub'] + zn['mean_necksub']
     assert np.abs(den.cpu().numpy() - ref).max() <= 1e-4 * np.abs(ref).max()
     assert tuple(inference.planar_frames(den).shape) == (2, 64, 2, 52)
+
+
+def test_window_gather_matches_slicing():
+    """gather_windows == data[start:start+window:interval] (dataUtils.py:646-665), with and
+    without the loader's cached standardisation (std < 1e-7 -> 1)."""
+    from a2m.windowing import PatsClip, gather_windows, window_index
+    g = torch.Generator().manual_seed(5)
+    mel = torch.randn(2000, 128, generator=g)
+    pose = torch.randn(330, 104, generator=g)
+    starts, window, interval = window_index(mel.shape[0], 'audio/log_mel_512', 15, 4.3, 5)
+    out = gather_windows(mel.cuda(), starts, window, interval)
+    ref = np.stack([mel.numpy()[s:s + window:interval] for s in starts])
+    assert out.shape == ref.shape == (len(starts), 64, 128) and np.array_equal(out.cpu().numpy(), ref)
+    mean, std = torch.randn(104, generator=g), torch.rand(104, generator=g) + 0.5
+    std[3] = 0.0
+    clip = PatsClip({'pose/data': pose.cuda(), 'audio/log_mel_512': mel.cuda()}, (15, 15), 4.3, 5,
+                    norm_stats={'pose/data': (mean.cuda(), std.cuda())})
+    n = len(clip)
+    assert n == min(len(window_index(330, 'pose/data', 15, 4.3, 5)[0]), len(starts))
+    b = clip.batch(np.arange(n))
+    sp = window_index(330, 'pose/data', 15, 4.3, 5)[0][:n]
+    sd = np.where(std.numpy() < 1e-7, 1.0, std.numpy())
+    ref_p = np.stack([(pose.numpy()[s:s + 64] - mean.numpy()) / sd for s in sp]).astype(np.float32)
+    assert np.abs(b['pose/data'].cpu().numpy() - ref_p).max() <= 1e-6 * np.abs(ref_p).max()
+    assert b['audio/log_mel_512'].shape == (n, 64, 128)
