@@ -34,13 +34,15 @@ def _check_dev(*ts):
 
 
 class _Workspace:
-    """One growable scratch buffer per device (ops on one stream run in order)."""
+    """One growable scratch buffer per (device, stream): ops on one stream run in order, and
+    streams that run concurrently (the generator's body / hand branches) get their own."""
 
     def __init__(self):
         self.buf = {}
 
     def get(self, device, nbytes=0):
-        key = torch.device(device).index or 0
+        device = torch.device(device)
+        key = (device.index or 0, torch.cuda.current_stream(device).cuda_stream)
         cur = self.buf.get(key)
         if cur is None or cur.numel() < nbytes:
             size = max(nbytes, 64 << 20, 0 if cur is None else 2 * cur.numel())

@@ -6,6 +6,8 @@ Same constructors, forward signatures, return values and state_dict keys as the 
   SelfAttention_D(in_channels=104, out_channels=64, n_downsampling=2, p=0.3, groups=1, aux_classes=10)
       .forward(motion [B,T-1,104], audio=None, aux_labels=None) -> ([B,4], [aux?])
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -129,8 +131,20 @@ class SelfAttention_G(_GraphTopology):
         B, T, _ = audio.shape
         feats = self.unet(self.audio_encoder(audio))
         out = torch.empty(B, T, self.body_feats + self.hand_feats, device=audio.device)
-        self._branch('body', feats, out, 0)
-        self._branch('hand', feats, out, self.body_feats)
+        if _BRANCH_STREAMS:
+            # the body and hand decoders are independent after the UNet: the body branch runs
+            # on a side stream (forked from / joined to the caller's, so graph capture records
+            # both), overlapping its latency-bound small launches with the hand branch's
+            main = torch.cuda.current_stream(audio.device)
+            side = _side_stream(audio.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._branch('body', feats, out, 0)
+            self._branch('hand', feats, out, self.body_feats)
+            main.wait_stream(side)
+        else:
+            self._branch('body', feats, out, 0)
+            self._branch('hand', feats, out, self.body_feats)
         losses = F.pose_losses(out, real_pose)
         internal = [losses[0]] if real_pose is not None else []
         internal.append(losses[1])
@@ -142,6 +156,18 @@ class SelfAttention_G(_GraphTopology):
 
     def compute_comprehensive_angle_loss(self, gen_pose):
         return F.pose_losses(gen_pose.contiguous())[1]
+
+
+_BRANCH_STREAMS = os.environ.get('A2M_BRANCH_STREAMS', '1') != '0'
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device):
+    key = device.index or 0
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return s
 
 
 class SelfAttention_D(_GraphTopology):

@@ -32,6 +32,8 @@ struct GemmArgs {
   int splits, kchunk;
   float* partial;
   int xcd_group;   // >0: XCD-aware block remap with this many M-tiles per group; 0: identity
+  int mcontig;     // output has unit m stride: the tile is staged through LDS and written
+                   // along m (split-K slabs then are [N][M])
 };
 
 struct RowInfo {
@@ -361,6 +363,42 @@ __device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int
   E.out[off] = v;
 }
 
+// One k-step: issue the global loads of tile i + 1 into registers, run the MFMAs of tile i
+// from LDS buffer i & 1, then store tile i + 1 into the other buffer.  (A two-tile register
+// prefetch measured 3-25 % slower: VGPR pressure.)
+template <int BM, int BN, int BK, int TM, int TN, class LA, class LB>
+__device__ __forceinline__ void gemm_kstep(LA& la, LB& lb, float* lds, int i, int nk, int kbeg,
+                                           int wm, int wn, int li, int lh, floatx16 (&acc)[TM][TN]) {
+  constexpr int STAGE = LA::TILE + LB::TILE;
+  if (i + 1 < nk) {
+    la.load(kbeg + (i + 1) * BK);
+    lb.load(kbeg + (i + 1) * BK);
+  }
+  const float* As = lds + (i & 1) * STAGE;
+  const float* Bs = As + LA::TILE;
+#pragma unroll
+  for (int half = 0; half < BK / 16; ++half) {
+    float af[TM][8], bf[TN][8];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) LA::frag(As, wm * (BM / 2) + t * 32 + li, half, lh, af[t]);
+#pragma unroll
+    for (int u = 0; u < TN; ++u) LB::frag(Bs, wn * (BN / 2) + u * 32 + li, half, lh, bf[u]);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][s], bf[u][s], acc[t][u], 0, 0, 0);
+  }
+  if (i + 1 < nk) {
+    float* nxt = lds + ((i + 1) & 1) * STAGE;
+    la.store(nxt);
+    lb.store(nxt + LA::TILE);
+  }
+  __syncthreads();
+}
+
 template <int BM, int BN, int BK, int MA, int MB>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -413,47 +451,48 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 
-  if (kbeg < kend) {
+  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) {
     la.load(kbeg);
     lb.load(kbeg);
     la.store(lds);
     lb.store(lds + LA::TILE);
   }
   __syncthreads();
-  int cur = 0;
-  for (int k = kbeg; k < kend; k += BK) {
-    const bool has_next = k + BK < kend;
-    if (has_next) {
-      la.load(k + BK);
-      lb.load(k + BK);
-    }
-    const float* As = lds + cur * STAGE;
-    const float* Bs = As + LA::TILE;
-#pragma unroll
-    for (int half = 0; half < BK / 16; ++half) {
-      float af[TM][8], bf[TN][8];
-#pragma unroll
-      for (int t = 0; t < TM; ++t) LA::frag(As, wm * (BM / 2) + t * 32 + li, half, lh, af[t]);
-#pragma unroll
-      for (int u = 0; u < TN; ++u) LB::frag(Bs, wn * (BN / 2) + u * 32 + li, half, lh, bf[u]);
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-#pragma unroll
-        for (int t = 0; t < TM; ++t)
-#pragma unroll
-          for (int u = 0; u < TN; ++u)
-            acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][s], bf[u][s], acc[t][u], 0, 0, 0);
-    }
-    if (has_next) {
-      float* nxt = lds + (cur ^ 1) * STAGE;
-      la.store(nxt);
-      lb.store(nxt + LA::TILE);
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
+  for (int i = 0; i < nk; ++i)
+    gemm_kstep<BM, BN, BK, TM, TN>(la, lb, lds, i, nk, kbeg, wm, wn, li, lh, acc);
 
   // epilogue
+  if (args.mcontig) {
+    // m-contiguous output (node-feature layouts [.., J*64]): a direct store would put the 32
+    // lanes of each instruction (consecutive n) M floats apart.  Stage the tile as Cs[n][m]
+    // (pitch BM + 1) in the now idle LDS and write it out along m instead.
+    static_assert(BN * (BM + 1) <= 2 * STAGE, "C tile must fit the LDS stages");
+    constexpr int LDC = BM + 1;
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          lds[(wn * (BN / 2) + u * 32 + li) * LDC + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) +
+              4 * lh] = acc[t][u][q];
+    __syncthreads();
+    const int ml = tid % BM;
+    const int m = m0 + ml;
+    if (m < args.M) {
+      for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
+        const int n = n0 + nl;
+        if (n >= args.N) break;
+        const float v = lds[nl * LDC + ml];
+        if (args.partial)
+          args.partial[(int64_t)zz * args.M * args.N + (int64_t)n * args.M + m] = v;
+        else
+          epi_store(args.E, batch, v, m, epi_addr(args.E, 0, n) + m);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < TN; ++u) {
     const int n = n0 + wn * (BN / 2) + u * 32 + li;
@@ -480,20 +519,28 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
   }
 }
 
-// Fixed-order (s = 0, 1, ...) sum of the split-K slabs + epilogue.  Four consecutive n per
-// thread (float4) when N % 4 == 0, and the slab loads of four splits are issued before their
-// adds, so the pass is bandwidth- rather than latency-bound.
+// Fixed-order (s = 0, 1, ...) sum of the split-K slabs + epilogue.  Slabs are [M][N], or
+// [N][M] for m-contiguous outputs (args.mcontig), so the inner slab index is also the output's
+// contiguous one.  Four consecutive inner elements per thread (float4) when the inner extent
+// is a multiple of 4, and the slab loads of four splits are issued before their adds, so the
+// pass is bandwidth- rather than latency-bound.
+__device__ __forceinline__ void reduce_store(const GemmArgs& args, int z, float v, int o, int in) {
+  const int m = args.mcontig ? in : o, n = args.mcontig ? o : in;
+  epi_store(args.E, z, v, m, epi_addr(args.E, m, n));
+}
+
 __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
   const int64_t MN = (int64_t)args.M * args.N;
   const int S = args.splits;
-  if ((args.N & 3) == 0) {
+  const int inner = args.mcontig ? args.M : args.N;
+  if ((inner & 3) == 0) {
     const int64_t total4 = MN * batch / 4;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
          i += (int64_t)gridDim.x * blockDim.x) {
       const int64_t e = i * 4;
       const int z = (int)(e / MN);
       const int64_t mn = e - (int64_t)z * MN;
-      const int m = (int)(mn / args.N), n = (int)(mn - (int64_t)m * args.N);
+      const int o = (int)(mn / inner), in = (int)(mn - (int64_t)o * inner);
       const float* p = args.partial + (int64_t)z * S * MN + mn;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       int s = 0;
@@ -511,10 +558,10 @@ __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
         const float4 a = *reinterpret_cast<const float4*>(p + s * MN);
         v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
       }
-      epi_store(args.E, z, v.x, m, epi_addr(args.E, m, n));
-      epi_store(args.E, z, v.y, m, epi_addr(args.E, m, n + 1));
-      epi_store(args.E, z, v.z, m, epi_addr(args.E, m, n + 2));
-      epi_store(args.E, z, v.w, m, epi_addr(args.E, m, n + 3));
+      reduce_store(args, z, v.x, o, in);
+      reduce_store(args, z, v.y, o, in + 1);
+      reduce_store(args, z, v.z, o, in + 2);
+      reduce_store(args, z, v.w, o, in + 3);
     }
     return;
   }
@@ -523,11 +570,11 @@ __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
        i += (int64_t)gridDim.x * blockDim.x) {
     const int z = (int)(i / MN);
     const int64_t mn = i - (int64_t)z * MN;
-    const int m = (int)(mn / args.N), n = (int)(mn - (int64_t)m * args.N);
+    const int o = (int)(mn / inner), in = (int)(mn - (int64_t)o * inner);
     const float* p = args.partial + (int64_t)z * S * MN + mn;
     float v = 0.f;
     for (int s = 0; s < S; ++s) v += p[s * MN];
-    epi_store(args.E, z, v, m, epi_addr(args.E, m, n));
+    reduce_store(args, z, v, o, in);
   }
 }
 
@@ -562,9 +609,18 @@ struct Plan {
   int bm, bk, splits, kchunk;
 };
 
-// Tile / split-K choice: fill the 256 CUs with >= ~2 workgroups each while keeping every
-// K-slice >= 256 deep.  A2M_GEMM_TILE=64|128, A2M_GEMM_SPLIT=n and
-// A2M_GEMM_XCD=g (XCD-aware remap, g M-tiles per group; 0 = off) override (experiments).
+// Tile / split-K choice by a cost model fitted to measured sweeps of the engine on MI355X
+// (tools/gemm_tune.py; DESIGN.md "GEMM planner").  For each candidate (tile, splits):
+//   blocks = tiles * splits, per_cu = ceil(blocks / 256) (the busiest CU), c = min(per_cu,
+//   resident blocks per CU: 4 at 64x64, 2 at 128x128 -- LDS-bound),
+//   t = per_cu * block_flops / thr(tile, c) + ceil(per_cu / occ) * t_fixed(tile) + t_launch
+//       + (splits > 1 ? (splits + 1) * M * N * 4 B / 3.5 TB/s + 3 us : 0)   (the slab reduce)
+// thr is the per-CU fp32 MFMA throughput measured at c co-resident blocks; a row-gathered
+// operand (modes 2/3: transposed LDS staging) costs the 64x64 tile ~16 % of throughput and
+// the 128x128 tile ~6 us more per round of blocks.  The model is
+// deterministic in (M, N, K, batch, gathered), so a shape always gets the same plan and the
+// same (bitwise-reproducible) split order.  A2M_GEMM_TILE=64|128, A2M_GEMM_SPLIT=n,
+// a2m_gemm_plan_override and A2M_GEMM_XCD=g override (experiments).
 static int gemm_bk() { return 32; }   // (BK = 16 measured slower end to end; not instantiated)
 
 static int gemm_xcd_group() {
@@ -572,32 +628,67 @@ static int gemm_xcd_group() {
   return g < 0 ? 0 : g;
 }
 
-static Plan plan_for(int M, int N, int K, int batch) {
-  static const int force_tile = env_int("A2M_GEMM_TILE", 0);
-  static const int force_split = env_int("A2M_GEMM_SPLIT", 0);
+static int g_override_tile = 0, g_override_split = 0;   // a2m_gemm_plan_override (tuning)
+
+static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int tile, int kchunk,
+                           int splits) {
+  static const double thr64[4] = {340e3, 428e3, 435e3, 440e3};   // flop / us per CU
+  static const double thr128[2] = {464e3, 500e3};
+  const int occ = tile == 128 ? 2 : 4;
+  const int64_t tiles = cdiv(M, tile) * cdiv(N, tile) * (int64_t)batch;
+  const int64_t per_cu = cdiv(tiles * splits, 256);
+  const int c = (int)std::min<int64_t>(per_cu, occ);
+  double thr = tile == 128 ? thr128[c - 1] : thr64[c - 1];
+  if (gathered && tile == 64) thr *= 0.84;
+  const double block_flops = 2.0 * tile * tile * (double)kchunk;
+  const double fixed = tile == 128 ? (gathered ? 16.0 : 10.0) : 3.0;
+  double t = per_cu * block_flops / thr + cdiv(per_cu, occ) * fixed + 4.0;
+  if (splits > 1) t += (splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0;
+  return t;
+}
+
+static Plan plan_for(int M, int N, int K, int batch, bool gathered) {
+  static const int env_tile = env_int("A2M_GEMM_TILE", 0);
+  static const int env_split = env_int("A2M_GEMM_SPLIT", 0);
+  const int force_tile = g_override_tile ? g_override_tile : env_tile;
+  const int force_split = g_override_split ? g_override_split : env_split;
   const int BK = gemm_bk();
-  auto splits_for = [&](int64_t tiles) {
-    int s = 1;
-    while (s < 64 && tiles * s < 512 && K / (s * 2) >= 256) s *= 2;
-    return s;
-  };
-  const int64_t t128 = cdiv(M, 128) * cdiv(N, 128) * (int64_t)batch;
-  const int64_t t64 = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
-  const int s128 = splits_for(t128), s64 = splits_for(t64);
-  Plan p;
-  p.bm = (M >= 128 && N >= 128 && t128 * s128 >= 256) ? 128 : 64;
-  if (force_tile == 64 || force_tile == 128) p.bm = force_tile;
-  int splits = p.bm == 128 ? s128 : s64;
-  if (force_split > 0) splits = force_split;
-  p.bk = BK;
-  p.kchunk = (int)(cdiv(cdiv(K, splits), BK) * BK);
-  p.splits = (int)cdiv(K, p.kchunk);
+  static const int cand_splits[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64};
+  Plan p{64, BK, 1, (int)(cdiv(std::max(K, 1), BK) * BK)};
+  double best = 1e300;
+  for (int tile : {64, 128}) {
+    if (force_tile && tile != force_tile) continue;
+    for (int s : cand_splits) {
+      if (force_split && s != force_split) continue;
+      const int kchunk = (int)(cdiv(cdiv(std::max(K, 1), s), BK) * BK);
+      const int se = (int)cdiv(std::max(K, 1), kchunk);
+      if (!force_split && se > 1 && kchunk < 128) continue;
+      if (se != s && s > 1 && !force_split) continue;   // the same plan at a smaller s
+      const double t = plan_cost_us(M, N, K, batch, gathered, tile, kchunk, se);
+      if (t < best) {
+        best = t;
+        p.bm = tile;
+        p.kchunk = kchunk;
+        p.splits = se;
+      }
+    }
+  }
+  if (force_split && best == 1e300) {   // a forced split outside the candidate list
+    p.bm = force_tile ? force_tile : 64;
+    p.kchunk = (int)(cdiv(cdiv(std::max(K, 1), force_split), BK) * BK);
+    p.splits = (int)cdiv(std::max(K, 1), p.kchunk);
+  }
   return p;
 }
 
 size_t gemm_ws_bytes(int M, int N, int K, int batch) {
-  Plan p = plan_for(M, N, K, batch);
-  return p.splits > 1 ? (size_t)p.splits * batch * M * N * sizeof(float) : 0;
+  // either operand orientation (the plan depends on whether an operand is row-gathered)
+  size_t need = 0;
+  for (bool gathered : {false, true}) {
+    const Plan p = plan_for(M, N, K, batch, gathered);
+    if (p.splits > 1) need = std::max(need, (size_t)p.splits * batch * M * N * sizeof(float));
+  }
+  return need;
 }
 
 template <int BM, int BN, int BK>
@@ -656,7 +747,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                 M, N, K, batch);
   GemmArgs a;
   a.A = A; a.B = B; a.E = E; a.M = M; a.N = N; a.K = K;
-  Plan p = plan_for(M, N, K, batch);
+  const int ma = operand_mode(A, K), mb = operand_mode(B, K);
+  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || mb == 3);
   if (force_split > 0) {
     p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk) * p.bk);
     p.splits = (int)cdiv(K, p.kchunk);
@@ -666,6 +758,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   a.kchunk = p.kchunk;
   a.partial = nullptr;
   a.xcd_group = gemm_xcd_group();
+  static const int stage_m = env_int("A2M_GEMM_MCONTIG", 1);
+  a.mcontig = stage_m && E.som == 1 && M > 1;
   if (p.splits > 1) {
     const size_t need = (size_t)p.splits * batch * M * N * sizeof(float);
     if (ws == nullptr || ws_bytes < need) {
@@ -674,18 +768,18 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     }
     a.partial = static_cast<float*>(ws);
   }
-  const int ma = operand_mode(A, K), mb = operand_mode(B, K);
   static const int log_launches = env_int("A2M_GEMM_LOG", 0);
   if (log_launches)
-    std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d\n", M, N,
-                 K, batch, p.bm, p.bk, p.splits, ma, mb);
+    std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
+                 M, N, K, batch, p.bm, p.bk, p.splits, ma, mb, E.som, E.so0, E.so1, E.so2, E.N1, E.N2);
   const long tm = g_timing ? timing_open(2.0 * M * N * (double)K * batch, stream) : -1;
   if (p.bm == 128) launch_tile<128, 128, 32>(a, ma, mb, batch, stream);
   else launch_tile<64, 64, 32>(a, ma, mb, batch, stream);
   A2M_LAUNCH_CHECK();
   if (tm >= 0) timing_mark(tm, 1, false, stream);
   if (p.splits > 1) {
-    const int64_t total = (int64_t)M * N * batch / ((N & 3) == 0 ? 4 : 1);
+    const int inner = a.mcontig ? M : N;
+    const int64_t total = (int64_t)M * N * batch / ((inner & 3) == 0 ? 4 : 1);
     const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, a, batch);
     A2M_LAUNCH_CHECK();
@@ -697,6 +791,14 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
 }  // namespace a2m
 
 extern "C" {
+
+int a2m_gemm_plan_override(int32_t tile, int32_t splits) {
+  A2M_CHECK_ARG((tile == 0 || tile == 64 || tile == 128) && splits >= 0 && splits <= 256,
+                "gemm_plan_override: tile %d splits %d", tile, splits);
+  a2m::g_override_tile = tile;
+  a2m::g_override_split = splits;
+  return A2M_OK;
+}
 
 int a2m_gemm_timing_begin(void) {
   std::lock_guard<std::mutex> lk(a2m::g_timing_mu);

@@ -70,12 +70,18 @@ def gemm_engine_timing(step):
     """Run one eager step with every implicit-GEMM launch bracketed by HIP events on its own
     stream (a2m_gemm_timing_*): the engine's launches/step, algorithmic FLOPs (2*M*N*K) and
     summed tile-kernel / split-K-reduce time.  rocprof's gemm_kernel<...> rows of the same
-    command (profiles/) must agree with ms_tile / launches."""
+    command (profiles/) must agree with ms_tile / launches.  The generator's decoder branches
+    run serialised for this pass, so no launch's duration includes a concurrent one's."""
     from a2m import functional as F
+    from a2m import real_motion_model as RM
     torch.cuda.synchronize()
-    with F.gemm_timing() as t:
-        step()
-        torch.cuda.synchronize()
+    branch, RM._BRANCH_STREAMS = RM._BRANCH_STREAMS, False
+    try:
+        with F.gemm_timing() as t:
+            step()
+            torch.cuda.synchronize()
+    finally:
+        RM._BRANCH_STREAMS = branch
     return t
 
 

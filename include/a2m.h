@@ -330,6 +330,9 @@ int a2m_window_gather_f32(const float* data, int64_t length, int32_t C, const in
  * the launches' algorithmic FLOPs (2*M*N*K*batch), the summed tile-kernel time and the summed
  * split-K reduce time (ms).  Not graph-capturable; no effect when disabled. */
 int a2m_gemm_timing_begin(void);
+/* Tuning hook: force the engine's tile (64 | 128) and split-K count for subsequent launches
+ * (0 = the planner's choice); workspace sizing follows.  Process-global, not for production. */
+int a2m_gemm_plan_override(int32_t tile, int32_t splits);
 int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                         int64_t* reduces);
 
