@@ -29,6 +29,28 @@ def test_logmel_build_config_vs_reference():
     assert rel_err(out, z['mel_build_out']) < TOL
 
 
+def test_logmel_batch_vs_oracle_full_frames():
+    """Register-FFT kernel (fft_len 2048) over a batch of 16 synthetic clips, 64 and 70 frames,
+    including a strided clip view (clip_stride != n_samples), vs the float64 numpy oracle."""
+    from a2m.mel_features import log_mel_batch
+    from oracle import mel as omel, synth
+    for frames, seed in ((64, 11), (70, 12)):
+        n = synth.samples_for_frames(frames)
+        wav = synth.speech_like(16, n + 37, seed=seed)
+        dev = torch.from_numpy(wav).to(DEV)[:, 5:5 + n]  # strided rows, odd start offset
+        out = log_mel_batch(dev).cpu().numpy()
+        for c in (0, 7, 15):
+            ref = omel.log_mel(wav[c, 5:5 + n], **omel.BUILD_CFG)
+            assert out.shape[1:] == ref.shape
+            assert rel_err(out[c], ref) < TOL, (frames, c)
+    # window 2000 < fft_len 2048 (zero-padded frames: the kernel's table-window variant)
+    cfg = dict(omel.BUILD_CFG, window_secs=0.125)
+    wav = synth.speech_like(3, 40000, seed=13)
+    out = log_mel_batch(torch.from_numpy(wav).to(DEV), window_length_secs=0.125).cpu().numpy()
+    for c in range(3):
+        assert rel_err(out[c], omel.log_mel(wav[c], **cfg)) < TOL
+
+
 def test_logmel_reference_signature_and_edges():
     from a2m.mel_features import log_mel_spectrogram
     z = golden('mel.npz')
