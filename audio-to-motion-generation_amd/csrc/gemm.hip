@@ -159,7 +159,7 @@ struct TileLoader {
   float r[NREG];
 
   __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid,
-                                       int kbeg) {
+                                       int kbeg, int kstride = BK) {
     g = &gg;
     base = gg.base + (int64_t)z * gg.bstride;
     K = KK;
@@ -188,7 +188,7 @@ struct TileLoader {
       kq = (tid % QPR) * 4;
     }
     if (MODE != 0) {
-      kstep = kpos(gg, BK);
+      kstep = kpos(gg, kstride);
 #pragma unroll
       for (int p = 0; p < NKP; ++p) kp[p] = kpos(gg, kbeg + kq + (MODE == 3 ? p * KPP : 0));
     }
@@ -363,44 +363,42 @@ __device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int
   E.out[off] = v;
 }
 
-// One k-step: issue the global loads of tile i + 1 into registers, run the MFMAs of tile i
-// from LDS buffer i & 1, then store tile i + 1 into the other buffer.  (A two-tile register
-// prefetch measured 3-25 % slower: VGPR pressure.)
-template <int BM, int BN, int BK, int TM, int TN, class LA, class LB>
-__device__ __forceinline__ void gemm_kstep(LA& la, LB& lb, float* lds, int i, int nk, int kbeg,
-                                           int wm, int wn, int li, int lh, floatx16 (&acc)[TM][TN]) {
-  constexpr int STAGE = LA::TILE + LB::TILE;
-  if (i + 1 < nk) {
-    la.load(kbeg + (i + 1) * BK);
-    lb.load(kbeg + (i + 1) * BK);
-  }
-  const float* As = lds + (i & 1) * STAGE;
-  const float* Bs = As + LA::TILE;
+// Main loop, BK = 32 (two 16-k halves per k-tile), one barrier per k-step placed mid-step:
+//   step i:  store tile i+1 (registers) -> LDS[(i+1)&1]; issue global loads of tile i+2;
+//            read half-1 fragments of tile i; MFMAs of half 0 (fragments read last step);
+//            barrier (tile i+1 visible, every read of tile i complete);
+//            read half-0 fragments of tile i+1; MFMAs of half 1.
+// The next tile's first fragments are read while this tile's second half is on the matrix
+// pipe, so no LDS latency sits between k-steps.  LDS[(i+1)&1] is free at the start of step i:
+// its last reads (tile i-1, half 1) preceded step i-1's barrier.
+template <int TM, int TN>
+struct Frags {
+  float a[TM][8], b[TN][8];
+};
+
+template <int BM, int BN, int TM, int TN, class LA, class LB>
+__device__ __forceinline__ void read_frags(const float* As, const float* Bs, int half, int wm, int wn,
+                                           int li, int lh, Frags<TM, TN>& f) {
 #pragma unroll
-  for (int half = 0; half < BK / 16; ++half) {
-    float af[TM][8], bf[TN][8];
+  for (int t = 0; t < TM; ++t) LA::frag(As, wm * (BM / 2) + t * 32 + li, half, lh, f.a[t]);
 #pragma unroll
-    for (int t = 0; t < TM; ++t) LA::frag(As, wm * (BM / 2) + t * 32 + li, half, lh, af[t]);
+  for (int u = 0; u < TN; ++u) LB::frag(Bs, wn * (BN / 2) + u * 32 + li, half, lh, f.b[u]);
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void mfma_half(const Frags<TM, TN>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
-    for (int u = 0; u < TN; ++u) LB::frag(Bs, wn * (BN / 2) + u * 32 + li, half, lh, bf[u]);
+  for (int s = 0; s < 8; ++s)
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+    for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int u = 0; u < TN; ++u)
-          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[t][s], bf[u][s], acc[t][u], 0, 0, 0);
-  }
-  if (i + 1 < nk) {
-    float* nxt = lds + ((i + 1) & 1) * STAGE;
-    la.store(nxt);
-    lb.store(nxt + LA::TILE);
-  }
-  __syncthreads();
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[t][s], f.b[u][s], acc[t][u], 0, 0, 0);
 }
 
 template <int BM, int BN, int BK, int MA, int MB>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
+  static_assert(BK == 32, "the k-step pipeline assumes two 16-k halves");
   constexpr int TM = BM / 64, TN = BN / 64;
   using LA = TileLoader<BM, BK, MA>;
   using LB = TileLoader<BN, BK, MB>;
@@ -452,15 +450,37 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 
   const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
+  Frags<TM, TN> f0, f1;
   if (nk > 0) {
     la.load(kbeg);
     lb.load(kbeg);
     la.store(lds);
     lb.store(lds + LA::TILE);
+    if (nk > 1) {
+      la.load(kbeg + BK);
+      lb.load(kbeg + BK);
+    }
   }
   __syncthreads();
-  for (int i = 0; i < nk; ++i)
-    gemm_kstep<BM, BN, BK, TM, TN>(la, lb, lds, i, nk, kbeg, wm, wn, li, lh, acc);
+  if (nk > 0) read_frags<BM, BN, TM, TN, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
+  for (int i = 0; i < nk; ++i) {
+    const float* cur = lds + (i & 1) * STAGE;
+    float* nxt = lds + ((i + 1) & 1) * STAGE;
+    if (i + 1 < nk) {
+      la.store(nxt);
+      lb.store(nxt + LA::TILE);
+    }
+    if (i + 2 < nk) {
+      la.load(kbeg + (i + 2) * BK);
+      lb.load(kbeg + (i + 2) * BK);
+    }
+    read_frags<BM, BN, TM, TN, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
+    mfma_half(f0, acc);
+    __syncthreads();
+    if (i + 1 < nk) read_frags<BM, BN, TM, TN, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
+    mfma_half(f1, acc);
+  }
+  __syncthreads();  // the m-contiguous epilogue reuses the stages
 
   // epilogue
   if (args.mcontig) {

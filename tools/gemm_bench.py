@@ -1,0 +1,56 @@
+"""Dense k-contiguous GEMM timing on the engine (a2m_gemm_f32), graph-replayed: isolates the
+tile kernel from the conv gathers.  usage: python tools/gemm_bench.py [M,N,K ...]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'audio-to-motion-generation_amd'))
+import torch  # noqa: E402
+
+from a2m import functional as F  # noqa: E402
+
+dev = torch.device('cuda')
+PLANS = [(0, 0)]
+if os.environ.get('SWEEP'):
+    PLANS = [(0, 0)] + [(t, sp) for t in (64, 128) for sp in (1, 2, 3, 4, 6, 8)]
+SHAPES = [(256, 4096, 768), (512, 4096, 3072), (2048, 1024, 3072), (1024, 2048, 6144),
+          (2560, 2048, 2048), (4096, 4096, 4096)]
+if len(sys.argv) > 1:
+    SHAPES = [tuple(int(v) for v in a.split(',')) for a in sys.argv[1:]]
+from a2m import _native as NN  # noqa: E402
+
+
+def one(M, N, K, tile, split):
+    NN.lib.a2m_gemm_plan_override(tile, split)
+    A = torch.randn(M, K, device=dev)
+    B = torch.randn(N, K, device=dev)
+    C = torch.empty(M, N, device=dev)
+    run = lambda: F.gemm(M, N, K, A, K, 1, B, K, 1, C, N, 1)  # noqa: E731
+    run()
+    torch.cuda.synchronize()
+    ref = (A.double() @ B.double().t()).float()
+    err = ((C - ref).abs().max() / ref.abs().max()).item()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    iters = 20
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(iters):
+                run()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(3):
+            g.replay()
+        e1.record(s)
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (3 * iters)
+    tag = f'tile {tile} split {split}' if tile or split else 'planner'
+    print(f'gemm {M}x{N}x{K} {tag:18s}: {us:8.1f} us  {2.0 * M * N * K / us / 1e6:6.1f} TF  rel err {err:.1e}', flush=True)
+
+
+for M, N, K in SHAPES:
+    for tile, split in PLANS:
+        one(M, N, K, tile, split)
+NN.lib.a2m_gemm_plan_override(0, 0)
