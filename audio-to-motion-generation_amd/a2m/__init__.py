@@ -9,3 +9,35 @@ import torch  # noqa: F401  (loads the ROCm runtime the library links against fi
 from . import _native  # noqa: F401  (raises ImportError if liba2m_hip.so is absent)
 
 __version__ = '0.1.0'
+
+
+def set_gemm_precision(dtype):
+    """Operand precision of every GEMM-engine launch issued afterwards: 'fp32' (default, the
+    parity configuration) or 'bf16' (bf16 operands, fp32 accumulation, fp32 storage -- the
+    torch.autocast(dtype=torch.bfloat16)-equivalent of BASELINE configs[4]).  Returns the
+    previous setting.  HIP graphs keep the precision they were captured with."""
+    prev = 'bf16' if _native.lib.a2m_get_gemm_precision() else 'fp32'
+    if dtype in ('bf16', torch.bfloat16):
+        flag = 1
+    elif dtype in ('fp32', torch.float32):
+        flag = 0
+    else:
+        raise ValueError(f'unsupported GEMM precision {dtype!r} (fp32 or bf16)')
+    _native.check(_native.lib.a2m_set_gemm_precision(flag))
+    return prev
+
+
+class gemm_precision:
+    """Context manager: `with a2m.gemm_precision('bf16'): ...`."""
+
+    def __init__(self, dtype):
+        self.dtype = dtype
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = set_gemm_precision(self.dtype)
+        return self
+
+    def __exit__(self, *exc):
+        set_gemm_precision(self.prev)
+        return False

@@ -1,543 +1,12 @@
-// Implicit-GEMM engine on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32, exact f32 FMA chain).
-//
-// C[m][n] = sum_k A(m,k) * B(n,k) with A, B described by a2m::Gather (dense matrices,
-// conv im2col, transposed-conv / dgrad gathers, wgrad operands) and a fused epilogue
-// (bias, BatchNorm-eval affine, activation, gamma scale, residual adds, strided store).
-//
-// Tiling: 256 threads = 4 waves in a 2x2 layout, block tile BM x BN (128x128 or 64x64),
-// BK = 16 or 32.  Both operands are staged in LDS as [row][k] with a (BK+4)-float row pitch:
-// a wave64 lane (i = lane&31, h = lane>>5) reads its k-values of row i 8 at a time as two
-// ds_read_b128 (conflict-free at this pitch) and feeds MFMA sub-step s with k = (BK/2)h + s
-// -- the MFMA's k slot assignment is free as long as A and B agree.  Global loads for tile
-// k+1 are issued into registers before the MFMAs of tile k; LDS is double-buffered so one
-// barrier per K-step suffices.  Split-K writes fp32 partial slabs to a workspace that a
-// second kernel reduces in a fixed order (bitwise reproducible) and runs the epilogue on.
+// Implicit-GEMM engine: host side (operand modes, planner, split-K reduce, launch, timing).
+// The kernels and their description are in gemm_kernel.h.
 #include <cstdlib>
 #include <mutex>
 #include <vector>
 
-#include "a2m_internal.h"
+#include "gemm_kernel.h"
 
 namespace a2m {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-// K-tile depth BK = 32 (the kernels are templated on it).  LDS row pitch BK+4 floats keeps the
-// per-lane ds_read_b128 fragment reads conflict-free (row*pitch mod 64 banks distinct over 16 rows).
-
-struct GemmArgs {
-  Gather A, B;
-  Epilogue E;
-  int M, N, K;
-  int splits, kchunk;
-  float* partial;
-  int xcd_group;   // >0: XCD-aware block remap with this many M-tiles per group; 0: identity
-  int mcontig;     // output has unit m stride: the tile is staged through LDS and written
-                   // along m (split-K slabs then are [N][M])
-};
-
-struct RowInfo {
-  int base, h, w;
-  bool valid;
-};
-
-__device__ __forceinline__ RowInfo row_info(const Gather& g, int r, int R) {
-  RowInfo ri;
-  ri.valid = r < R;
-  int rr = ri.valid ? r : 0;
-  int r2 = rr % g.R2;
-  int t = rr / g.R2;
-  int r1 = t % g.R1;
-  int r0 = t / g.R1;
-  ri.base = r0 * g.sr0;
-  ri.h = r1 * g.ar1 + g.ch;
-  ri.w = r2 * g.ar2 + g.cw;
-  return ri;
-}
-
-struct KPos {
-  int k, k0, k1, k2;
-};
-
-__device__ __forceinline__ KPos kpos(const Gather& g, int k) {
-  KPos p;
-  p.k = k;
-  p.k2 = k % g.K2;
-  int t = k / g.K2;
-  p.k1 = t % g.K1;
-  p.k0 = t / g.K1;
-  return p;
-}
-
-// p += d in the mixed radix (k0, K1, K2) with d.k1 < K1, d.k2 < K2: branch-free, no division
-// (the loaders advance their k positions by BK per k-step this way).
-__device__ __forceinline__ void kadd(const Gather& g, KPos& p, const KPos& d) {
-  p.k += d.k;
-  int k2 = p.k2 + d.k2;
-  const int c2 = k2 >= g.K2;
-  k2 -= c2 ? g.K2 : 0;
-  int k1 = p.k1 + d.k1 + c2;
-  const int c1 = k1 >= g.K1;
-  k1 -= c1 ? g.K1 : 0;
-  p.k0 += d.k0 + c1;
-  p.k1 = k1;
-  p.k2 = k2;
-}
-
-__device__ __forceinline__ void kinc(const Gather& g, KPos& p) {
-  ++p.k;
-  if (++p.k2 == g.K2) {
-    p.k2 = 0;
-    if (++p.k1 == g.K1) {
-      p.k1 = 0;
-      ++p.k0;
-    }
-  }
-}
-
-__device__ __forceinline__ float gather_elem(const Gather& g, const float* base, const RowInfo& ri,
-                                             const KPos& p, int K) {
-  int h = ri.h + p.k1 * g.bk1;
-  int w = ri.w + p.k2 * g.bk2;
-  bool v = ri.valid && p.k < K && h >= 0 && w >= 0;
-  if (g.divh > 1) {
-    v = v && (h % g.divh) == 0;
-    h /= g.divh;
-  }
-  if (g.divw > 1) {
-    v = v && (w % g.divw) == 0;
-    w /= g.divw;
-  }
-  v = v && h < g.Lh && w < g.Lw;
-  return v ? base[ri.base + p.k0 * g.sk0 + h * g.sh + w * g.sw] : 0.f;
-}
-
-typedef float float4u __attribute__((ext_vector_type(4), aligned(4)));
-
-// Operand staging.  The MFMA k-slot order is k = 16*half + 8*h + s (h = lane>>5, s = 0..7,
-// half = 0..BK/16-1) for both operands.
-//   MODE 0: dense k-contiguous rows, float4 loads, LDS [row][k].
-//   MODE 1: k-contiguous gather (scalar loads), LDS [row][k].
-//   MODE 2: row-contiguous gather (scalar loads, lanes along rows), LDS [row][k].
-//   MODE 3: row-contiguous rows loaded 4 at a time (float4 along the row axis: [K][R] matrices
-//           and stride-1/2 conv im2col over [B][C][T]); written transposed into LDS [row][k]
-//           (A2M_M3_TRANSPOSE, default) or kept k-major with ds_read_b32 fragments.
-//   MODE 4: k-contiguous runs (the inner k digit has unit stride, K2 % 4 == 0: wgrad operands
-//           over [B][C][T]) loaded 4 k at a time, LDS [row][k].
-#ifndef A2M_M3_TRANSPOSE
-#define A2M_M3_TRANSPOSE 1
-#endif
-template <int BR, int BK, int MODE>
-struct TileLoader {
-  // MODE 3 with A2M_M3_TRANSPOSE: the float4 of 4 rows is written as 4 scalars into the
-  // [row][k] layout (lanes spread over k so the writes stay conflict-free), and fragments are
-  // the same two ds_read_b128 as the other modes.
-  static constexpr bool KMAJ = MODE == 3 && !A2M_M3_TRANSPOSE;
-  static constexpr int LDK = BK + 4;                // [row][k] pitch
-  static constexpr int LDR = BR + 4;                // [k][row] pitch: 8*LDR = 32 mod 64 banks
-  static constexpr int TILE = KMAJ ? BK * LDR : BR * LDK;
-  static constexpr int QPR = BK / 4;                // k-major maps: float4 quads per row
-  static constexpr int RPP = 256 / QPR;             //   rows per pass
-  static constexpr int NPASS = BR / RPP;
-  static constexpr int KPT = BK * BR / 256;         // row-major map: k per thread
-  static constexpr int NREG = BK * BR / 256;        // floats per thread
-  static constexpr int QR = BR / 4;                 // mode 3: float4 row groups per k
-  static constexpr int KPP = 256 / QR;              //   k per pass
-  static constexpr int NP3 = BK / KPP;
-  const Gather* g;
-  const float* base;
-  int K;
-  RowInfo ri[MODE == 2 || MODE == 3 ? 1 : NPASS];
-  int lrow[MODE == 2 || MODE == 3 ? 1 : NPASS];
-  int kq;  // k offset of this thread inside the tile
-  int nrow;  // mode 3: rows of this group that exist (0..4)
-  int rdim;   // mode 3: 0 rows via r0, 1 rows along h, 2 rows along w
-  int rstep;  // mode 3: element step between consecutive rows (1, or 2 for stride-2 convs)
-  static constexpr int NKP = MODE == 3 ? NP3 : 1;
-  KPos kp[NKP];   // k position of each of this thread's k groups at the next load (modes 1-3)
-  KPos kstep;     // BK in (k0, k1, k2) digits
-  float r[NREG];
-
-  __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid,
-                                       int kbeg, int kstride = BK) {
-    g = &gg;
-    base = gg.base + (int64_t)z * gg.bstride;
-    K = KK;
-    if (MODE == 3) {
-      if (KMAJ) {
-        lrow[0] = (tid % QR) * 4;
-        kq = tid / QR;
-      } else {
-        lrow[0] = (tid / KPP) * 4;
-        kq = tid % KPP;
-      }
-      ri[0] = row_info(gg, row0 + lrow[0], R);
-      nrow = min(4, max(0, R - (row0 + lrow[0])));
-      rdim = gg.R2 > 1 ? 2 : (gg.R1 > 1 ? 1 : 0);
-      rstep = rdim == 2 ? gg.ar2 : (rdim == 1 ? gg.ar1 : 1);
-    } else if (MODE == 2) {
-      lrow[0] = tid % BR;
-      kq = (tid / BR) * KPT;
-      ri[0] = row_info(gg, row0 + lrow[0], R);
-    } else {
-#pragma unroll
-      for (int p = 0; p < NPASS; ++p) {
-        lrow[p] = tid / QPR + p * RPP;
-        ri[p] = row_info(gg, row0 + lrow[p], R);
-      }
-      kq = (tid % QPR) * 4;
-    }
-    if (MODE != 0) {
-      kstep = kpos(gg, kstride);
-#pragma unroll
-      for (int p = 0; p < NKP; ++p) kp[p] = kpos(gg, kbeg + kq + (MODE == 3 ? p * KPP : 0));
-    }
-  }
-
-  __device__ __forceinline__ void load(int k0) {
-    if (MODE == 0) {
-#pragma unroll
-      for (int p = 0; p < NPASS; ++p) {
-        int k = k0 + kq;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ri[p].valid && k < K) v = *reinterpret_cast<const float4*>(base + ri[p].base + k);
-        r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
-      }
-    } else if (MODE == 4) {
-      // k-contiguous runs: the 4 k of a quad share k0, k1 (host: K2 % 4 == 0) and sit at
-      // consecutive addresses (bk2 * sw == 1), so one float4 unless the quad crosses an edge
-#pragma unroll
-      for (int p = 0; p < NPASS; ++p) {
-        const KPos q = kp[0];
-        int h = ri[p].h + q.k1 * g->bk1;
-        const int w = ri[p].w + q.k2;
-        bool hv = ri[p].valid && h >= 0;
-        if (g->divh > 1) {
-          hv = hv && (h % g->divh) == 0;
-          h = h / g->divh;
-        }
-        hv = hv && h < g->Lh;
-        float4 v;
-        if (hv && q.k + 3 < K && w >= 0 && w + 3 < g->Lw) {
-          const float4u u = *reinterpret_cast<const float4u*>(
-              base + ri[p].base + (int64_t)q.k0 * g->sk0 + (int64_t)h * g->sh + w);
-          v = make_float4(u.x, u.y, u.z, u.w);
-        } else {
-          KPos qq = q;
-          float e[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            e[j] = gather_elem(*g, base, ri[p], qq, K);
-            kinc(*g, qq);
-          }
-          v = make_float4(e[0], e[1], e[2], e[3]);
-        }
-        r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
-      }
-      kadd(*g, kp[0], kstep);
-    } else if (MODE == 1) {
-#pragma unroll
-      for (int p = 0; p < NPASS; ++p) {
-        KPos q = kp[0];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          r[p * 4 + j] = gather_elem(*g, base, ri[p], q, K);
-          kinc(*g, q);
-        }
-      }
-      kadd(*g, kp[0], kstep);
-    } else if (MODE == 2) {
-      KPos q = kp[0];
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) {
-        r[j] = gather_elem(*g, base, ri[0], q, K);
-        kinc(*g, q);
-      }
-      kadd(*g, kp[0], kstep);
-    } else {
-      // 4 consecutive rows differ only in the row axis (host guarantees it): rdim 0 = rows via
-      // r0 with unit stride, 1 = rows along h (sh == 1), 2 = rows along w (sw == 1), so their
-      // elements are consecutive floats (rstep 1) or every other float (stride-2 convs).
-      const int dh = rdim == 1 ? rstep : 0, dw = rdim == 2 ? rstep : 0;
-#pragma unroll
-      for (int p = 0; p < NP3; ++p) {
-        const KPos q = kp[p];
-        kadd(*g, kp[p], kstep);
-        int h = ri[0].h + q.k1 * g->bk1;
-        const int w = ri[0].w + q.k2 * g->bk2;
-        bool kv = q.k < K && nrow > 0;
-        if (g->divh > 1) {  // only with rdim != 1
-          kv = kv && h >= 0 && (h % g->divh) == 0;
-          h = h / g->divh;
-        }
-        const int64_t a = (int64_t)ri[0].base + (int64_t)q.k0 * g->sk0 + (int64_t)h * g->sh +
-                          (int64_t)w * g->sw;
-        float4 v;
-        if (kv && nrow == 4 && h >= 0 && h + 3 * dh < g->Lh && w >= 0 && w + 3 * dw < g->Lw) {
-          const float4u u = *reinterpret_cast<const float4u*>(base + a);
-          if (rstep == 1) {
-            v = make_float4(u.x, u.y, u.z, u.w);
-          } else {  // stride-2 rows: elements a, a+2 | a+4, a+6 (second load ends at a+6)
-            const float4u u1 = *reinterpret_cast<const float4u*>(base + a + 3);
-            v = make_float4(u.x, u.z, u1.y, u1.w);
-          }
-        } else {
-          float e[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int hj = h + j * dh, wj = w + j * dw;
-            e[j] = (kv && j < nrow && hj >= 0 && hj < g->Lh && wj >= 0 && wj < g->Lw)
-                       ? base[a + j * rstep] : 0.f;
-          }
-          v = make_float4(e[0], e[1], e[2], e[3]);
-        }
-        r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
-      }
-    }
-  }
-
-  __device__ __forceinline__ void store(float* lds) const {
-    if (MODE == 3 && KMAJ) {
-#pragma unroll
-      for (int p = 0; p < NP3; ++p)
-        *reinterpret_cast<float4*>(lds + (kq + p * KPP) * LDR + lrow[0]) =
-            make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
-    } else if (MODE == 3) {
-#pragma unroll
-      for (int p = 0; p < NP3; ++p)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) lds[(lrow[0] + j) * LDK + kq + p * KPP] = r[p * 4 + j];
-    } else if (MODE == 2) {
-      float* dst = lds + lrow[0] * LDK + kq;
-#pragma unroll
-      for (int j = 0; j < KPT; j += 4)
-        *reinterpret_cast<float4*>(dst + j) = make_float4(r[j], r[j + 1], r[j + 2], r[j + 3]);
-    } else {
-#pragma unroll
-      for (int p = 0; p < NPASS; ++p)
-        *reinterpret_cast<float4*>(lds + lrow[p] * LDK + kq) =
-            make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
-    }
-  }
-
-  // The 8 k-values (k = 16*half + 8*lh + s, s = 0..7) of tile row `row` for one lane.
-  __device__ __forceinline__ static void frag(const float* lds, int row, int half, int lh, float* f) {
-    if (KMAJ) {
-      const float* q = lds + (half * 16 + lh * 8) * LDR + row;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) f[s] = q[s * LDR];
-    } else {
-      const float* q = lds + row * LDK + half * 16 + lh * 8;
-      const float4 v0 = *reinterpret_cast<const float4*>(q);
-      const float4 v1 = *reinterpret_cast<const float4*>(q + 4);
-      f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w;
-      f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
-    }
-  }
-};
-
-__device__ __forceinline__ int64_t epi_addr(const Epilogue& E, int m, int n) {
-  int n2 = n % E.N2;
-  int t = n / E.N2;
-  int n1 = t % E.N1;
-  int n0 = t / E.N1;
-  return (int64_t)n0 * E.so0 + (int64_t)n1 * E.so1 + (int64_t)n2 * E.so2 + (int64_t)m * E.som;
-}
-
-__device__ __forceinline__ float epi_value(const Epilogue& E, float v, int m) {
-  if (E.bias) v += E.bias[m];
-  if (E.bn_w) v = (v - E.bn_rm[m]) * (E.bn_w[m] / sqrtf(E.bn_rv[m] + E.bn_eps)) + E.bn_b[m];
-  if (E.act == ACT_RELU) v = v > 0.f ? v : 0.f;
-  else if (E.act == ACT_LRELU) v = v > 0.f ? v : v * E.slope;
-  else if (E.act == ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
-  if (E.gamma) v *= E.gamma[0];
-  return v;
-}
-
-__device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int m, int64_t a) {
-  int64_t off = (int64_t)z * E.bstride + a;
-  v = epi_value(E, v, m);
-  if (E.res1) v += E.res1[off];
-  if (E.res2) v += E.res2[off];
-  if (E.accumulate) v += E.out[off];
-  E.out[off] = v;
-}
-
-// Main loop, BK = 32 (two 16-k halves per k-tile), one barrier per k-step placed mid-step:
-//   step i:  store tile i+1 (registers) -> LDS[(i+1)&1]; issue global loads of tile i+2;
-//            read half-1 fragments of tile i; MFMAs of half 0 (fragments read last step);
-//            barrier (tile i+1 visible, every read of tile i complete);
-//            read half-0 fragments of tile i+1; MFMAs of half 1.
-// The next tile's first fragments are read while this tile's second half is on the matrix
-// pipe, so no LDS latency sits between k-steps.  LDS[(i+1)&1] is free at the start of step i:
-// its last reads (tile i-1, half 1) preceded step i-1's barrier.
-template <int TM, int TN>
-struct Frags {
-  float a[TM][8], b[TN][8];
-};
-
-template <int BM, int BN, int TM, int TN, class LA, class LB>
-__device__ __forceinline__ void read_frags(const float* As, const float* Bs, int half, int wm, int wn,
-                                           int li, int lh, Frags<TM, TN>& f) {
-#pragma unroll
-  for (int t = 0; t < TM; ++t) LA::frag(As, wm * (BM / 2) + t * 32 + li, half, lh, f.a[t]);
-#pragma unroll
-  for (int u = 0; u < TN; ++u) LB::frag(Bs, wn * (BN / 2) + u * 32 + li, half, lh, f.b[u]);
-}
-
-template <int TM, int TN>
-__device__ __forceinline__ void mfma_half(const Frags<TM, TN>& f, floatx16 (&acc)[TM][TN]) {
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-#pragma unroll
-    for (int t = 0; t < TM; ++t)
-#pragma unroll
-      for (int u = 0; u < TN; ++u)
-        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[t][s], f.b[u][s], acc[t][u], 0, 0, 0);
-}
-
-template <int BM, int BN, int BK, int MA, int MB>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
-  static_assert(BK == 32, "the k-step pipeline assumes two 16-k halves");
-  constexpr int TM = BM / 64, TN = BN / 64;
-  using LA = TileLoader<BM, BK, MA>;
-  using LB = TileLoader<BN, BK, MB>;
-  constexpr int STAGE = LA::TILE + LB::TILE;
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int li = lane & 31, lh = lane >> 5;
-
-  // Block -> (n-tile, m-tile, batch*split).  With xcd_group > 0 the linear block id, which the
-  // dispatcher deals round-robin over the 8 XCDs, is first made contiguous per XCD (bijective
-  // for any grid size) and then walked in groups of xcd_group M-tiles, so the blocks that share
-  // an XCD's L2 share A panels (weights) and B panels (activations).
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (args.xcd_group > 0) {
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int total = gx * gy * gridDim.z;
-    const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const int q = total / 8, r = total % 8, x = L % 8;
-    const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
-    bz = t / (gx * gy);
-    const int rem = t - bz * gx * gy;
-    const int gm = args.xcd_group;
-    const int group = rem / (gm * gx);
-    const int first_m = group * gm;
-    const int gsz = min(gy - first_m, gm);
-    const int in = rem - group * gm * gx;
-    by = first_m + in % gsz;
-    bx = in / gsz;
-  }
-  const int zz = bz;
-  const int batch = zz / args.splits, split = zz % args.splits;
-  const int m0 = by * BM, n0 = bx * BN;
-  const int kbeg = split * args.kchunk;
-  const int kend = min(args.K, kbeg + args.kchunk);
-
-  LA la;
-  LB lb;
-  la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
-  lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
-
-  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
-  Frags<TM, TN> f0, f1;
-  if (nk > 0) {
-    la.load(kbeg);
-    lb.load(kbeg);
-    la.store(lds);
-    lb.store(lds + LA::TILE);
-    if (nk > 1) {
-      la.load(kbeg + BK);
-      lb.load(kbeg + BK);
-    }
-  }
-  __syncthreads();
-  if (nk > 0) read_frags<BM, BN, TM, TN, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
-  for (int i = 0; i < nk; ++i) {
-    const float* cur = lds + (i & 1) * STAGE;
-    float* nxt = lds + ((i + 1) & 1) * STAGE;
-    if (i + 1 < nk) {
-      la.store(nxt);
-      lb.store(nxt + LA::TILE);
-    }
-    if (i + 2 < nk) {
-      la.load(kbeg + (i + 2) * BK);
-      lb.load(kbeg + (i + 2) * BK);
-    }
-    read_frags<BM, BN, TM, TN, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
-    mfma_half(f0, acc);
-    __syncthreads();
-    if (i + 1 < nk) read_frags<BM, BN, TM, TN, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
-    mfma_half(f1, acc);
-  }
-  __syncthreads();  // the m-contiguous epilogue reuses the stages
-
-  // epilogue
-  if (args.mcontig) {
-    // m-contiguous output (node-feature layouts [.., J*64]): a direct store would put the 32
-    // lanes of each instruction (consecutive n) M floats apart.  Stage the tile as Cs[n][m]
-    // (pitch BM + 1) in the now idle LDS and write it out along m instead.
-    static_assert(BN * (BM + 1) <= 2 * STAGE, "C tile must fit the LDS stages");
-    constexpr int LDC = BM + 1;
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-          lds[(wn * (BN / 2) + u * 32 + li) * LDC + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) +
-              4 * lh] = acc[t][u][q];
-    __syncthreads();
-    const int ml = tid % BM;
-    const int m = m0 + ml;
-    if (m < args.M) {
-      for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
-        const int n = n0 + nl;
-        if (n >= args.N) break;
-        const float v = lds[nl * LDC + ml];
-        if (args.partial)
-          args.partial[(int64_t)zz * args.M * args.N + (int64_t)n * args.M + m] = v;
-        else
-          epi_store(args.E, batch, v, m, epi_addr(args.E, 0, n) + m);
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int u = 0; u < TN; ++u) {
-    const int n = n0 + wn * (BN / 2) + u * 32 + li;
-    if (n >= args.N) continue;
-    if (args.partial) {
-      float* dst = args.partial + (int64_t)zz * args.M * args.N + n;
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int m = m0 + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-          if (m < args.M) dst[(int64_t)m * args.N] = acc[t][u][q];
-        }
-    } else {
-      const int64_t an = epi_addr(args.E, 0, n);
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int m = m0 + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-          if (m < args.M) epi_store(args.E, batch, acc[t][u][q], m, an + (int64_t)m * args.E.som);
-        }
-    }
-  }
-}
 
 // Fixed-order (s = 0, 1, ...) sum of the split-K slabs + epilogue.  Slabs are [M][N], or
 // [N][M] for m-contiguous outputs (args.mcontig), so the inner slab index is also the output's
@@ -641,7 +110,11 @@ struct Plan {
 // deterministic in (M, N, K, batch, gathered), so a shape always gets the same plan and the
 // same (bitwise-reproducible) split order.  A2M_GEMM_TILE=64|128, A2M_GEMM_SPLIT=n,
 // a2m_gemm_plan_override and A2M_GEMM_XCD=g override (experiments).
-static int gemm_bk() { return 32; }   // (BK = 16 measured slower end to end; not instantiated)
+// Operand precision of the engine: 0 = fp32 (v_mfma_f32_32x32x2_f32, BK 32; the default and
+// the parity configuration), 1 = bf16 (operands rounded to bf16 in LDS, fp32 accumulation,
+// BK 64; a2m_set_gemm_precision, configs[4]).  (BK = 16 measured slower end to end.)
+static int g_gemm_bf16 = 0;
+static int gemm_bk(bool bf16) { return bf16 ? 64 : 32; }
 
 static int gemm_xcd_group() {
   static const int g = env_int("A2M_GEMM_XCD", 0);
@@ -651,7 +124,7 @@ static int gemm_xcd_group() {
 static int g_override_tile = 0, g_override_split = 0;   // a2m_gemm_plan_override (tuning)
 
 static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int tile, int kchunk,
-                           int splits) {
+                           int splits, bool bf16) {
   static const double thr64[4] = {340e3, 428e3, 435e3, 440e3};   // flop / us per CU
   static const double thr128[2] = {464e3, 500e3};
   const int occ = tile == 128 ? 2 : 4;
@@ -660,6 +133,7 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   const int c = (int)std::min<int64_t>(per_cu, occ);
   double thr = tile == 128 ? thr128[c - 1] : thr64[c - 1];
   if (gathered && tile == 64) thr *= 0.84;
+  if (bf16) thr *= 4.0;  // staging-bound rather than MFMA-bound (16x MFMA rate); rough
   const double block_flops = 2.0 * tile * tile * (double)kchunk;
   const double fixed = tile == 128 ? (gathered ? 16.0 : 10.0) : 3.0;
   double t = per_cu * block_flops / thr + cdiv(per_cu, occ) * fixed + 4.0;
@@ -667,12 +141,12 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   return t;
 }
 
-static Plan plan_for(int M, int N, int K, int batch, bool gathered) {
+static Plan plan_for(int M, int N, int K, int batch, bool gathered, bool bf16) {
   static const int env_tile = env_int("A2M_GEMM_TILE", 0);
   static const int env_split = env_int("A2M_GEMM_SPLIT", 0);
   const int force_tile = g_override_tile ? g_override_tile : env_tile;
   const int force_split = g_override_split ? g_override_split : env_split;
-  const int BK = gemm_bk();
+  const int BK = gemm_bk(bf16);
   static const int cand_splits[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64};
   Plan p{64, BK, 1, (int)(cdiv(std::max(K, 1), BK) * BK)};
   double best = 1e300;
@@ -684,7 +158,7 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered) {
       const int se = (int)cdiv(std::max(K, 1), kchunk);
       if (!force_split && se > 1 && kchunk < 128) continue;
       if (se != s && s > 1 && !force_split) continue;   // the same plan at a smaller s
-      const double t = plan_cost_us(M, N, K, batch, gathered, tile, kchunk, se);
+      const double t = plan_cost_us(M, N, K, batch, gathered, tile, kchunk, se, bf16);
       if (t < best) {
         best = t;
         p.bm = tile;
@@ -702,26 +176,15 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered) {
 }
 
 size_t gemm_ws_bytes(int M, int N, int K, int batch) {
-  // either operand orientation (the plan depends on whether an operand is row-gathered)
+  // either operand orientation (the plan depends on whether an operand is row-gathered) and
+  // either precision
   size_t need = 0;
-  for (bool gathered : {false, true}) {
-    const Plan p = plan_for(M, N, K, batch, gathered);
-    if (p.splits > 1) need = std::max(need, (size_t)p.splits * batch * M * N * sizeof(float));
-  }
+  for (bool gathered : {false, true})
+    for (bool bf16 : {false, true}) {
+      const Plan p = plan_for(M, N, K, batch, gathered, bf16);
+      if (p.splits > 1) need = std::max(need, (size_t)p.splits * batch * M * N * sizeof(float));
+    }
   return need;
-}
-
-template <int BM, int BN, int BK>
-static void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
-  dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
-#define A2M_L(MA_, MB_) \
-  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_>), grid, dim3(256), 0, st, a); return; }
-  A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3) A2M_L(0, 4)
-  A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2) A2M_L(1, 3) A2M_L(1, 4)
-  A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3) A2M_L(2, 4)
-  A2M_L(3, 0) A2M_L(3, 1) A2M_L(3, 2) A2M_L(3, 3) A2M_L(3, 4)
-  A2M_L(4, 0) A2M_L(4, 1) A2M_L(4, 2) A2M_L(4, 3) A2M_L(4, 4)
-#undef A2M_L
 }
 
 // Optional per-launch timing of the engine (bench.py's live roofline): HIP events recorded on
@@ -768,7 +231,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   GemmArgs a;
   a.A = A; a.B = B; a.E = E; a.M = M; a.N = N; a.K = K;
   const int ma = operand_mode(A, K), mb = operand_mode(B, K);
-  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || mb == 3);
+  const bool bf16 = g_gemm_bf16 != 0;
+  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || mb == 3, bf16);
   if (force_split > 0) {
     p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk) * p.bk);
     p.splits = (int)cdiv(K, p.kchunk);
@@ -793,8 +257,13 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
                  M, N, K, batch, p.bm, p.bk, p.splits, ma, mb, E.som, E.so0, E.so1, E.so2, E.N1, E.N2);
   const long tm = g_timing ? timing_open(2.0 * M * N * (double)K * batch, stream) : -1;
-  if (p.bm == 128) launch_tile<128, 128, 32>(a, ma, mb, batch, stream);
-  else launch_tile<64, 64, 32>(a, ma, mb, batch, stream);
+  if (bf16) {
+    if (p.bm == 128) launch_tile<128, 128, 64, true>(a, ma, mb, batch, stream);
+    else launch_tile<64, 64, 64, true>(a, ma, mb, batch, stream);
+  } else {
+    if (p.bm == 128) launch_tile<128, 128, 32, false>(a, ma, mb, batch, stream);
+    else launch_tile<64, 64, 32, false>(a, ma, mb, batch, stream);
+  }
   A2M_LAUNCH_CHECK();
   if (tm >= 0) timing_mark(tm, 1, false, stream);
   if (p.splits > 1) {
@@ -819,6 +288,14 @@ int a2m_gemm_plan_override(int32_t tile, int32_t splits) {
   a2m::g_override_split = splits;
   return A2M_OK;
 }
+
+int a2m_set_gemm_precision(int32_t bf16) {
+  A2M_CHECK_ARG(bf16 == 0 || bf16 == 1, "set_gemm_precision: %d (0 = fp32, 1 = bf16)", bf16);
+  a2m::g_gemm_bf16 = bf16;
+  return A2M_OK;
+}
+
+int32_t a2m_get_gemm_precision(void) { return a2m::g_gemm_bf16; }
 
 int a2m_gemm_timing_begin(void) {
   std::lock_guard<std::mutex> lk(a2m::g_timing_mu);

@@ -333,6 +333,13 @@ int a2m_gemm_timing_begin(void);
 /* Tuning hook: force the engine's tile (64 | 128) and split-K count for subsequent launches
  * (0 = the planner's choice); workspace sizing follows.  Process-global, not for production. */
 int a2m_gemm_plan_override(int32_t tile, int32_t splits);
+/* Operand precision of every GEMM-engine launch (convs, linears, attention products and their
+ * backward) issued after the call: 0 = fp32 (default; the parity configuration), 1 = bf16
+ * operands with fp32 accumulation (BASELINE configs[4], torch.autocast(bfloat16)-equivalent:
+ * weights and activations stay fp32 in HBM, rounded to bf16 where they enter the MFMA).
+ * Process-wide; not thread-safe against concurrent launches. */
+int a2m_set_gemm_precision(int32_t bf16);
+int32_t a2m_get_gemm_precision(void);
 int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                         int64_t* reduces);
 

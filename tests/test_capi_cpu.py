@@ -159,3 +159,16 @@ def test_pats_window_index_geometry():
     assert list(s0) == list(range(0, 200 - 64, 64))
     with pytest.raises(AssertionError):
         window_index(200, 'pose/data', 15, 4.3, 64)
+
+
+def test_gemm_precision_switch():
+    """fp32 by default; the context manager sets and restores; bad values raise like the ABI."""
+    import a2m
+    from a2m import _native as N
+    assert N.lib.a2m_get_gemm_precision() == 0
+    with a2m.gemm_precision('bf16'):
+        assert N.lib.a2m_get_gemm_precision() == 1
+    assert N.lib.a2m_get_gemm_precision() == 0
+    assert N.lib.a2m_set_gemm_precision(7) == N.A2M_EINVAL
+    with pytest.raises(ValueError):
+        a2m.set_gemm_precision('fp16')
