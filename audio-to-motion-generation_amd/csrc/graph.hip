@@ -143,9 +143,23 @@ __global__ __launch_bounds__(256, 3) void graph_layer_kernel(
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
 
+  // B fragments (L2-resident weights) run one k-chunk ahead of the MFMAs; the neighbour gather
+  // is unpredicated (rows past the degree read node 0 with weight 0), so its 16 LDS reads issue
+  // back to back and wait once per k-chunk.
   const int nseg = kind == 0 ? GHEADS : 2;
+  auto wseg = [&](int sg) { return kind == 0 ? w0 + (int64_t)sg * GF * GF : (sg == 0 ? w0 : w1); };
+  auto load_b = [&](int sg, int kc, float4 (&bw)[2][2]) {
+    const float* W = wseg(sg);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float* p = W + (t * 32 + li) * GF + kc * 16 + lh * 8;
+      bw[t][0] = *reinterpret_cast<const float4*>(p);
+      bw[t][1] = *reinterpret_cast<const float4*>(p + 4);
+    }
+  };
+  float4 bcur[2][2], bnxt[2][2];
+  load_b(0, 0, bcur);
   for (int seg = 0; seg < nseg; ++seg) {
-    const float* W = kind == 0 ? w0 + (int64_t)seg * GF * GF : (seg == 0 ? w0 : w1);
     const bool agg = kind == 0 || seg == 0;
     float wq[GMAXDEG];
     if (kind == 0) {  // edge softmax of head `seg` for this lane's row (PyG: LeakyReLU 0.2)
@@ -172,29 +186,24 @@ __global__ __launch_bounds__(256, 3) void graph_layer_kernel(
     }
 #pragma unroll
     for (int kc = 0; kc < 4; ++kc) {
-      // B fragments for this k-chunk: lane (li, lh) needs W[t*32 + li][kc*16 + 8*lh .. +8]
-      // (L2-resident weights, requested before the gather below)
-      float4 bw[2][2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const float* p = W + (t * 32 + li) * GF + kc * 16 + lh * 8;
-        bw[t][0] = *reinterpret_cast<const float4*>(p);
-        bw[t][1] = *reinterpret_cast<const float4*>(p + 4);
-      }
+      if (kc < 3) load_b(seg, kc + 1, bnxt);
+      else if (seg + 1 < nseg) load_b(seg + 1, 0, bnxt);
       float af[8];
       if (agg) {
-#pragma unroll
-        for (int s = 0; s < 8; ++s) af[s] = 0.f;
+        float4 v[GMAXDEG][2];
 #pragma unroll
         for (int q = 0; q < GMAXDEG; ++q) {
-          if (q < d) {
-            const float* p = xs + ids[q] * ZP + kc * 16 + lh * 8;
-            const float4 v0 = *reinterpret_cast<const float4*>(p);
-            const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
-            const float w = wq[q];
-            af[0] += w * v0.x; af[1] += w * v0.y; af[2] += w * v0.z; af[3] += w * v0.w;
-            af[4] += w * v1.x; af[5] += w * v1.y; af[6] += w * v1.z; af[7] += w * v1.w;
-          }
+          const float* p = xs + ids[q] * ZP + kc * 16 + lh * 8;
+          v[q][0] = *reinterpret_cast<const float4*>(p);
+          v[q][1] = *reinterpret_cast<const float4*>(p + 4);
+        }
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) af[s8] = 0.f;
+#pragma unroll
+        for (int q = 0; q < GMAXDEG; ++q) {
+          const float w = wq[q];
+          af[0] += w * v[q][0].x; af[1] += w * v[q][0].y; af[2] += w * v[q][0].z; af[3] += w * v[q][0].w;
+          af[4] += w * v[q][1].x; af[5] += w * v[q][1].y; af[6] += w * v[q][1].z; af[7] += w * v[q][1].w;
         }
       } else {  // GraphConv root term
         const float* p = xs + row * ZP + kc * 16 + lh * 8;
@@ -205,11 +214,16 @@ __global__ __launch_bounds__(256, 3) void graph_layer_kernel(
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const float bf[8] = {bw[t][0].x, bw[t][0].y, bw[t][0].z, bw[t][0].w,
-                             bw[t][1].x, bw[t][1].y, bw[t][1].z, bw[t][1].w};
+        const float bf[8] = {bcur[t][0].x, bcur[t][0].y, bcur[t][0].z, bcur[t][0].w,
+                             bcur[t][1].x, bcur[t][1].y, bcur[t][1].z, bcur[t][1].w};
 #pragma unroll
         for (int s = 0; s < 8; ++s)
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        bcur[t][0] = bnxt[t][0];
+        bcur[t][1] = bnxt[t][1];
       }
     }
   }

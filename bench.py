@@ -26,6 +26,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md, chip-level parameters
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA (MI355X_MICROARCH.md; = 16 x the fp32 rate)
 HBM_PEAK_GBS = 8000.0
 SR, WIN, HOP = 16000, 2048, 1067
 
@@ -194,17 +195,20 @@ def run_train(args, world, rank, dev):
     ms = elapsed / args.steps * 1e3
     flops = TRAIN_GFLOP_PER_CLIP_T64 * 1e9 * B * T / 64           # per rank
     tf = flops * world / (ms * 1e-3) / 1e12
+    peak = mfma_peak(args.dtype)
+    cfg = ('configs[2]' if args.dtype == 'fp32' else
+           'configs[4] (bf16 GEMM operands, fp32 master weights / accumulation)')
     result = {
         'metric': 'pose-frames/sec (whole node), PATS 64-frame clips batch 64, training iteration',
         'value': round(Bg * T / (ms * 1e-3), 1), 'unit': 'pose-frames/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
-        'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32',
+        'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32' if args.dtype == 'fp32' else 'bf16',
         'data': 'synthetic mel/pose tensors, random-init weights',
-        'config': {'workload': 'configs[2]: version5_model_train.py iteration (G x3 + D x1, Adam, '
+        'config': {'workload': cfg + ': version5_model_train.py iteration (G x3 + D x1, Adam, '
                                'smoothed noisy labels), DP over ranks, per-rank BatchNorm statistics',
                    'global_batch': Bg, 'seq_len': T, 'parallelism': f'dp{world}'},
-        'path_roofline': {'bound': 'mfma', 'achieved': round(tf, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
-                          'unit': 'TFLOP/s', 'frac': round(tf / FP32_MFMA_PEAK_TFLOPS / world, 4),
+        'path_roofline': {'bound': 'mfma', 'achieved': round(tf, 2), 'peak': peak,
+                          'unit': 'TFLOP/s', 'frac': round(tf / peak / world, 4),
                           'gflop_per_iteration': round(flops * world / 1e9, 1),
                           'flop_source': 'SURVEY.md 8(d) FlopCounter count, dense'},
     }
@@ -214,12 +218,17 @@ def run_train(args, world, rank, dev):
         dist.destroy_process_group()
 
 
-def roofline_entry(gt):
+def mfma_peak(dtype):
+    return FP32_MFMA_PEAK_TFLOPS if dtype == 'fp32' else BF16_MFMA_PEAK_TFLOPS
+
+
+def roofline_entry(gt, peak=None):
+    peak = peak or FP32_MFMA_PEAK_TFLOPS
     tf = gt.flops / (gt.ms_tile * 1e-3) / 1e12
-    tr = load_traffic('gemm_kernel')
+    tr = load_traffic('gemm_kernel') if peak == FP32_MFMA_PEAK_TFLOPS else None
     return {'bound': 'mfma', 'kernel': 'gemm_kernel (implicit-GEMM engine: every launch of one step)',
-            'achieved': round(tf, 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+            'achieved': round(tf, 2), 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': round(tf / peak, 4),
             'traffic': tr['bytes_per_launch'] if tr else None,
             'traffic_source': tr['source'] if tr else None,
             'launches_per_step': gt.launches, 'ms_per_launch': round(gt.ms_tile / max(gt.launches, 1), 4),
@@ -238,6 +247,8 @@ def main():
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--mode', choices=('infer', 'train'), default='infer')
+    ap.add_argument('--dtype', choices=('fp32', 'bf16'), default='fp32',
+                    help='GEMM operand precision (bf16: configs[4], fp32 accumulation/storage)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -247,6 +258,8 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
+    import a2m
+    a2m.set_gemm_precision(args.dtype)
     if args.mode == 'train':
         return run_train(args, world, rank, dev)
 
@@ -307,22 +320,31 @@ def main():
         gt = gemm_engine_timing(step)
         mel_ms, mel_bytes = run_mel_kernel(dev, wave)
     path_tf = g_forward_flops(B, T) / (ms_step * 1e-3) / 1e12
+    peak = mfma_peak(args.dtype)
+    if args.dtype == 'bf16':
+        workload = (f'configs[4] (bf16 GEMM operands, fp32 accumulation): log-mel + SelfAttention_G '
+                    f'forward (eval), batch-{B} x {T}-frame clips per GPU, replicas only')
+    elif T != 64:
+        workload = (f'configs[3] long-form: log-mel + SelfAttention_G forward (eval), batch-{B} x '
+                    f'{T}-frame ({(T - 1) * HOP + WIN} samples) clips per GPU, replicas only')
+    else:
+        workload = (f'configs[1]: log-mel + SelfAttention_G forward (eval), batch-{B} x {T}-frame '
+                    f'clips per GPU, replicas only')
     result = {
         'metric': 'pose-frames/sec (whole node), PATS 64-frame clips batch 64, 1/2/4/8 MI355X',
         'value': round(value, 1), 'unit': 'pose-frames/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32' if args.dtype == 'fp32' else 'bf16',
         'data': 'synthetic 16 kHz speech-like audio, random-init weights',
-        'config': {'workload': 'configs[1]: log-mel + SelfAttention_G forward (eval), batch-64 x 64-frame '
-                               'clips per GPU, replicas only', 'global_batch': B * world, 'seq_len': T,
+        'config': {'workload': workload, 'global_batch': B * world, 'seq_len': T,
                    'parallelism': f'replicas{world}', 'hip_graph': graph is not None},
-        'roofline': roofline_entry(gt),
+        'roofline': roofline_entry(gt, peak),
         'mel_roofline': {'bound': 'hbm', 'achieved': round(mel_bytes / (mel_ms * 1e-3) / 1e9, 1),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(mel_bytes / (mel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          'ms_per_launch': round(mel_ms, 4)},
-        'path_roofline': {'bound': 'mfma', 'achieved': round(path_tf, 2), 'peak': FP32_MFMA_PEAK_TFLOPS,
-                          'unit': 'TFLOP/s', 'frac': round(path_tf / FP32_MFMA_PEAK_TFLOPS, 4),
+        'path_roofline': {'bound': 'mfma', 'achieved': round(path_tf, 2), 'peak': peak,
+                          'unit': 'TFLOP/s', 'frac': round(path_tf / peak, 4),
                           'gflop_per_step': round(g_forward_flops(B, T) / 1e9, 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
