@@ -84,7 +84,9 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
   __shared__ float ew[BMAXN][BDEG];
   __shared__ float dsb[BMAXN][BDEG];
   __shared__ float dal[BMAXN][2];
+  __shared__ float dalh[BH][2][BMAXN];  // every head's (da_src, da_dst), for the dU pass
   __shared__ unsigned char nbl[BMAXN][BDEG];
+  __shared__ unsigned char rev[BMAXN][BDEG];  // GAT: slot of n in nbl[nbl[n][q]] (0xff: none)
   __shared__ unsigned char ndeg[BMAXN];
   __shared__ float red[16][3 * BF];
 
@@ -121,10 +123,25 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
       for (int e = nbr_ptr[ln]; e < nbr_ptr[ln + 1] && d < BDEG; ++e) nbl[n][d++] = f0 + nbr_idx[e];
       if (kind == 0 && d < BDEG) nbl[n][d++] = n;
     }
+    for (int q = d; q < BDEG; ++q) nbl[n][q] = 0;  // unpredicated gathers read row 0, weight 0
     ndeg[n] = d;
   }
   __syncthreads();
   if (kind == 0) {
+    // reverse-edge slots, once per block (the per-head adjoint loops index them directly
+    // instead of searching the neighbour list of every neighbour)
+    for (int n = tid; n < NB; n += blockDim.x) {
+      const int d = ndeg[n];
+      for (int q = 0; q < BDEG; ++q) {
+        unsigned char r = 0xff;
+        if (q < d) {
+          const int i = nbl[n][q];
+          for (int p = ndeg[i] - 1; p >= 0; --p)
+            if (nbl[i][p] == n) r = (unsigned char)p;  // first match, as the search did
+        }
+        rev[n][q] = r;
+      }
+    }
     for (int i = tid; i < NB * 2 * BH; i += blockDim.x) {
       const int n = i >> 3, q = i & 7;
       float s = 0.f;
@@ -173,10 +190,14 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
         const int n = i >> 4, c4 = i & 15;
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
         const int d = n < NB ? ndeg[n] : 0;
-        for (int q = 0; q < d; ++q) {
-          const float w = kind == 0 ? ew[n][q] : 1.f;
-          const float4 v = *reinterpret_cast<const float4*>(xs + nbl[n][q] * BZP + c4 * 4);
-          a.x += w * v.x; a.y += w * v.y; a.z += w * v.z; a.w += w * v.w;
+        float4 v[BDEG];
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q)
+          v[q] = *reinterpret_cast<const float4*>(xs + nbl[n][q] * BZP + c4 * 4);
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q) {
+          const float w = q < d ? (kind == 0 ? ew[n][q] : 1.f) : 0.f;
+          a.x += w * v[q].x; a.y += w * v[q].y; a.z += w * v[q].z; a.w += w * v[q].w;
         }
         *reinterpret_cast<float4*>(bufA + n * BZP + c4 * 4) = a;
         if (n < NB) *reinterpret_cast<float4*>(ybuf + (node0 + n) * ywidth + seg * BF + c4 * 4) = a;
@@ -267,14 +288,19 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
         const int n = i >> 4, c4 = i & 15;
         const int d = ndeg[n];
         const float4 g = *reinterpret_cast<const float4*>(bufA + n * BZP + c4 * 4);
-        for (int q = 0; q < BDEG; ++q) {
-          float v = 0.f;
-          if (q < d) {
-            const float4 xv = *reinterpret_cast<const float4*>(xs + nbl[n][q] * BZP + c4 * 4);
-            v = g.x * xv.x + g.y * xv.y + g.z * xv.z + g.w * xv.w;
-          }
-          v = row16_sum(v);
-          if (c4 == 0) dsb[n][q] = v;
+        float4 xv[BDEG];
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q)
+          xv[q] = *reinterpret_cast<const float4*>(xs + nbl[n][q] * BZP + c4 * 4);
+        float v[BDEG];
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q)
+          v[q] = q < d ? g.x * xv[q].x + g.y * xv[q].y + g.z * xv[q].z + g.w * xv[q].w : 0.f;
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q) v[q] = row16_sum(v[q]);
+        if (c4 == 0) {
+#pragma unroll
+          for (int q = 0; q < BDEG; ++q) dsb[n][q] = v[q];
         }
       }
       __syncthreads();
@@ -293,17 +319,18 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
           sum += ds;
         }
         dal[n][1] = sum;
+        dalh[h][1][n] = sum;
       }
       __syncthreads();
       // da_src[j] = sum over the targets i that have j as a source (symmetric graph)
       for (int j = tid; j < NB; j += blockDim.x) {
         float s = 0.f;
         for (int q = 0; q < ndeg[j]; ++q) {
-          const int i = nbl[j][q];
-          for (int p = 0; p < ndeg[i]; ++p)
-            if (nbl[i][p] == j) { s += dsb[i][p]; break; }
+          const int p = rev[j][q];
+          if (p != 0xff) s += dsb[nbl[j][q]][p];
         }
         dal[j][0] = s;
+        dalh[h][0][j] = s;
       }
       __syncthreads();
       // dx += aggregation adjoint + logit adjoint;  dU partials
@@ -312,28 +339,36 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
         const int n = nr0 + 16 * r;
         if (n >= NB) continue;
         float a[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int q = 0; q < ndeg[n]; ++q) {
+        float4 gv[BDEG];
+        float al4[BDEG];
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q) {
           const int i = nbl[n][q];
-          float alpha = 0.f;
-          for (int p = 0; p < ndeg[i]; ++p)
-            if (nbl[i][p] == n) { alpha = ew[i][p]; break; }
-          const float4 g = *reinterpret_cast<const float4*>(bufA + i * BZP + cg * 4);
-          a[0] += alpha * g.x; a[1] += alpha * g.y; a[2] += alpha * g.z; a[3] += alpha * g.w;
+          const int p = rev[n][q];
+          gv[q] = *reinterpret_cast<const float4*>(bufA + i * BZP + cg * 4);
+          al4[q] = p != 0xff ? ew[i][p] : 0.f;  // 0xff past the degree
+        }
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q) {
+          a[0] += al4[q] * gv[q].x; a[1] += al4[q] * gv[q].y; a[2] += al4[q] * gv[q].z;
+          a[3] += al4[q] * gv[q].w;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           dxa[r][q] += a[q] + dal[n][0] * U[h][cg * 4 + q] + dal[n][1] * U[BH + h][cg * 4 + q];
       }
-      for (int k2 = 0; k2 < 2; ++k2) {
-        const int item = tid + 256 * k2;  // [8][64]
-        const int qq = item / BF, k = item % BF;
-        if ((qq & 3) != h) continue;
-        const int which = qq >> 2;  // 0: src, 1: dst
-        float s = 0.f;
-        for (int n = 0; n < NB; ++n) s += dal[n][which] * xs[n * BZP + k];
-        dU[k2] += s;
-      }
       __syncthreads();
+    }
+    // dU partials, all heads in one pass over the block's nodes (every thread: items tid and
+    // tid + 256 of [8][64], q = which * 4 + h)
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const int item = tid + 256 * k2;
+      const int qq = item / BF, k = item % BF;
+      const float* dl = dalh[qq & 3][qq >> 2];
+      float s = 0.f;
+      for (int n = 0; n < NB; ++n) s += dl[n] * xs[n * BZP + k];
+      dU[k2] = s;
     }
   } else {
     // dagg = do W_rel -> bufA ; dx_root = do W_root -> xs (x no longer needed)
@@ -352,10 +387,14 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
       float a[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) a[q] = xs[n * BZP + cg * 4 + q];
-      for (int q = 0; q < ndeg[n]; ++q) {
-        const float4 g = *reinterpret_cast<const float4*>(bufA + nbl[n][q] * BZP + cg * 4);
-        a[0] += g.x; a[1] += g.y; a[2] += g.z; a[3] += g.w;
-      }
+      const int dn = ndeg[n];
+      float4 gv[BDEG];
+#pragma unroll
+      for (int q = 0; q < BDEG; ++q)
+        gv[q] = *reinterpret_cast<const float4*>(bufA + nbl[n][q] * BZP + cg * 4);
+#pragma unroll
+      for (int q = 0; q < BDEG; ++q)
+        if (q < dn) { a[0] += gv[q].x; a[1] += gv[q].y; a[2] += gv[q].z; a[3] += gv[q].w; }
 #pragma unroll
       for (int q = 0; q < 4; ++q) dxa[r][q] += a[q];
     }
