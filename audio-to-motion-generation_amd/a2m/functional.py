@@ -360,6 +360,40 @@ def _bcl(t):
     return B, C, L, t.stride(0), t.stride(1)
 
 
+# SyncBatchNorm: when a process group is set, training BatchNorm all-reduces its
+# per-channel statistics (float64 sums) across the group in the forward and backward, so ranks
+# normalise over the whole data-parallel batch like the single-device step.  Every rank must
+# hold the same number of clips (n_total = world * local count).
+_sync_bn_group = None
+
+
+def set_sync_bn_group(group):
+    """Process group for SyncBN (torch.distributed default group: pass `dist.group.WORLD`), or
+    None for per-rank statistics (the default).  Returns the previous setting."""
+    global _sync_bn_group
+    prev, _sync_bn_group = _sync_bn_group, group
+    return prev
+
+
+def _sync_world():
+    if _sync_bn_group is None:
+        return 0
+    if hasattr(_sync_bn_group, 'all_reduce_sum'):   # an in-process group (tests/test_gpu_syncbn.py)
+        w = _sync_bn_group.size()
+    else:
+        import torch.distributed as dist
+        w = dist.get_world_size(_sync_bn_group)
+    return w if w > 1 else 0
+
+
+def _allreduce_sum_(t):
+    if hasattr(_sync_bn_group, 'all_reduce_sum'):
+        _sync_bn_group.all_reduce_sum(t)
+        return
+    import torch.distributed as dist
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_sync_bn_group)
+
+
 def bn_train(x, gamma, beta, rmean, rvar, momentum, eps, p, mode, seed, act, slope=0.2, out=None):
     """Training-mode BatchNorm fused with dropout and activation; updates rmean / rvar."""
     _check_dev(x, gamma, beta, rmean, rvar, out)
@@ -369,6 +403,16 @@ def bn_train(x, gamma, beta, rmean, rvar, momentum, eps, p, mode, seed, act, slo
     _, _, _, ysb, ysc = _bcl(out)
     mean = torch.empty(C, device=x.device)
     rstd = torch.empty(C, device=x.device)
+    world = _sync_world()
+    if world:
+        sums = torch.empty(C, 2, device=x.device, dtype=torch.float64)
+        _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_sync_stats_f32(
+            _p(x), xsb, xsc, B, C, L, p, mode, seed, _p(sums), wp, wn, _stream()))
+        _allreduce_sum_(sums)
+        N.check(N.lib.a2m_bn_sync_apply_f32(
+            _p(x), xsb, xsc, B, C, L, _p(sums), B * L * world, _p(gamma), _p(beta), _p(rmean), _p(rvar),
+            momentum, eps, p, mode, seed, act, slope, _p(out), ysb, ysc, _p(mean), _p(rstd), _stream()))
+        return out, mean, rstd
     _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_train_fwd_f32(
         _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(rmean), _p(rvar), momentum, eps, p, mode,
         seed, act, slope, _p(out), ysb, ysc, _p(mean), _p(rstd), wp, wn, _stream()))
@@ -383,6 +427,17 @@ def bn_train_bwd(dy, x, gamma, beta, mean, rstd, p, mode, seed, act, slope=0.2, 
     dg = torch.empty(C, device=x.device) if gamma is not None else None
     db = torch.empty(C, device=x.device) if beta is not None else None
     dbias = torch.empty(C, device=x.device) if want_bias else None
+    world = _sync_world()
+    if world:
+        sums = torch.empty(C, 2, device=x.device, dtype=torch.float64)
+        _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_sync_bwd_stats_f32(
+            _p(dy), dsb, dsc, _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(mean), _p(rstd), p, mode,
+            seed, act, slope, _p(sums), _p(dg), _p(db), wp, wn, _stream()))
+        _allreduce_sum_(sums)
+        _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_sync_bwd_apply_f32(
+            _p(dy), dsb, dsc, _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(mean), _p(rstd), p, mode,
+            seed, act, slope, _p(sums), B * L * world, _p(dx), _p(dbias), wp, wn, _stream()))
+        return dx, dg, db, dbias
     _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_train_bwd_f32(
         _p(dy), dsb, dsc, _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(mean), _p(rstd), p, mode,
         seed, act, slope, _p(dx), _p(dg), _p(db), _p(dbias), wp, wn, _stream()))

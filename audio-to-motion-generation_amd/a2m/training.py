@@ -19,6 +19,7 @@ import torch
 import torch.distributed as dist
 
 from . import autograd as AG
+from . import functional as F
 from .optim import FlatAdam
 
 
@@ -109,7 +110,7 @@ class GANTrainer:
     """One version5_model_train.py iteration per call, optionally data-parallel."""
 
     def __init__(self, generator, discriminator, lr=10e-4, lambda_gan=1.0, lambda_d=1.0,
-                 dynamic=None, fixed_labels=None, process_group=None):
+                 dynamic=None, fixed_labels=None, process_group=None, sync_bn=False):
         self.G, self.D = generator, discriminator
         self.opt_G = FlatAdam(generator.parameters(), lr=lr)
         self.opt_D = FlatAdam(discriminator.parameters(), lr=lr)
@@ -118,6 +119,9 @@ class GANTrainer:
         self.fixed_labels = fixed_labels          # (valid, fake) values for deterministic runs
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        # SyncBN: BatchNorm statistics all-reduced over the DP group, so the
+        # ranks normalise over the whole batch like the single-device reference step
+        self.sync_bn = bool(sync_bn) and self.world > 1
         self.last_d_loss = None
 
     def _allreduce_(self, t):
@@ -160,6 +164,15 @@ class GANTrainer:
 
     def iteration(self, audio, real_pose, epoch=0, g_freq=None, d_freq=None, sync_losses=True):
         """version5_model_train.py:330-414 for one batch; returns (D_loss, G_loss) tensors."""
+        if not self.sync_bn:
+            return self._iteration(audio, real_pose, epoch, g_freq, d_freq, sync_losses)
+        prev = F.set_sync_bn_group(self.pg if self.pg is not None else dist.group.WORLD)
+        try:
+            return self._iteration(audio, real_pose, epoch, g_freq, d_freq, sync_losses)
+        finally:
+            F.set_sync_bn_group(prev)
+
+    def _iteration(self, audio, real_pose, epoch, g_freq, d_freq, sync_losses):
         dev = audio.device
         gf = g_freq if g_freq is not None else self.dyn.g_train_freq
         df = d_freq if d_freq is not None else self.dyn.d_train_freq

@@ -131,6 +131,7 @@ struct BNBwdArgs {
   const float* dy; int64_t dys_b, dys_c;
   const float* mean; const float* rstd; const float* gamma; const float* beta;
   int act; float slope;
+  float n_div;  // element count the means divide by: B*L here, the all-rank total under SyncBN
 };
 
 // g = dL/d(bn output before act): dy * act' (* drop-after scale)
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a, const fl
   const int64_t N = (int64_t)f.B * f.L;
   const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
   const float mu = a.mean[c], rs = a.rstd[c], gm = a.gamma ? a.gamma[c] : 1.f;
-  const float mg = sums[2 * c] / (float)N, mgx = sums[2 * c + 1] / (float)N;
+  const float mg = sums[2 * c] / a.n_div, mgx = sums[2 * c + 1] / a.n_div;
   double sd = 0.0;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int b = (int)(i / f.L), l = (int)(i % f.L);
@@ -202,6 +203,45 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a, const fl
   }
   sd = block_sum_d(sd, red);
   if (threadIdx.x == 0) part[(int64_t)c * f.slices + s] = sd;
+}
+
+// SyncBN helpers: per-channel float64 (sum, sum2) pairs over the slices (all-reduced by the
+// host between the stats and apply phases), and the finalize / conversion steps on them.
+__global__ void reduce_pairs_kernel(const double* part, int C, int slices, double* sums,
+                                    float* lo_out, float* hi_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < slices; ++s) {
+    s1 += part[2 * ((int64_t)c * slices + s)];
+    s2 += part[2 * ((int64_t)c * slices + s) + 1];
+  }
+  sums[2 * c] = s1;
+  sums[2 * c + 1] = s2;
+  if (lo_out) lo_out[c] = (float)s1;  // backward: local dbeta = sum g
+  if (hi_out) hi_out[c] = (float)s2;  //           local dgamma = sum g xhat
+}
+
+__global__ void bn_finalize_sums_kernel(const double* sums, int C, int64_t N, float eps,
+                                        float momentum, float* rmean, float* rvar, float* mean_out,
+                                        float* rstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mean = sums[2 * c] / (double)N;
+  double var = sums[2 * c + 1] / (double)N - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  mean_out[c] = (float)mean;
+  rstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (rmean) {
+    const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+}
+
+__global__ void sums_to_float_kernel(const double* sums, int n, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (float)sums[i];
 }
 
 __global__ void reduce_slices_kernel(const double* part, int C, int slices, float* out) {
@@ -360,6 +400,7 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
   a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
   a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
   a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
+  a.n_div = (float)N;
   hipStream_t st = as_stream(stream);
   double* part = static_cast<double*>(ws);
   float* sums = reinterpret_cast<float*>(part + 2 * (size_t)C * S);
@@ -369,6 +410,107 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
                      sums, dgamma, dbeta);
   A2M_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(C * S), dim3(256), 0, st, a, sums, dx, part);
+  A2M_LAUNCH_CHECK();
+  if (dbias) {
+    hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C,
+                       S, dbias);
+    A2M_LAUNCH_CHECK();
+  }
+  return A2M_OK;
+}
+
+// ---- SyncBN phases (the fused entry points above split at their reductions)
+int a2m_bn_sync_stats_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
+                          int32_t L, float drop_p, int32_t drop_mode, uint64_t seed, double* sums,
+                          void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && sums && B > 0 && C > 0 && L > 0, "bn_sync_stats: bad args");
+  const int64_t N = (int64_t)B * L;
+  const int S = bn_slices(N);
+  const size_t need = sizeof(double) * 2 * (size_t)C * S;
+  if (!ws || ws_bytes < need) { set_error("bn_sync_stats: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
+  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  hipStream_t st = as_stream(stream);
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_pairs_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C, S,
+                     sums, nullptr, nullptr);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_bn_sync_apply_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
+                          int32_t L, const double* sums, int64_t n_total, const float* gamma,
+                          const float* beta, float* running_mean, float* running_var,
+                          float momentum, float eps, float drop_p, int32_t drop_mode,
+                          uint64_t seed, int32_t act, float slope, float* y, int64_t ys_b,
+                          int64_t ys_c, float* save_mean, float* save_rstd, void* stream) {
+  A2M_CHECK_ARG(x && y && sums && save_mean && save_rstd && B > 0 && C > 0 && L > 0 && n_total > 0,
+                "bn_sync_apply: bad args");
+  const int S = bn_slices((int64_t)B * L);
+  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, sums, C,
+                     n_total, eps, momentum, running_mean, running_var, save_mean, save_rstd);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(C * S), dim3(256), 0, st, a, save_mean, save_rstd, gamma,
+                     beta, act, slope, y, ys_b, ys_c);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_bn_sync_bwd_stats_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x,
+                              int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
+                              const float* gamma, const float* beta, const float* save_mean,
+                              const float* save_rstd, float drop_p, int32_t drop_mode,
+                              uint64_t seed, int32_t act, float slope, double* sums,
+                              float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(dy && x && sums && save_mean && save_rstd && B > 0 && C > 0 && L > 0,
+                "bn_sync_bwd_stats: bad args");
+  const int64_t N = (int64_t)B * L;
+  const int S = bn_slices(N);
+  const size_t need = sizeof(double) * 2 * (size_t)C * S;
+  if (!ws || ws_bytes < need) { set_error("bn_sync_bwd_stats: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
+  BNBwdArgs a;
+  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
+  a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
+  a.n_div = (float)N;
+  hipStream_t st = as_stream(stream);
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_pairs_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C, S,
+                     sums, dbeta, dgamma);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_bn_sync_bwd_apply_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x,
+                              int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
+                              const float* gamma, const float* beta, const float* save_mean,
+                              const float* save_rstd, float drop_p, int32_t drop_mode,
+                              uint64_t seed, int32_t act, float slope, const double* sums,
+                              int64_t n_total, float* dx, float* dbias, void* ws, size_t ws_bytes,
+                              void* stream) {
+  A2M_CHECK_ARG(dy && x && dx && sums && save_mean && save_rstd && B > 0 && C > 0 && L > 0 &&
+                n_total > 0, "bn_sync_bwd_apply: bad args");
+  const int64_t N = (int64_t)B * L;
+  const int S = bn_slices(N);
+  const size_t need = sizeof(double) * (size_t)C * S + sizeof(float) * 2 * (size_t)C + 16;
+  if (!ws || ws_bytes < need) { set_error("bn_sync_bwd_apply: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
+  BNBwdArgs a;
+  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
+  a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
+  a.n_div = (float)n_total;
+  hipStream_t st = as_stream(stream);
+  double* part = static_cast<double*>(ws);
+  float* fsums = reinterpret_cast<float*>(part + (size_t)C * S);
+  hipLaunchKernelGGL(sums_to_float_kernel, dim3((unsigned)cdiv(2 * C, 256)), dim3(256), 0, st, sums,
+                     2 * C, fsums);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(C * S), dim3(256), 0, st, a, fsums, dx, part);
   A2M_LAUNCH_CHECK();
   if (dbias) {
     hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C,

@@ -211,6 +211,35 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
                          const float* save_rstd, float drop_p, int32_t drop_mode, uint64_t seed,
                          int32_t act, float slope, float* dx, float* dgamma, float* dbeta,
                          float* dbias, void* ws, size_t ws_bytes, void* stream);
+/* SyncBatchNorm phases for data-parallel training (per-layer all-reduce of the
+ * BatchNorm statistics so DP over ranks normalises like the single-device batch,
+ * version5_model_train.py:342-414 at B = 64).  The fused bn_train_fwd/bwd above split at their
+ * per-channel reductions; the caller all-reduces (SUM) the float64 pairs between the phases:
+ *   fwd:  sync_stats -> sums[C][2] = (sum z, sum z^2) -> all-reduce -> sync_apply(n_total)
+ *   bwd:  sync_bwd_stats -> sums[C][2] = (sum g, sum g*xhat), local dbeta / dgamma
+ *         -> all-reduce -> sync_bwd_apply(n_total).   n_total = sum over ranks of B*L. */
+int a2m_bn_sync_stats_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
+                          int32_t L, float drop_p, int32_t drop_mode, uint64_t seed, double* sums,
+                          void* ws, size_t ws_bytes, void* stream);
+int a2m_bn_sync_apply_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
+                          int32_t L, const double* sums, int64_t n_total, const float* gamma,
+                          const float* beta, float* running_mean, float* running_var,
+                          float momentum, float eps, float drop_p, int32_t drop_mode,
+                          uint64_t seed, int32_t act, float slope, float* y, int64_t ys_b,
+                          int64_t ys_c, float* save_mean, float* save_rstd, void* stream);
+int a2m_bn_sync_bwd_stats_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x,
+                              int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
+                              const float* gamma, const float* beta, const float* save_mean,
+                              const float* save_rstd, float drop_p, int32_t drop_mode,
+                              uint64_t seed, int32_t act, float slope, double* sums,
+                              float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+int a2m_bn_sync_bwd_apply_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x,
+                              int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
+                              const float* gamma, const float* beta, const float* save_mean,
+                              const float* save_rstd, float drop_p, int32_t drop_mode,
+                              uint64_t seed, int32_t act, float slope, const double* sums,
+                              int64_t n_total, float* dx, float* dbias, void* ws, size_t ws_bytes,
+                              void* stream);
 /* nn.Dropout(p) with the hash mask (real_motion_model.py:203,255); backward = same call. */
 int a2m_dropout_f32(const float* x, int64_t n, float p, uint64_t seed, float* y, void* stream);
 /* y[c] (+)= sum_{b,t} x[b][c][t] (conv / linear bias gradients). */
