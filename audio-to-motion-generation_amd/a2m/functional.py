@@ -217,6 +217,9 @@ def stacked_qkv(wq, bq, wk, bk, wv, bv, cache=None):
     return w, b
 
 
+_ATTN_EVAL_FUSED = __import__('os').environ.get('A2M_ATTN_EVAL_FUSED', '1') != '0'
+
+
 def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=None, cache=None):
     """SelfAttention forward.  x, res, out: [B, C, T] with t contiguous and channel stride T.
     `save`, if a dict, receives the qkv and attention intermediates; `cache` (a dict owned by
@@ -229,9 +232,15 @@ def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=No
     assert out.stride(0) == x.stride(0) and out.stride(1) == T and out.stride(2) == 1
     if res is not None:
         assert res.stride() == out.stride()
+    wqkv, bqkv = stacked_qkv(wq, bq, wk, bk, wv, bv, cache)
+    if save is None and _ATTN_EVAL_FUSED and N.lib.a2m_self_attention_eval_fits(C, T) and \
+            x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 and N.lib.a2m_get_gemm_precision() == 0:
+        # inference: q/k/v projections fused into the attention core, one launch
+        N.check(N.lib.a2m_self_attention_eval_f32(_p(x), x.stride(0), B, C, T, _p(wqkv), _p(bqkv), _p(gamma),
+                                                  _p(res), _p(out), out.stride(0), _stream()))
+        return out
     qkv = torch.empty(B, C // 4 + C, T, device=x.device, dtype=x.dtype)
     attn = torch.empty(B, T, T, device=x.device, dtype=x.dtype)
-    wqkv, bqkv = stacked_qkv(wq, bq, wk, bk, wv, bv, cache)
     _with_ws(x.device, lambda wp, wn: N.lib.a2m_self_attention_packed_fwd_f32(
         _p(x), x.stride(0), B, C, T, _p(wqkv), _p(bqkv), _p(gamma),
         _p(res), _p(out), out.stride(0), _p(qkv), _p(attn), wp, wn, _stream()))

@@ -171,5 +171,10 @@ bool attn_core_fits(int C, int T);
 int attn_core(const float* qkv, int64_t qs_b, int B, int C, int T, const float* gamma,
               const float* x, int64_t x_bs, const float* res, float* y, float* attn_out,
               hipStream_t st);
+// Eval-only QKV + attention in one launch (C in {128, 256}, T <= 64, T % 4 == 0).
+bool attn_fused_eval_fits(int C, int T);
+int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const float* wqkv,
+                    const float* bqkv, const float* gamma, const float* res, float* y,
+                    hipStream_t st);
 
 }  // namespace a2m

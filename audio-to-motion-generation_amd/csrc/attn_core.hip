@@ -152,6 +152,217 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Eval-only fusion of the q/k/v 1x1 convolutions into the core (no qkv / attention outputs
+// are kept for a backward pass): one workgroup per (clip, 64-channel chunk of V), C in
+// {128, 256}, T <= 64.  The clip's x [C][T] is staged once in LDS as [t][c]; the four waves
+// compute Q^T and K^T ([64 t][C/8], bias added; waves 0-1 / 2-3) and then this chunk's V
+// ([64 c][64 t]) with B / A fragments of the stacked weights read from L2, after which the
+// score / softmax / PV / epilogue steps are those of attn_core_kernel.  Q and K are
+// recomputed by each of the C/64 chunks of a clip (C/8 of the C + C/4 projection rows), which
+// costs less than the round trip of qkv through HBM and a second launch.
+// ---------------------------------------------------------------------------------------
+constexpr int QP = 36;  // Q^T / K^T pitch (C/8 <= 32 columns): conflict-free b128 rows
+
+template <int TM>
+__device__ __forceinline__ void mfma_lds_l2(floatx16& acc, const float* arow_lds, const float* brow_g,
+                                            int K, int lh) {
+  // acc += A[32 rows][K] (LDS row pointer for this lane's row) . B[32 rows][K] (global row
+  // pointer for this lane's row); k-slot order k = 16 kc + 8 lh + s for both operands.  The
+  // global fragments run one k-chunk ahead.
+  float4 b0 = *reinterpret_cast<const float4*>(brow_g + lh * 8);
+  float4 b1 = *reinterpret_cast<const float4*>(brow_g + lh * 8 + 4);
+  for (int kc = 0; kc < K; kc += 16) {
+    float4 n0 = b0, n1 = b1;
+    if (kc + 16 < K) {
+      n0 = *reinterpret_cast<const float4*>(brow_g + kc + 16 + lh * 8);
+      n1 = *reinterpret_cast<const float4*>(brow_g + kc + 16 + lh * 8 + 4);
+    }
+    const float4 a0 = *reinterpret_cast<const float4*>(arow_lds + kc + lh * 8);
+    const float4 a1 = *reinterpret_cast<const float4*>(arow_lds + kc + lh * 8 + 4);
+    const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float bf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+    b0 = n0;
+    b1 = n1;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_fused_eval_kernel(
+    const float* __restrict__ x, int64_t x_bs, int C, int T, const float* __restrict__ wqkv,
+    const float* __restrict__ bqkv, const float* __restrict__ gamma, const float* __restrict__ res,
+    float* __restrict__ y) {
+  constexpr int XP = 256 + 4;                                    // [t][c] pitch, C <= 256
+  __shared__ __attribute__((aligned(16))) float xs[AT * XP];     // x^T, later the scores
+  __shared__ __attribute__((aligned(16))) float qs[AT * QP];     // Q^T [i][c']
+  __shared__ __attribute__((aligned(16))) float ks[AT * QP];     // K^T [j][c']
+  __shared__ __attribute__((aligned(16))) float vs[ACH * AP];    // V chunk [c][j]
+  float* ss = xs;
+  const int b = blockIdx.y, c0 = blockIdx.x * ACH;
+  const int Cq = C / 8;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const float* xb = x + (int64_t)b * x_bs;
+
+  {  // x [C][T] -> xs [t][c]: float4 along t, lanes along c (conflict-free LDS writes)
+    const int nq = C * (AT / 4);                                 // float4 slots of the tile
+    for (int base = 0; base < nq; base += 256 * 8) {
+      float4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = base + tid + j * 256;
+        const int c = e % C, tq = e / C;
+        v[j] = (e < nq && 4 * tq < T) ? *reinterpret_cast<const float4*>(xb + (int64_t)c * T + 4 * tq)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = base + tid + j * 256;
+        if (e >= nq) continue;
+        const int c = e % C, tq = e / C;
+        xs[(4 * tq + 0) * XP + c] = v[j].x;
+        xs[(4 * tq + 1) * XP + c] = v[j].y;
+        xs[(4 * tq + 2) * XP + c] = v[j].z;
+        xs[(4 * tq + 3) * XP + c] = v[j].w;
+      }
+    }
+  }
+  __syncthreads();
+
+  floatx16 acc;
+  // Q^T (waves 0, 1) and K^T (waves 2, 3): rows t = 32 (wave & 1) + li, columns c' < Cq = 32
+  {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int proj = wave >> 1, t0 = (wave & 1) * 32;
+    const float* wrow = wqkv + (int64_t)(proj * Cq + li) * C;   // B row c' = li (Cq = 32)
+    mfma_lds_l2<1>(acc, xs + (t0 + li) * XP, wrow, C, lh);
+    float* dst = proj ? ks : qs;
+    const float bias = bqkv[proj * Cq + li];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = t0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      dst[t * QP + li] = acc[r] + bias;
+    }
+  }
+  // V chunk: rows c = 32 wm + li of [c0, c0 + 64), columns t = 32 wn + li
+  {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // here A (weights) comes from L2 and B (x^T) from LDS: acc^T = B . A^T, so run the helper
+    // with the roles swapped and transpose on the way out
+    const float* wrow = wqkv + (int64_t)(2 * Cq + c0 + wm * 32 + li) * C;
+    mfma_lds_l2<1>(acc, xs + (wn * 32 + li) * XP, wrow, C, lh);
+    // acc[r] = out(row = t: 32 wn + (r&3) + 8 (r>>2) + 4 lh, col = c: 32 wm + li)
+    const float bias = bqkv[2 * Cq + c0 + wm * 32 + li];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      vs[(wm * 32 + li) * AP + t] = t < T ? acc[r] + bias : 0.f;
+    }
+  }
+  __syncthreads();  // Q, K, V in LDS; x^T dead (ss reuses it)
+
+  // S[i][j] = sum_c' Q^T[i][c'] K^T[j][c']
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  {
+    const int ia = wm * 32 + li, jb = wn * 32 + li;
+    for (int kc = 0; kc < Cq; kc += 16) {
+      const float4 a0 = *reinterpret_cast<const float4*>(qs + ia * QP + kc + lh * 8);
+      const float4 a1 = *reinterpret_cast<const float4*>(qs + ia * QP + kc + lh * 8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(ks + jb * QP + kc + lh * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(ks + jb * QP + kc + lh * 8 + 4);
+      const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+    ss[i * AP + wn * 32 + li] = acc[r];
+  }
+  __syncthreads();
+
+  {  // row softmax over j < T: four lanes per row, quad reductions in DPP
+    const int i = tid >> 2, part = tid & 3;
+    float* rowp = ss + i * AP + part * 16;
+    float e[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const float4 v4 = *reinterpret_cast<const float4*>(rowp + 4 * q4);
+      e[4 * q4] = v4.x; e[4 * q4 + 1] = v4.y; e[4 * q4 + 2] = v4.z; e[4 * q4 + 3] = v4.w;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (part * 16 + q >= T) e[q] = -INFINITY;
+      mx = fmaxf(mx, e[q]);
+    }
+    mx = quad_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      e[q] = part * 16 + q < T ? expf(e[q] - mx) : 0.f;
+      sum += e[q];
+    }
+    sum = quad_sum(sum);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) e[q] = i < T ? e[q] * inv : 0.f;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4)
+      *reinterpret_cast<float4*>(rowp + 4 * q4) = make_float4(e[4 * q4], e[4 * q4 + 1], e[4 * q4 + 2], e[4 * q4 + 3]);
+  }
+  __syncthreads();
+
+  // out[c][i] = sum_j V[c][j] A[i][j]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  {
+    const int ca = wm * 32 + li, ib = wn * 32 + li;
+    for (int kc = 0; kc < AT; kc += 16) {
+      const float4 a0 = *reinterpret_cast<const float4*>(vs + ca * AP + kc + lh * 8);
+      const float4 a1 = *reinterpret_cast<const float4*>(vs + ca * AP + kc + lh * 8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(ss + ib * AP + kc + lh * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(ss + ib * AP + kc + lh * 8 + 4);
+      const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+    }
+  }
+  const float g = gamma[0];
+  const int i = wn * 32 + li;
+  if (i < T) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = c0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (c >= C) continue;
+      const int64_t o = (int64_t)b * x_bs + (int64_t)c * T + i;
+      float val = g * acc[r] + xb[(int64_t)c * T + i];
+      if (res) val += res[o];
+      y[o] = val;
+    }
+  }
+}
+
+bool attn_fused_eval_fits(int C, int T) { return T <= AT && T % 4 == 0 && (C == 128 || C == 256); }
+
+int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const float* wqkv,
+                    const float* bqkv, const float* gamma, const float* res, float* y,
+                    hipStream_t st) {
+  dim3 grid((unsigned)cdiv(C, ACH), (unsigned)B);
+  hipLaunchKernelGGL(attn_fused_eval_kernel, grid, dim3(256), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
+                     res, y);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
 bool attn_core_fits(int C, int T) { return T <= AT && C % 8 == 0 && C / 8 <= AT && (C / 8) % 16 == 0; }
 
 int attn_core(const float* qkv, int64_t qs_b, int B, int C, int T, const float* gamma,

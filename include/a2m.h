@@ -142,6 +142,15 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
                                       float* qkv_out, float* attn_out, void* ws, size_t ws_bytes,
                                       void* stream);
 
+/* Inference-only SelfAttention with the q/k/v projections fused into the attention core (one
+ * launch; no qkv / attention intermediates).  Supported when a2m_self_attention_eval_fits(C, T):
+ * C in {128, 256}, T <= 64, T % 4 == 0 (the decoders' SelfAttention(256) at T = 64).
+ * Same arguments and results as a2m_self_attention_packed_fwd_f32 otherwise. */
+int32_t a2m_self_attention_eval_fits(int32_t C, int32_t T);
+int a2m_self_attention_eval_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
+                                const float* wqkv, const float* bqkv, const float* gamma,
+                                const float* res, float* y, int64_t y_bs, void* stream);
+
 /* ChannelAttention (model_layers.py:149-174): y = x * (mlp(avg_T x) + mlp(max_T x)),
  * mlp = Linear(C, C/r) -> ReLU -> Linear(C/r, C) -> Sigmoid.  x, y contiguous [B][C][T];
  * att_out [B][C] (required) receives the channel weights; y may alias x. */

@@ -141,8 +141,11 @@ def test_interp_time():
     assert rel_err(F.interp_time(x2.to(DEV), 480).cpu(), ref2) < TOL
 
 
-@pytest.mark.parametrize('B,C,T', [(2, 256, 64), (2, 2048, 16), (1, 64, 480), (3, 16, 5)])
+@pytest.mark.parametrize('B,C,T', [(2, 256, 64), (2, 2048, 16), (1, 64, 480), (3, 16, 5), (64, 256, 64),
+                                   (3, 128, 36)])
 def test_self_attention(B, C, T):
+    """Eval path: (B, 256, 64) / (B, 128, 36) run the fused QKV + attention kernel
+    (a2m_self_attention_eval_f32); the others the packed QKV GEMM + core / general path."""
     from a2m import functional as F
     from oracle import model as OM
     x, res = _rand(B, C, T, seed=50), _rand(B, C, T, seed=51)
@@ -158,6 +161,13 @@ def test_self_attention(B, C, T):
                            d['a.key_conv.weight'], d['a.key_conv.bias'], d['a.value_conv.weight'],
                            d['a.value_conv.bias'], d['a.gamma'], res=res.to(DEV))
     assert rel_err(out.cpu(), ref) < TOL
+    from a2m import _native as N
+    if N.lib.a2m_self_attention_eval_fits(C, T):  # the fused kernel equals the packed path
+        save = {}
+        out2 = F.self_attention(x.to(DEV), d['a.query_conv.weight'], d['a.query_conv.bias'],
+                                d['a.key_conv.weight'], d['a.key_conv.bias'], d['a.value_conv.weight'],
+                                d['a.value_conv.bias'], d['a.gamma'], res=res.to(DEV), save=save)
+        assert 'qkv' in save and rel_err(out.cpu(), out2.cpu()) < 2e-6
 
 
 def test_derived_weight_caches_follow_updates():
