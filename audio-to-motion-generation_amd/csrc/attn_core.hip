@@ -164,32 +164,39 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------------------
 constexpr int QP = 36;  // Q^T / K^T pitch (C/8 <= 32 columns): conflict-free b128 rows
 
-template <int TM>
-__device__ __forceinline__ void mfma_lds_l2(floatx16& acc, const float* arow_lds, const float* brow_g,
-                                            int K, int lh) {
-  // acc += A[32 rows][K] (LDS row pointer for this lane's row) . B[32 rows][K] (global row
-  // pointer for this lane's row); k-slot order k = 16 kc + 8 lh + s for both operands.  The
-  // global fragments run one k-chunk ahead.
-  float4 b0 = *reinterpret_cast<const float4*>(brow_g + lh * 8);
-  float4 b1 = *reinterpret_cast<const float4*>(brow_g + lh * 8 + 4);
-  for (int kc = 0; kc < K; kc += 16) {
-    float4 n0 = b0, n1 = b1;
-    if (kc + 16 < K) {
-      n0 = *reinterpret_cast<const float4*>(brow_g + kc + 16 + lh * 8);
-      n1 = *reinterpret_cast<const float4*>(brow_g + kc + 16 + lh * 8 + 4);
-    }
-    const float4 a0 = *reinterpret_cast<const float4*>(arow_lds + kc + lh * 8);
-    const float4 a1 = *reinterpret_cast<const float4*>(arow_lds + kc + lh * 8 + 4);
-    const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float bf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+// One lane's weight-row fragments for all of K = C <= 256 (k = 16 kc + 8 lh + s), loaded
+// into registers before the x tile is staged: the workgroup is alone on its CU (LDS-bound), so
+// the 128 VGPRs per row buy an MFMA loop with no L2 waits.
+constexpr int KC_MAX = 256 / 16;
+__device__ __forceinline__ void load_row_frags(float4 (&f)[KC_MAX][2], const float* row, int K, int lh) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
-    b0 = n0;
-    b1 = n1;
+  for (int kc = 0; kc < KC_MAX; ++kc) {
+    if (kc * 16 < K) {
+      f[kc][0] = *reinterpret_cast<const float4*>(row + kc * 16 + lh * 8);
+      f[kc][1] = *reinterpret_cast<const float4*>(row + kc * 16 + lh * 8 + 4);
+    } else {
+      f[kc][0] = f[kc][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void attn_fused_eval_kernel(
+// acc += A[32 rows][K] (this lane's LDS row) . B[32 rows][K] (this lane's register fragments)
+__device__ __forceinline__ void mfma_lds_reg(floatx16& acc, const float* arow_lds,
+                                             const float4 (&f)[KC_MAX][2], int K, int lh) {
+#pragma unroll
+  for (int kc = 0; kc < KC_MAX; ++kc) {
+    if (kc * 16 >= K) break;
+    const float4 a0 = *reinterpret_cast<const float4*>(arow_lds + kc * 16 + lh * 8);
+    const float4 a1 = *reinterpret_cast<const float4*>(arow_lds + kc * 16 + lh * 8 + 4);
+    const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float bf[8] = {f[kc][0].x, f[kc][0].y, f[kc][0].z, f[kc][0].w,
+                         f[kc][1].x, f[kc][1].y, f[kc][1].z, f[kc][1].w};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void attn_fused_eval_kernel(
     const float* __restrict__ x, int64_t x_bs, int C, int T, const float* __restrict__ wqkv,
     const float* __restrict__ bqkv, const float* __restrict__ gamma, const float* __restrict__ res,
     float* __restrict__ y) {
@@ -205,6 +212,10 @@ __global__ __launch_bounds__(256) void attn_fused_eval_kernel(
   const int li = lane & 31, lh = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
   const float* xb = x + (int64_t)b * x_bs;
+  // weight fragments first: this lane's Q/K projection row (c' = li) and V row (c0 + 32 wm + li)
+  float4 fqk[KC_MAX][2], fv[KC_MAX][2];
+  load_row_frags(fqk, wqkv + (int64_t)((wave >> 1) * Cq + li) * C, C, lh);
+  load_row_frags(fv, wqkv + (int64_t)(2 * Cq + c0 + wm * 32 + li) * C, C, lh);
 
   {  // x [C][T] -> xs [t][c]: float4 along t, lanes along c (conflict-free LDS writes)
     const int nq = C * (AT / 4);                                 // float4 slots of the tile
@@ -236,9 +247,8 @@ __global__ __launch_bounds__(256) void attn_fused_eval_kernel(
   {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const int proj = wave >> 1, t0 = (wave & 1) * 32;
-    const float* wrow = wqkv + (int64_t)(proj * Cq + li) * C;   // B row c' = li (Cq = 32)
-    mfma_lds_l2<1>(acc, xs + (t0 + li) * XP, wrow, C, lh);
+    const int proj = wave >> 1, t0 = (wave & 1) * 32;            // B row c' = li (Cq = 32)
+    mfma_lds_reg(acc, xs + (t0 + li) * XP, fqk, C, lh);
     float* dst = proj ? ks : qs;
     const float bias = bqkv[proj * Cq + li];
 #pragma unroll
@@ -253,8 +263,7 @@ __global__ __launch_bounds__(256) void attn_fused_eval_kernel(
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     // here A (weights) comes from L2 and B (x^T) from LDS: acc^T = B . A^T, so run the helper
     // with the roles swapped and transpose on the way out
-    const float* wrow = wqkv + (int64_t)(2 * Cq + c0 + wm * 32 + li) * C;
-    mfma_lds_l2<1>(acc, xs + (wn * 32 + li) * XP, wrow, C, lh);
+    mfma_lds_reg(acc, xs + (wn * 32 + li) * XP, fv, C, lh);
     // acc[r] = out(row = t: 32 wn + (r&3) + 8 (r>>2) + 4 lh, col = c: 32 wm + li)
     const float bias = bqkv[2 * Cq + c0 + wm * 32 + li];
 #pragma unroll

@@ -483,6 +483,48 @@ int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, i
                                     ws_bytes - pack_bytes, stream);
 }
 
+// im2col for conv2d over a live column range: col[n][k], n = (b, ho, wn) with wn over
+// [w_lo, w_hi), k = (ci, i, j) -- the dense [N][K] operand of the encoder convolutions
+// (model_layers.py:60-118 at the AudioEncoder shapes).  Rows are written along k, four
+// consecutive k per thread (float4 stores); the input reads are L2 hits (each element is read
+// kh*kw / stride^2 times).
+__global__ __launch_bounds__(256) void im2col2d_kernel(const float* __restrict__ x, int Ci, int H, int W,
+                                                       int kh, int kw, int stride, int ph, int pw,
+                                                       int Hout, int Wn, int w_lo, int K,
+                                                       float* __restrict__ col) {
+  // one workgroup per (b, ho): each thread decomposes its four k = (ci, i, j) once and then
+  // writes them for every live column wn (the k -> input-row arithmetic is amortised over Wn)
+  const int ho = blockIdx.x % Hout, b = blockIdx.x / Hout;
+  const int hb = ho * stride - ph;
+  const int khw = kh * kw;
+  float* rows = col + (int64_t)blockIdx.x * Wn * K;
+  for (int k0 = threadIdx.x * 4; k0 < K; k0 += blockDim.x * 4) {
+    const float* src[4];
+    int jj[4];
+    bool hv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k0 + q;
+      const int ci = k / khw, r = k - ci * khw;
+      const int i = r / kw, j = r - i * kw;
+      const int h = hb + i;
+      hv[q] = h >= 0 && h < H;
+      src[q] = x + ((int64_t)(b * Ci + ci) * H + (hv[q] ? h : 0)) * W;
+      jj[q] = j;
+    }
+    for (int wn = 0; wn < Wn; ++wn) {
+      const int wb = (w_lo + wn) * stride - pw;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int w = wb + jj[q];
+        v[q] = (hv[q] && w >= 0 && w < W) ? src[q][w] : 0.f;
+      }
+      *reinterpret_cast<float4*>(rows + (int64_t)wn * K + k0) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
 int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
                        const float* w, const float* bias, int32_t Co, int32_t kh, int32_t kw,
                        int32_t stride, int32_t pad_h, int32_t pad_w, const float* bn_w,
@@ -498,6 +540,30 @@ int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t
                 "conv2d: too large");
   const int Wn = w_hi - w_lo;
   Gather A = dense_rk(w, Ci * kh * kw);
+  static const int im2col2d_on = std::getenv("A2M_CONV2D_IM2COL") ? std::atoi(std::getenv("A2M_CONV2D_IM2COL")) : 1;
+  const int64_t K = (int64_t)Ci * kh * kw, N = (int64_t)B * Hout * Wn;
+  // explicit im2col into the workspace head, then a dense x dense GEMM, where the GEMM's gain
+  // over the gathered (mode-2) operand outweighs writing the [N][K] matrix: measured on the
+  // encoder, K >= 2048 (conv2 / conv3 / conv4: 26 / 22 / 18 us of im2col for 32 / 29 / 32 us
+  // of GEMM time saved); conv1 (K = 1024, 92 MB of columns at B = 64) loses.
+  if (im2col2d_on && Co >= 128 && K >= 2048 && K % 4 == 0 && N * K < (1LL << 31)) {
+    const size_t col_bytes = ((size_t)(N * K) * sizeof(float) + 255) & ~size_t(255);
+    const size_t need = col_bytes + gemm_ws_bytes(Co, (int)N, (int)K, 1);
+    if (!ws || ws_bytes < need) {
+      set_error("conv2d: workspace too small (%zu < %zu bytes)", ws_bytes, need);
+      return A2M_EWS;
+    }
+    float* col = static_cast<float*>(ws);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(im2col2d_kernel, dim3((unsigned)(B * Hout)), dim3(256), 0, st, x, Ci, H, W, kh,
+                       kw, stride, pad_h, pad_w, Hout, Wn, w_lo, (int)K, col);
+    A2M_LAUNCH_CHECK();
+    Gather Bd = dense_rk(col, (int)K);
+    Epilogue E = epi_bn(y + w_lo, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+    E.N1 = Hout; E.N2 = Wn; E.so0 = Co * Hout * Wout; E.so1 = Wout; E.so2 = 1; E.som = Hout * Wout;
+    return gemm(A, Bd, E, Co, (int)N, (int)K, 1, static_cast<char*>(ws) + col_bytes,
+                ws_bytes - col_bytes, st);
+  }
   Gather Bg{};
   Bg.base = x; Bg.sr0 = Ci * H * W; Bg.R1 = Hout; Bg.R2 = Wn; Bg.ar1 = stride; Bg.ar2 = stride;
   Bg.sk0 = H * W; Bg.K1 = kh; Bg.K2 = kw; Bg.bk1 = 1; Bg.bk2 = 1;

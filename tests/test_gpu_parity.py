@@ -129,6 +129,16 @@ def test_conv2d_column_range():
     ref2 = torch.nn.functional.conv2d(x, w2, None, stride=1, padding=(1, 3))
     out2 = F.conv2d(x.to(DEV), w2.to(DEV), None, 1, (1, 3))
     assert rel_err(out2.cpu(), ref2) < TOL
+    # Co >= 128: the explicit 2-D im2col + dense GEMM path (encoder layers), with and without
+    # a live-column window, stride 2 / k4 and stride 1 / (3, 8) kernels
+    x3 = _rand(3, 64, 16, 24, seed=34)
+    for w3, s3, p3, cols in ((_rand(128, 64, 4, 4, seed=35, scale=0.05), 2, (1, 1), (2, 9)),
+                             (_rand(128, 64, 3, 8, seed=36, scale=0.05), 1, (1, 3), None)):
+        ref3 = torch.nn.functional.conv2d(x3, w3, None, stride=s3, padding=p3)
+        out3 = torch.zeros(ref3.shape, device=DEV)
+        F.conv2d(x3.to(DEV), w3.to(DEV), None, s3, p3, cols=cols, out=out3)
+        lo, hi = cols if cols else (0, ref3.shape[-1])
+        assert rel_err(out3[..., lo:hi].cpu(), ref3[..., lo:hi]) < TOL
 
 
 def test_interp_time():

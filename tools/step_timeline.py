@@ -37,3 +37,8 @@ for s, e, n in iv:
 print('per-kernel time in this step:')
 for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
     print(f'  {t / 1e3:8.1f} us {c:4d} x  {n}')
+per_q = {}
+for r in win:
+    q = r.get('Queue_Id', '?')
+    per_q[q] = per_q.get(q, 0) + int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+print('kernel time per hardware queue:', {k: round(v / 1e3, 1) for k, v in per_q.items()})
