@@ -261,7 +261,11 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     if (p.bm == 128) launch_tile<128, 128, 64, true>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 64, true>(a, ma, mb, batch, stream);
   } else {
+    static const int ks2 = env_int("A2M_GEMM_KS2", 1);
     if (p.bm == 128) launch_tile<128, 128, 32, false>(a, ma, mb, batch, stream);
+    // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
+    // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end
+    else if (ks2 && ma == 0 && mb == 0) launch_tile<64, 64, 32, false, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, false>(a, ma, mb, batch, stream);
   }
   A2M_LAUNCH_CHECK();

@@ -459,15 +459,22 @@ __device__ __forceinline__ void mfma_half(const Frags<TM, TN, true>& f, floatx16
 // H = false: fp32 operands, v_mfma_f32_32x32x2_f32, BK = 32 (two 16-k halves).
 // H = true:  operands rounded to bf16 (RNE) when staged in LDS, v_mfma_f32_32x32x16_bf16 with
 //            fp32 accumulation, BK = 64 (two 32-k halves of two K16 chunks).
-template <int BM, int BN, int BK, int MA, int MB, bool H>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
+// KS = 2 (64x64 fp32 tile): 512 threads, two wave groups on the same output subtiles, group g
+// running the MFMAs of k-half g of every k-tile (so each SIMD holds two waves that fill each
+// other's issue gaps at one block per CU); group 0 stages the tiles, the partial accumulators
+// are summed through LDS before the epilogue.  (The k-halves of one k-tile are added in a
+// different order than KS = 1: results agree to fp32 rounding, not bitwise.)
+template <int BM, int BN, int BK, int MA, int MB, bool H, int KS = 1>
+__global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
   static_assert(BK == (H ? 64 : 32), "the k-step pipeline assumes two halves per k-tile");
   constexpr int TM = BM / 64, TN = BN / 64;
   using LA = TileLoader<BM, BK, MA, H>;
   using LB = TileLoader<BN, BK, MB, H>;
   constexpr int STAGE = LA::TILE + LB::TILE;
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
-  const int tid = threadIdx.x;
+  static_assert(KS == 1 || (TM * TN * 16 * 256 <= 2 * STAGE), "KS = 2 partials must fit the stages");
+  const int grp = KS == 1 ? 0 : (int)(threadIdx.x >> 8);
+  const int tid = threadIdx.x & 255;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
@@ -513,37 +520,95 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 
   const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
-  Frags<TM, TN, H> f0, f1;
-  if (nk > 0) {
-    la.load(kbeg);
-    lb.load(kbeg);
-    la.store(lds);
-    lb.store(lds + LA::TILE);
-    if (nk > 1) {
-      la.load(kbeg + BK);
-      lb.load(kbeg + BK);
+  if constexpr (KS == 1) {
+    Frags<TM, TN, H> f0, f1;
+    if (nk > 0) {
+      la.load(kbeg);
+      lb.load(kbeg);
+      la.store(lds);
+      lb.store(lds + LA::TILE);
+      if (nk > 1) {
+        la.load(kbeg + BK);
+        lb.load(kbeg + BK);
+      }
     }
-  }
-  __syncthreads();
-  if (nk > 0) read_frags<BM, BN, TM, TN, H, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
-  for (int i = 0; i < nk; ++i) {
-    const float* cur = lds + (i & 1) * STAGE;
-    float* nxt = lds + ((i + 1) & 1) * STAGE;
-    if (i + 1 < nk) {
-      la.store(nxt);
-      lb.store(nxt + LA::TILE);
-    }
-    if (i + 2 < nk) {
-      la.load(kbeg + (i + 2) * BK);
-      lb.load(kbeg + (i + 2) * BK);
-    }
-    read_frags<BM, BN, TM, TN, H, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
-    mfma_half(f0, acc);
     __syncthreads();
-    if (i + 1 < nk) read_frags<BM, BN, TM, TN, H, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
-    mfma_half(f1, acc);
+    if (nk > 0) read_frags<BM, BN, TM, TN, H, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
+    for (int i = 0; i < nk; ++i) {
+      const float* cur = lds + (i & 1) * STAGE;
+      float* nxt = lds + ((i + 1) & 1) * STAGE;
+      if (i + 1 < nk) {
+        la.store(nxt);
+        lb.store(nxt + LA::TILE);
+      }
+      if (i + 2 < nk) {
+        la.load(kbeg + (i + 2) * BK);
+        lb.load(kbeg + (i + 2) * BK);
+      }
+      read_frags<BM, BN, TM, TN, H, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
+      mfma_half(f0, acc);
+      __syncthreads();
+      if (i + 1 < nk) read_frags<BM, BN, TM, TN, H, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
+      mfma_half(f1, acc);
+    }
+    __syncthreads();  // the m-contiguous epilogue reuses the stages
+  } else {
+    Frags<TM, TN, H> f;
+    if (grp == 0 && nk > 0) {
+      la.load(kbeg);
+      lb.load(kbeg);
+      la.store(lds);
+      lb.store(lds + LA::TILE);
+      if (nk > 1) {
+        la.load(kbeg + BK);
+        lb.load(kbeg + BK);
+      }
+    }
+    __syncthreads();
+    if (nk > 0) read_frags<BM, BN, TM, TN, H, LA, LB>(lds, lds + LA::TILE, grp, wm, wn, li, lh, f);
+    for (int i = 0; i < nk; ++i) {
+      float* nxt = lds + ((i + 1) & 1) * STAGE;
+      if (grp == 0) {
+        if (i + 1 < nk) {
+          la.store(nxt);
+          lb.store(nxt + LA::TILE);
+        }
+        if (i + 2 < nk) {
+          la.load(kbeg + (i + 2) * BK);
+          lb.load(kbeg + (i + 2) * BK);
+        }
+      }
+      mfma_half(f, acc);
+      __syncthreads();
+      if (i + 1 < nk) read_frags<BM, BN, TM, TN, H, LA, LB>(nxt, nxt + LA::TILE, grp, wm, wn, li, lh, f);
+    }
+    // sum the two groups' partial accumulators (group 1 -> LDS -> group 0)
+    __syncthreads();
+    constexpr int NQ = TM * TN * 16;
+    if (grp == 1) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) lds[((t * TN + u) * 16 + q) * 256 + tid] = acc[t][u][q];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[t][u][q] += lds[((t * TN + u) * 16 + q) * 256 + tid];
+    }
+    (void)NQ;
+    __syncthreads();  // the partials region is free again
+    if (grp == 1) {
+      if (args.mcontig) __syncthreads();  // the epilogue's one barrier
+      return;
+    }
   }
-  __syncthreads();  // the m-contiguous epilogue reuses the stages
 
   // epilogue
   if (args.mcontig) {
@@ -605,11 +670,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs args) {
 
 // Launch one tile configuration for the operand modes (ma, mb).  Instantiated per (tile, type)
 // in its own translation unit (gemm_f32_64.hip, ...), so the 25 mode pairs compile in parallel.
-template <int BM, int BN, int BK, bool H>
+template <int BM, int BN, int BK, bool H, int KS = 1>
 void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
-  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, H>), grid, dim3(256), 0, st, a); return; }
+  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, H, KS>), grid, dim3(256 * KS), 0, st, a); return; }
+  if constexpr (KS == 2) {  // dense operands only (gemm.hip)
+    A2M_L(0, 0)
+    return;
+  }
   A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3) A2M_L(0, 4)
   A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2) A2M_L(1, 3) A2M_L(1, 4)
   A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3) A2M_L(2, 4)
@@ -619,6 +688,7 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
 }
 
 extern template void launch_tile<64, 64, 32, false>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<64, 64, 32, false, 2>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 32, false>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 64, true>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 64, true>(const GemmArgs&, int, int, int, hipStream_t);
