@@ -434,6 +434,28 @@ __device__ __forceinline__ void read_frags(const float* As, const float* Bs, int
   }
 }
 
+// MFMA sub-steps [S0, S1) of a half (fp32: s = 0..7, bf16: c = 0..1)
+template <int S0, int S1, int TM, int TN>
+__device__ __forceinline__ void mfma_part(const Frags<TM, TN, false>& f, floatx16 (&acc)[TM][TN]) {
+#pragma unroll
+  for (int s = S0; s < S1; ++s)
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[t][s], f.b[u][s], acc[t][u], 0, 0, 0);
+}
+template <int S0, int S1, int TM, int TN>
+__device__ __forceinline__ void mfma_part(const Frags<TM, TN, true>& f, floatx16 (&acc)[TM][TN]) {
+#pragma unroll
+  for (int c = S0; c < S1; ++c)
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][c], f.b[u][c], acc[t][u], 0, 0, 0);
+}
+
 template <int TM, int TN>
 __device__ __forceinline__ void mfma_half(const Frags<TM, TN, false>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
@@ -541,15 +563,32 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
         la.store(nxt);
         lb.store(nxt + LA::TILE);
       }
+      __builtin_amdgcn_sched_barrier(0);  // the tile stores stay ahead of the fragment reads
       if (i + 2 < nk) {
         la.load(kbeg + (i + 2) * BK);
         lb.load(kbeg + (i + 2) * BK);
       }
       read_frags<BM, BN, TM, TN, H, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
       mfma_half(f0, acc);
-      __syncthreads();
+      // The step's barrier, pinned after the first half's MFMAs (left to itself the compiler
+      // hoists it above them, and __syncthreads' fence would also wait for the second half's
+      // fragment reads).  Only this wave's tile stores must have landed: LDS ops retire in
+      // order, so the 2 (TM + TN) fragment reads issued after them may stay in flight (the
+      // second half's MFMAs wait for them where they are used).  s_waitcnt simm16 on gfx950:
+      // vmcnt / expcnt at their maxima (no wait), lgkmcnt in bits 11:8.
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((2 * (TM + TN)) << 8));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // the next tile's first fragments are read behind the first MFMAs of this second half
+      // (issued right after the barrier they would be waited for before any MFMA: the compiler
+      // cannot tell them apart from the second half's own reads in the LDS counter)
+      constexpr int SPLIT = H ? 1 : 2;
+      mfma_part<0, SPLIT>(f1, acc);
+      __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < nk) read_frags<BM, BN, TM, TN, H, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
-      mfma_half(f1, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_part<SPLIT, H ? 2 : 8>(f1, acc);
     }
     __syncthreads();  // the m-contiguous epilogue reuses the stages
   } else {
