@@ -141,3 +141,52 @@ def test_dp_two_ranks_matches_single_process():
     p0, p1 = res[0][1], res[1][1]
     assert (p0[0] == p1[0]).all() and (p0[1] == p1[1]).all()         # bitwise-identical replicas
     assert p0[2] == p1[2] and p0[3] == p1[3]                        # identical branch inputs
+
+
+def _syncbn_worker(rank, world, port, q):
+    """SyncBN host plumbing over a real gloo group: the group seen by the BN wrappers during a
+    GANTrainer(sync_bn=True) iteration, the float64 SUM all-reduce, and restoration after."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from a2m import functional as F
+        from a2m.training import GANTrainer
+        _patch_ops()
+        seen = []
+
+        class RecG(TinyG):
+            def forward(self, audio, real_pose=None):
+                seen.append(F._sync_world())
+                return super().forward(audio, real_pose)
+
+        torch.manual_seed(11)
+        tr = GANTrainer(RecG(), TinyD(), lr=1e-2, fixed_labels=(0.93, 0.07), sync_bn=True)
+        audio, pose = _data()
+        tr.iteration(audio[rank::world], pose[rank::world], epoch=0, g_freq=1, d_freq=1)
+        after = F._sync_world()
+        prev = F.set_sync_bn_group(dist.group.WORLD)
+        t = torch.tensor([[1.5 + rank, 2.0 * rank]], dtype=torch.float64)
+        F._allreduce_sum_(t)
+        F.set_sync_bn_group(prev)
+        q.put((rank, (tr.sync_bn, seen, after, t.tolist())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_syncbn_plumbing_two_ranks():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_syncbn_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        sync_bn, seen, after, t = res[r]
+        assert sync_bn and seen and all(w == 2 for w in seen)   # every BN in the step sees 2 ranks
+        assert after == 0                                       # per-rank statistics restored
+        assert t == [[1.5 + 2.5, 2.0]]                          # SUM over the ranks, float64
