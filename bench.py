@@ -67,6 +67,57 @@ def g_forward_flops(B, T, C=256):
     return f * B
 
 
+def encoder_flops(B, T):
+    """Useful FLOPs of the AudioEncoder over its live columns."""
+    def conv(co, ci, k, L):
+        return 2 * co * ci * k * L
+    f = conv(64, 1, 16, T // 2 * 46) + conv(128, 64, 16, T // 4 * 22) + conv(256, 128, 16, T // 8 * 10)
+    f += conv(512, 256, 9, T // 8 * 8) + conv(256, 512, 24, T // 8 * 1)
+    return f * B
+
+
+def run_graphed(dev, fn, iters=20, reps=5):
+    """Average duration of fn() over `iters` launches captured in one HIP graph."""
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        fn()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(iters):
+                fn()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            g.replay()
+        e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / (iters * reps)
+
+
+def mel_encoder_roofline(dev, g, wave, mel_ms, mel_bytes, peak):
+    """north_star's mel + encoder path: the log-mel kernel (HBM-bound: wav in + mel out) and
+    the AudioEncoder (MFMA-bound: live-column FLOPs; its minimum HBM traffic, mel in + features
+    out + weights, is far below its FLOPs / ridge), each against its own roof, and the path as
+    sum_k max(F_k / P_flop, B_k / P_bw) / measured time."""
+    from a2m.mel_features import log_mel_batch
+    mel = log_mel_batch(wave)
+    B, T = mel.shape[0], mel.shape[1]
+    with torch.no_grad():
+        enc_ms = run_graphed(dev, lambda: g.audio_encoder(mel))
+    ef = encoder_flops(B, T)
+    wbytes = sum(p.numel() * 4 for p in g.audio_encoder.parameters())
+    eb = mel.numel() * 4 + B * 256 * T * 4 + wbytes
+    ideal_ms = mel_bytes / (HBM_PEAK_GBS * 1e9) * 1e3 + max(ef / (peak * 1e12), eb / (HBM_PEAK_GBS * 1e9)) * 1e3
+    return {'mel_ms': round(mel_ms, 4), 'encoder_ms': round(enc_ms, 4),
+            'encoder_achieved_tflops': round(ef / (enc_ms * 1e-3) / 1e12, 2), 'encoder_peak_tflops': peak,
+            'encoder_frac': round(ef / (enc_ms * 1e-3) / 1e12 / peak, 4),
+            'encoder_gflop': round(ef / 1e9, 2),
+            'path_roofline_ms': round(ideal_ms, 4),
+            'path_frac': round(ideal_ms / (mel_ms + enc_ms), 4)}
+
+
 def gemm_engine_timing(step):
     """Run one eager step with every implicit-GEMM launch bracketed by HIP events on its own
     stream (a2m_gemm_timing_*): the engine's launches/step, algorithmic FLOPs (2*M*N*K) and
@@ -322,6 +373,7 @@ def main():
         value = world * B * T / (elapsed / args.steps)
         gt = gemm_engine_timing(step)
         mel_ms, mel_bytes = run_mel_kernel(dev, wave)
+        mel_enc = mel_encoder_roofline(dev, g, wave, mel_ms, mel_bytes, mfma_peak(args.dtype))
     path_tf = g_forward_flops(B, T) / (ms_step * 1e-3) / 1e12
     peak = mfma_peak(args.dtype)
     if args.dtype == 'bf16':
@@ -346,6 +398,7 @@ def main():
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(mel_bytes / (mel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          'ms_per_launch': round(mel_ms, 4)},
+        'mel_encoder_roofline': mel_enc,
         'path_roofline': {'bound': 'mfma', 'achieved': round(path_tf, 2), 'peak': peak,
                           'unit': 'TFLOP/s', 'frac': round(path_tf / peak, 4),
                           'gflop_per_step': round(g_forward_flops(B, T) / 1e9, 1)},
