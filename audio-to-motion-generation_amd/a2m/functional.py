@@ -557,10 +557,18 @@ def self_attention_bwd(dy, x, weights, qkv, attn):
     dy = dy.contiguous()
     assert x.stride(0) == dy.stride(0) and x.stride(1) == T and x.stride(2) == 1
     dx = torch.empty(B, C, T, device=x.device)
-    dwq, dwk, dwv = torch.empty_like(wq), torch.empty_like(wk), torch.empty_like(wv)
-    dbq = torch.empty_like(bq) if bq is not None else None
-    dbk = torch.empty_like(bk) if bk is not None else None
-    dbv = torch.empty_like(bv) if bv is not None else None
+    # one buffer each for the weight and bias gradients: the library then reduces all three
+    # projections in one GEMM / one bias pass (train_attn.hip, packed_w / packed_b)
+    Cq = wq.shape[0]
+    dwcat = torch.empty(2 * Cq + C, C, device=x.device)
+    dwq, dwk, dwv = dwcat[:Cq].view_as(wq), dwcat[Cq:2 * Cq].view_as(wk), dwcat[2 * Cq:].view_as(wv)
+    if bq is not None and bk is not None and bv is not None:
+        dbcat = torch.empty(2 * Cq + C, device=x.device)
+        dbq, dbk, dbv = dbcat[:Cq], dbcat[Cq:2 * Cq], dbcat[2 * Cq:]
+    else:
+        dbq = torch.empty_like(bq) if bq is not None else None
+        dbk = torch.empty_like(bk) if bk is not None else None
+        dbv = torch.empty_like(bv) if bv is not None else None
     dg = torch.empty(1, device=x.device)
     need = N.lib.a2m_self_attention_bwd_ws_bytes(B, C, T)
     WS.get(x.device, need)

@@ -6,7 +6,13 @@ their .grad as views of one contiguous gradient buffer, so autograd accumulates 
 into it, the data-parallel all-reduce is a single collective over `flat_grad`, and the
 update is one launch over `flat`.  `param_groups[0]['lr']` may be changed between steps
 (DynamicGANTraining.adjust_learning_rates does).
+
+Every parameter starts on a 64-byte boundary of the buffer (ALIGN floats): the GEMM engine
+stages a 16-byte-aligned weight as a dense operand, a misaligned one through the slower
+gathered path (SelfAttention's 1-element gamma would otherwise shift every later weight).
+The padding holds zeros and its gradient stays zero.
 """
+ALIGN = 16
 import torch
 
 from . import functional as F
@@ -16,18 +22,15 @@ class FlatAdam:
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         self.params = [p for p in params if p.requires_grad]
         dev = self.params[0].device
-        n = sum(p.numel() for p in self.params)
-        self.flat = torch.empty(n, device=dev)
+        n = sum(-(-p.numel() // ALIGN) * ALIGN for p in self.params)
+        self.flat = torch.zeros(n, device=dev)
         self.flat_grad = torch.zeros(n, device=dev)
         self.exp_avg = torch.zeros(n, device=dev)
         self.exp_avg_sq = torch.zeros(n, device=dev)
-        off = 0
-        for p in self.params:
-            k = p.numel()
+        for p, (off, k) in zip(self.params, self._spans()):
             self.flat[off:off + k].copy_(p.detach().reshape(-1))
             p.data = self.flat[off:off + k].view_as(p)
             p.grad = self.flat_grad[off:off + k].view_as(p)
-            off += k
         self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)]
         self.step_count = 0
 
@@ -41,7 +44,7 @@ class FlatAdam:
         off = 0
         for p in self.params:
             yield off, p.numel()
-            off += p.numel()
+            off += -(-p.numel() // ALIGN) * ALIGN
 
     @torch.no_grad()
     def step(self):

@@ -67,6 +67,57 @@ __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
   }
 }
 
+// Many splits over few outputs (graph-layer weight gradients: 64 x 64 outputs, K up to 172,032
+// nodes, 128-256 splits): the per-thread serial sum above would be latency-bound on a handful of
+// blocks, so here 16 lanes of a block share one float4 of outputs, each summing the splits
+// s = lane, lane + 16, ... in order, and the 16 lane sums are added in lane order (a fixed order:
+// still bitwise reproducible).  Inner extent a multiple of 4.
+constexpr int RW_LANES = 16, RW_COLS = 16;
+__global__ __launch_bounds__(RW_LANES * RW_COLS) void splitk_reduce_wide_kernel(GemmArgs args,
+                                                                               int batch) {
+  __shared__ float4 red[RW_LANES][RW_COLS];
+  const int64_t MN = (int64_t)args.M * args.N;
+  const int S = args.splits;
+  const int inner = args.mcontig ? args.M : args.N;
+  const int col = threadIdx.x % RW_COLS, lane = threadIdx.x / RW_COLS;
+  const int64_t i = (int64_t)blockIdx.x * RW_COLS + col;
+  const int64_t total4 = MN * batch / 4;
+  const int64_t e = i * 4;
+  const int z = (int)(e / MN);
+  const int64_t mn = e - (int64_t)z * MN;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < total4) {
+    const float* p = args.partial + (int64_t)z * S * MN + mn;
+    int s = lane;
+    for (; s + 3 * RW_LANES < S; s += 4 * RW_LANES) {
+      const float4 a0 = *reinterpret_cast<const float4*>(p + (int64_t)s * MN);
+      const float4 a1 = *reinterpret_cast<const float4*>(p + (int64_t)(s + RW_LANES) * MN);
+      const float4 a2 = *reinterpret_cast<const float4*>(p + (int64_t)(s + 2 * RW_LANES) * MN);
+      const float4 a3 = *reinterpret_cast<const float4*>(p + (int64_t)(s + 3 * RW_LANES) * MN);
+      v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
+      v.x += a1.x; v.y += a1.y; v.z += a1.z; v.w += a1.w;
+      v.x += a2.x; v.y += a2.y; v.z += a2.z; v.w += a2.w;
+      v.x += a3.x; v.y += a3.y; v.z += a3.z; v.w += a3.w;
+    }
+    for (; s < S; s += RW_LANES) {
+      const float4 a = *reinterpret_cast<const float4*>(p + (int64_t)s * MN);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+  }
+  red[lane][col] = v;
+  __syncthreads();
+  if (lane != 0 || i >= total4) return;
+  for (int l = 1; l < RW_LANES; ++l) {
+    const float4 a = red[l][col];
+    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  }
+  const int o = (int)(mn / inner), in = (int)(mn - (int64_t)o * inner);
+  reduce_store(args, z, v.x, o, in);
+  reduce_store(args, z, v.y, o, in + 1);
+  reduce_store(args, z, v.z, o, in + 2);
+  reduce_store(args, z, v.w, o, in + 3);
+}
+
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v ? std::atoi(v) : dflt;
@@ -147,7 +198,7 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered, bool bf16) {
   const int force_tile = g_override_tile ? g_override_tile : env_tile;
   const int force_split = g_override_split ? g_override_split : env_split;
   const int BK = gemm_bk(bf16);
-  static const int cand_splits[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64};
+  static const int cand_splits[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256};
   Plan p{64, BK, 1, (int)(cdiv(std::max(K, 1), BK) * BK)};
   double best = 1e300;
   for (int tile : {64, 128}) {
@@ -194,16 +245,18 @@ struct GemmTiming {
   hipEvent_t e0, e1, e2;
   double flops;
   bool reduce;
+  char desc[96];   // shape/plan, printed per launch by a2m_gemm_timing_end under A2M_GEMM_LOG=2
 };
 static std::mutex g_timing_mu;
 static bool g_timing = false;
 static std::vector<GemmTiming> g_timing_recs;
 
-static long timing_open(double flops, hipStream_t st) {
+static long timing_open(double flops, const char* desc, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_timing_mu);
   if (!g_timing) return -1;
   GemmTiming t{};
   t.flops = flops;
+  std::snprintf(t.desc, sizeof(t.desc), "%s", desc);
   if (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess ||
       hipEventCreate(&t.e2) != hipSuccess)
     return -1;
@@ -256,7 +309,13 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   if (log_launches)
     std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
                  M, N, K, batch, p.bm, p.bk, p.splits, ma, mb, E.som, E.so0, E.so1, E.so2, E.N1, E.N2);
-  const long tm = g_timing ? timing_open(2.0 * M * N * (double)K * batch, stream) : -1;
+  long tm = -1;
+  if (g_timing) {
+    char desc[96];
+    std::snprintf(desc, sizeof(desc), "M=%d N=%d K=%d b=%d tile=%d split=%d modes=%d,%d", M, N, K,
+                  batch, p.bm, p.splits, ma, mb);
+    tm = timing_open(2.0 * M * N * (double)K * batch, desc, stream);
+  }
   if (bf16) {
     if (p.bm == 128) launch_tile<128, 128, 64, true>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 64, true>(a, ma, mb, batch, stream);
@@ -273,8 +332,14 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   if (p.splits > 1) {
     const int inner = a.mcontig ? M : N;
     const int64_t total = (int64_t)M * N * batch / ((inner & 3) == 0 ? 4 : 1);
-    const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, a, batch);
+    static const int wide_on = env_int("A2M_GEMM_WIDE_REDUCE", 1);
+    if (wide_on && (inner & 3) == 0 && p.splits >= 2 * RW_LANES && total <= 65536) {
+      hipLaunchKernelGGL(splitk_reduce_wide_kernel, dim3((unsigned)cdiv(total, RW_COLS)),
+                         dim3(RW_LANES * RW_COLS), 0, stream, a, batch);
+    } else {
+      const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, a, batch);
+    }
     A2M_LAUNCH_CHECK();
   }
   if (tm >= 0) timing_mark(tm, 2, p.splits > 1, stream);
@@ -324,6 +389,10 @@ int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, doubl
     }
     ++n;
     f += t.flops;
+    static const int log_launches = a2m::env_int("A2M_GEMM_LOG", 0);
+    if (log_launches >= 2)
+      std::fprintf(stderr, "a2m gemm-time %s tile %.1f us reduce %.1f us %.1f TF\n", t.desc,
+                   1e3 * a, 1e3 * b, a > 0 ? t.flops / (1e9 * a) : 0.0);
     mt += a;
     if (t.reduce) { mr += b; ++nr; }
     (void)hipEventDestroy(t.e0);

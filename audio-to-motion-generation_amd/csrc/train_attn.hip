@@ -173,6 +173,8 @@ size_t a2m_self_attention_bwd_ws_bytes(int32_t B, int32_t C, int32_t T) {
   g = std::max(g, gemm_ws_bytes(C / 8, T, T, B));
   g = std::max(g, gemm_ws_bytes(C, B * T, Cqkv, 1));
   g = std::max(g, gemm_ws_bytes(C, C, B * T, 1));
+  g = std::max(g, gemm_ws_bytes(Cqkv, C, B * T, 1));
+  g = std::max(g, gemm_ws_bytes(C / 8, C, B * T, 1));
   return s + g;
 }
 
@@ -241,13 +243,31 @@ int a2m_self_attention_bwd_f32(const float* dy, const float* x, int64_t bs, int3
   float* dws[3] = {dwq, dwk, dwv};
   float* dbs[3] = {dbq, dbk, dbv};
   const int rows[3] = {Cq, Cq, C}, offs[3] = {0, Cq, 2 * Cq};
+  // dwq|dwk|dwv (and dbq|dbk|dbv) laid out back to back, as the Python layer allocates them:
+  // one [Cqkv x C] GEMM and one bias reduction instead of three each
+  const bool packed_w = dwk == dwq + (size_t)Cq * C && dwv == dwk + (size_t)Cq * C;
+  const bool packed_b = dbq && dbk && dbv && dbk == dbq + Cq && dbv == dbk + Cq;
+  if (packed_w) {
+    Gather Ad = Bx;
+    Ad.base = dqkv;
+    Ad.sk0 = (int)qs_b;
+    rc = gemm(Ad, Bx, epi_dense(dwq, C), Cqkv, C, B * T, 1, gws, gbytes, st);
+    if (rc) return rc;
+  }
+  if (packed_b) {
+    rc = a2m_sum_bt_f32(dqkv, qs_b, T, 1, B, Cqkv, T, dbq, 0, stream);
+    if (rc) return rc;
+  }
   for (int i = 0; i < 3; ++i) {
+    if (packed_w && (packed_b || !dbs[i])) continue;
     Gather Ad = Bx;
     Ad.base = dqkv + (int64_t)offs[i] * T;
     Ad.sk0 = (int)qs_b;
-    rc = gemm(Ad, Bx, epi_dense(dws[i], C), rows[i], C, B * T, 1, gws, gbytes, st);
-    if (rc) return rc;
-    if (dbs[i]) {
+    if (!packed_w) {
+      rc = gemm(Ad, Bx, epi_dense(dws[i], C), rows[i], C, B * T, 1, gws, gbytes, st);
+      if (rc) return rc;
+    }
+    if (dbs[i] && !packed_b) {
       rc = a2m_sum_bt_f32(dqkv + (int64_t)offs[i] * T, qs_b, T, 1, B, rows[i], T, dbs[i], 0, stream);
       if (rc) return rc;
     }

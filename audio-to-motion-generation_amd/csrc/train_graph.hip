@@ -483,7 +483,7 @@ extern "C" int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t 
   const size_t b_part = al256(sizeof(float) * (size_t)blocks * BPART);
   const size_t b_red = al256(sizeof(float) * BPART);
   const size_t fixed = b_u + b_y + b_do + b_part + b_red;
-  const size_t need = fixed + gemm_ws_bytes(BF, BH * BF, (int)Nn, 1) + gemm_ws_bytes(BF, BF, (int)Nn, 2);
+  const size_t need = fixed + std::max(gemm_ws_bytes(BF, BF, (int)Nn, BH), gemm_ws_bytes(BF, BF, (int)Nn, 1));
   if (!ws || ws_bytes < need) {
     set_error("graph_layer_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need);
     return A2M_EWS;

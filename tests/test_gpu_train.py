@@ -262,6 +262,25 @@ def test_adam_matches_torch():
         opt.step()
     for p, q in zip(ps, pd):
         assert rel_err(q.detach().cpu(), p.detach()) < 1e-6
+    # every parameter (and its gradient view) starts on a 64-byte boundary of the flat buffers
+    for q in pd:
+        assert q.data_ptr() % 64 == 0 and q.grad.data_ptr() % 64 == 0
+
+
+@pytest.mark.parametrize('M,N,K,batch', [(64, 64, 172032, 1), (64, 64, 172032, 4), (64, 64, 40960, 1),
+                                         (32, 256, 4096, 1), (320, 256, 4096, 1)])
+def test_gemm_many_splits_vs_fp64(M, N, K, batch):
+    """Weight-gradient shapes of a training step (graph layers: 64 x 64 outputs over every node;
+    SelfAttention Q|K|V): the planner splits K up to 256 ways and the split-K reduce runs its
+    16-lane variant for few outputs; compared with an fp64 matmul."""
+    from a2m import functional as F
+    A = _r(batch, M, K, seed=80)
+    B = _r(batch, N, K, seed=81)
+    C = torch.empty(batch, M, N, device=DEV)
+    F.gemm(M, N, K, A.to(DEV), K, 1, B.to(DEV), K, 1, C, N, 1, batch=batch, a_bs=M * K, b_bs=N * K,
+           c_bs=M * N)
+    ref = torch.bmm(A.double(), B.double().transpose(1, 2))
+    assert rel_err(C.cpu().double(), ref) < TOL
 
 
 def test_dropout_mask_statistics():
