@@ -483,8 +483,8 @@ __device__ __forceinline__ void mfma_half(const Frags<TM, TN, true>& f, floatx16
 //            fp32 accumulation, BK = 64 (two 32-k halves of two K16 chunks).
 // KS = 2 (64x64 fp32 tile): 512 threads, two wave groups on the same output subtiles, group g
 // running the MFMAs of k-half g of every k-tile (so each SIMD holds two waves that fill each
-// other's issue gaps at one block per CU); group 0 stages the tiles, the partial accumulators
-// are summed through LDS before the epilogue.  (The k-halves of one k-tile are added in a
+// other's issue gaps at one block per CU); the groups stage alternate k-tiles, the partial
+// accumulators are summed through LDS before the epilogue.  (The k-halves of one k-tile are added in a
 // different order than KS = 1: results agree to fp32 rounding, not bitwise.)
 template <int BM, int BN, int BK, int MA, int MB, bool H, int KS = 1>
 __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
@@ -592,13 +592,21 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
     }
     __syncthreads();  // the m-contiguous epilogue reuses the stages
   } else {
+    // The groups take turns staging: group j % 2 loads k-tile j three steps ahead and stores it
+    // one step ahead, so a tile's global loads have two k-steps to land (one with a single
+    // staging group) at no extra registers.
     Frags<TM, TN, H> f;
-    if (grp == 0 && nk > 0) {
-      la.load(kbeg);
-      lb.load(kbeg);
-      la.store(lds);
-      lb.store(lds + LA::TILE);
-      if (nk > 1) {
+    if (nk > 0) {
+      if (grp == 0) {
+        la.load(kbeg);
+        lb.load(kbeg);
+        la.store(lds);
+        lb.store(lds + LA::TILE);
+        if (nk > 2) {
+          la.load(kbeg + 2 * BK);
+          lb.load(kbeg + 2 * BK);
+        }
+      } else if (nk > 1) {
         la.load(kbeg + BK);
         lb.load(kbeg + BK);
       }
@@ -607,14 +615,14 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
     if (nk > 0) read_frags<BM, BN, TM, TN, H, LA, LB>(lds, lds + LA::TILE, grp, wm, wn, li, lh, f);
     for (int i = 0; i < nk; ++i) {
       float* nxt = lds + ((i + 1) & 1) * STAGE;
-      if (grp == 0) {
+      if (grp == ((i + 1) & 1)) {
         if (i + 1 < nk) {
           la.store(nxt);
           lb.store(nxt + LA::TILE);
         }
-        if (i + 2 < nk) {
-          la.load(kbeg + (i + 2) * BK);
-          lb.load(kbeg + (i + 2) * BK);
+        if (i + 3 < nk) {
+          la.load(kbeg + (i + 3) * BK);
+          lb.load(kbeg + (i + 3) * BK);
         }
       }
       mfma_half(f, acc);

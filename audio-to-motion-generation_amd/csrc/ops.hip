@@ -281,25 +281,44 @@ int stack_qkv(const float* wq, const float* bq, const float* wk, const float* bk
 }
 
 // im2col for conv1d over [B][C][T] (t contiguous): col[b*Tout + t][ci*ks + tap] =
-// x[b][ci][t*s + tap - pad] (0 outside).  One workgroup per (64 output steps, 16 channels,
+// x[b][ci][t*s + tap - pad] (0 outside).  One workgroup per (64 output steps, CC channels,
 // clip): the input window is staged through LDS with coalesced row loads, and every output row
-// segment (16*ks contiguous floats) is written by consecutive lanes.  The dense [N][K] result is
+// segment (CC*ks contiguous floats) is written by consecutive lanes.  The dense [N][K] result is
 // the engine's fastest operand form (mode 0), which the [B][C][T] gather cannot match.
-constexpr int I2C_T = 64, I2C_C = 16, I2C_SPAN = 2 * (I2C_T - 1) + 8;
+// Blocks are numbered XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so block L
+// runs on XCD L % 8; all CC-channel slices of one row tile get the same L % 8, and the row
+// segments they write side by side meet in that XCD's L2 as whole 128-byte lines instead of
+// being written back as partial lines from different L2s.  With CC = 32 a segment of a
+// 3- or 4-tap conv is itself a whole number of lines (384 / 512 B).
+constexpr int I2C_T = 64, I2C_SPAN = 2 * (I2C_T - 1) + 8;
+template <int CC>
 __global__ __launch_bounds__(256) void im2col1d_kernel(const float* __restrict__ x, int64_t xs_b,
                                                        int64_t xs_c, int Ci, int Tin, int Tout,
-                                                       int ks, int stride, int pad,
+                                                       int ks, int stride, int pad, int n_rows,
+                                                       int n_ctiles, int xcd_map,
                                                        float* __restrict__ col) {
-  __shared__ float win[I2C_C][I2C_SPAN + 1];
-  const int t0 = blockIdx.x * I2C_T, ci0 = blockIdx.y * I2C_C, b = blockIdx.z;
+  __shared__ float win[CC][I2C_SPAN + 1];
+  int r, ct;
+  if (xcd_map) {
+    const int L = blockIdx.x, xcd = L & 7, j = L >> 3;
+    ct = j % n_ctiles;
+    r = (j / n_ctiles) * 8 + xcd;
+    if (r >= n_rows) return;
+  } else {
+    ct = blockIdx.x % n_ctiles;
+    r = blockIdx.x / n_ctiles;
+  }
+  const int n_ttiles = (Tout + I2C_T - 1) / I2C_T;
+  const int b = r / n_ttiles, t0 = (r - b * n_ttiles) * I2C_T, ci0 = ct * CC;
   const int span = (I2C_T - 1) * stride + ks;
   const int tin0 = t0 * stride - pad;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* xb = x + (int64_t)b * xs_b;
-  // wave w stages channels w, w+4, w+8, w+12 (lanes along t): all loads issued first
-  float v[4][3];
+  // wave w stages channels w, w+4, w+8, ... (lanes along t): all loads issued first
+  constexpr int CW = CC / 4;
+  float v[CW][3];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < CW; ++j) {
     const int c = wave + 4 * j;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -308,21 +327,28 @@ __global__ __launch_bounds__(256) void im2col1d_kernel(const float* __restrict__
     }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < CW; ++j)
 #pragma unroll
     for (int q = 0; q < 3; ++q)
       if (lane + 64 * q < span) win[wave + 4 * j][lane + 64 * q] = v[j][q];
   __syncthreads();
-  // wave w writes rows w, w+4, ...; lane owns the fixed k offsets kk = lane, lane + 64
-  const int K = Ci * ks, seg = min(I2C_C, Ci - ci0) * ks;
+  // wave w writes rows w, w+4, ...; lane owns the fixed k offsets kk = lane + 64 q
+  const int K = Ci * ks, seg = min(CC, Ci - ci0) * ks;
   const int nt = min(I2C_T, Tout - t0);
-  const int kk0 = lane, kk1 = lane + 64;
-  const int c0 = kk0 / ks, tap0 = kk0 - c0 * ks, c1 = kk1 / ks, tap1 = kk1 - c1 * ks;
+  constexpr int NQ = CC * 8 / 64;   // ks <= 8
+  int src[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int kk = lane + 64 * q, c = kk / ks;
+    src[q] = c * (I2C_SPAN + 1) + (kk - c * ks);
+  }
+  const float* w0 = &win[0][0];
   float* base = col + ((int64_t)b * Tout + t0) * K + (int64_t)ci0 * ks;
   for (int tt = wave; tt < nt; tt += 4) {
     float* row = base + (int64_t)tt * K;
-    if (kk0 < seg) row[kk0] = win[c0][tt * stride + tap0];
-    if (kk1 < seg) row[kk1] = win[c1][tt * stride + tap1];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (lane + 64 * q < seg) row[lane + 64 * q] = w0[src[q] + tt * stride];
   }
 }
 
@@ -372,9 +398,17 @@ int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t,
     }
     float* col = static_cast<float*>(ws);
     hipStream_t st = as_stream(stream);
-    dim3 grid((unsigned)cdiv(Tout, I2C_T), (unsigned)cdiv(Ci, I2C_C), (unsigned)B);
-    hipLaunchKernelGGL(im2col1d_kernel, grid, dim3(256), 0, st, x, xs_b, xs_c, Ci, Tin, Tout, ks,
-                       stride, pad, col);
+    static const int cc_env = std::getenv("A2M_I2C_C") ? std::atoi(std::getenv("A2M_I2C_C")) : 16;
+    static const int xcd_env = std::getenv("A2M_I2C_XCD") ? std::atoi(std::getenv("A2M_I2C_XCD")) : 1;
+    const int cc = cc_env == 32 ? 32 : 16;   // 16 and 32 measured alike (tools/ab_i2c.sh)
+    const int n_rows = B * (int)cdiv(Tout, I2C_T), n_ct = (int)cdiv(Ci, cc);
+    const unsigned blocks = xcd_env ? (unsigned)(8 * n_ct * cdiv(n_rows, 8)) : (unsigned)(n_rows * n_ct);
+    if (cc == 16)
+      hipLaunchKernelGGL(im2col1d_kernel<16>, dim3(blocks), dim3(256), 0, st, x, xs_b, xs_c, Ci, Tin,
+                         Tout, ks, stride, pad, n_rows, n_ct, xcd_env, col);
+    else
+      hipLaunchKernelGGL(im2col1d_kernel<32>, dim3(blocks), dim3(256), 0, st, x, xs_b, xs_c, Ci, Tin,
+                         Tout, ks, stride, pad, n_rows, n_ct, xcd_env, col);
     A2M_LAUNCH_CHECK();
     Bg = dense_rk(col, (int)K);
     Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);

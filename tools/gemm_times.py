@@ -45,7 +45,7 @@ def child(mode):
 
 def main():
     pat = re.compile(r'a2m gemm-time (.*) tile ([\d.]+) us reduce ([\d.]+) us ([\d.]+) TF')
-    for mode in ('infer', 'train'):
+    for mode in os.environ.get('GT_MODES', 'infer,train').split(','):
         env = dict(os.environ, A2M_GEMM_LOG='2')
         r = subprocess.run([sys.executable, __file__, '--child', mode], env=env, capture_output=True,
                            text=True, timeout=300)
