@@ -86,6 +86,7 @@ SIGNATURES = {
     'a2m_diff_time_f32': (ctypes.c_int, [P, I32, I32, I32, P, P]),
     'a2m_diff_time_bwd_f32': (ctypes.c_int, [P, I32, I32, I32, P, I32, P]),
     'a2m_adam_f32': (ctypes.c_int, [P, P, P, P, I64, F32, F32, F32, F32, F32, I32, P]),
+    'a2m_gather_segments_f32': (ctypes.c_int, [P, P, P, I32, P, P]),
     'a2m_gemm_f32': (ctypes.c_int, [I32, I32, I32, I32, I32, I32, P, I64, I64, I64, I64, P, I64, I64, I64,
                                     I64, I64, P, I64, I64, I64, I64, P, F32, I32, P, SZ, P]),
     'a2m_pose_moments_f32': (ctypes.c_int, [P, I64, I32, P, P]),

@@ -676,6 +676,21 @@ def diff_time_bwd(dy, dx=None, accumulate=False):
     return dx
 
 
+def gather_segments_(dst, segments):
+    """dst[off:off + t.numel()] = t.reshape(-1) for every (off, t) in segments (contiguous fp32
+    device tensors), 48 segments per launch (a2m_gather_segments_f32)."""
+    if not segments:
+        return dst
+    _check_dev(dst, *[t for _, t in segments])
+    assert dst.is_contiguous() and all(t.is_contiguous() and t.dtype == torch.float32 for _, t in segments)
+    k = len(segments)
+    src = (ctypes.c_void_p * k)(*[t.data_ptr() for _, t in segments])
+    off = (ctypes.c_int64 * k)(*[o for o, _ in segments])
+    n = (ctypes.c_int64 * k)(*[t.numel() for _, t in segments])
+    N.check(N.lib.a2m_gather_segments_f32(src, off, n, k, _p(dst), _stream()))
+    return dst
+
+
 def adam_(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
     _check_dev(param, grad, exp_avg, exp_avg_sq)
     N.check(N.lib.a2m_adam_f32(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), lr, beta1,

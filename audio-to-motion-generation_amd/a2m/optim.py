@@ -1,10 +1,11 @@
 """Adam over a flat parameter buffer (torch.optim.Adam semantics, the optimiser of
 version5_model_train.py:285-286), one fused HIP kernel per step.
 
-On construction the module's parameters are re-seated as views of one contiguous buffer and
-their .grad as views of one contiguous gradient buffer, so autograd accumulates straight
-into it, the data-parallel all-reduce is a single collective over `flat_grad`, and the
-update is one launch over `flat`.  `param_groups[0]['lr']` may be changed between steps
+On construction the module's parameters are re-seated as views of one contiguous buffer.
+zero_grad() leaves .grad unset, so autograd's AccumulateGrad keeps each fresh gradient tensor
+as it is (no per-parameter add kernel), and collect_grads() gathers them into one contiguous
+gradient buffer with a few segment-gather launches; the data-parallel all-reduce is then a
+single collective over `flat_grad`, and the update is one launch over `flat`.  `param_groups[0]['lr']` may be changed between steps
 (DynamicGANTraining.adjust_learning_rates does).
 
 Every parameter starts on a 64-byte boundary of the buffer (ALIGN floats): the GEMM engine
@@ -35,10 +36,29 @@ class FlatAdam:
         self.step_count = 0
 
     def zero_grad(self, set_to_none=False):
+        """Zero the flat gradient and detach .grad from it: autograd then hands each parameter
+        its fresh gradient tensor (no per-parameter add), and collect_grads() gathers them all
+        into `flat_grad` in a few launches."""
         self.flat_grad.zero_()
+        for p in self.params:
+            p.grad = None
+
+    @torch.no_grad()
+    def collect_grads(self):
+        """Gather every .grad that is not already its view of `flat_grad` into the flat buffer
+        (a2m_gather_segments_f32) and re-seat .grad as that view.  Call before reducing
+        `flat_grad` across ranks; step() calls it too (a no-op the second time)."""
+        segs, seat = [], []
         for p, (o, k) in zip(self.params, self._spans()):
-            if p.grad is None or p.grad.data_ptr() != self.flat_grad[o:o + k].data_ptr():
-                p.grad = self.flat_grad[o:o + k].view_as(p)
+            view = self.flat_grad[o:o + k]
+            if p.grad is None:
+                seat.append((p, view))
+            elif p.grad.data_ptr() != view.data_ptr():
+                segs.append((o, p.grad.contiguous()))
+                seat.append((p, view))
+        F.gather_segments_(self.flat_grad, segs)
+        for p, view in seat:
+            p.grad = view.view_as(p)
 
     def _spans(self):
         off = 0
@@ -48,11 +68,7 @@ class FlatAdam:
 
     @torch.no_grad()
     def step(self):
-        # a gradient that autograd replaced instead of accumulating in place is folded back
-        for p, (o, k) in zip(self.params, self._spans()):
-            if p.grad is not None and p.grad.data_ptr() != self.flat_grad[o:o + k].data_ptr():
-                self.flat_grad[o:o + k].copy_(p.grad.reshape(-1))
-                p.grad = self.flat_grad[o:o + k].view_as(p)
+        self.collect_grads()
         self.step_count += 1
         g = self.param_groups[0]
         F.adam_(self.flat, self.flat_grad, self.exp_avg, self.exp_avg_sq, g['lr'], g['betas'][0],

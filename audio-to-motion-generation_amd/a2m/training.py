@@ -145,6 +145,7 @@ class GANTrainer:
         for loss in internal:
             g_loss = g_loss + loss
         g_loss.backward()
+        self.opt_G.collect_grads()
         self._allreduce_(self.opt_G.flat_grad)
         self.opt_G.step()
         return g_loss.detach()
@@ -158,6 +159,7 @@ class GANTrainer:
         real_d, _ = self.D(real_motion)
         d_loss = AG.mse_loss(real_d, valid) + self.lambda_d * AG.mse_loss(fake_d, fake)
         d_loss.backward()
+        self.opt_D.collect_grads()
         self._allreduce_(self.opt_D.flat_grad)
         self.opt_D.step()
         return d_loss.detach()

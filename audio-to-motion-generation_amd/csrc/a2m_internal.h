@@ -111,8 +111,17 @@ size_t gemm_ws_bytes(int M, int N, int K, int batch);
 int softmax_rows(float* x, int rows, int n, hipStream_t st);                       // ops.hip
 int stack_qkv(const float* wq, const float* bq, const float* wk, const float* bk,  // ops.hip
               const float* wv, const float* bv, int C, float* wcat, float* bcat, hipStream_t st);
+// Output segments of reduce_cols: column j goes to out[i][j - start[i]] for the last i with
+// start[i] <= j (start[0] = 0, n <= 4).
+struct ColOuts {
+  float* out[4];
+  int start[4];
+  int n;
+};
 int reduce_cols(const float* part, int rows, int stride, int cols, float* out,     // train_norm.hip
                 int accumulate, hipStream_t st);
+int reduce_cols(const float* part, int rows, int stride, int cols, const ColOuts& outs,
+                int accumulate, hipStream_t st);                                  // train_norm.hip
 
 inline Gather gather_bct(const float* x, int64_t bs, int cs, int T) {  // rows n=(b,t), k=c of [B][C][T]
   Gather g{};

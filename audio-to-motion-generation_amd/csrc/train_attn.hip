@@ -294,10 +294,13 @@ int a2m_channel_attention_bwd_f32(const float* dy, const float* x, int32_t B, in
   hipLaunchKernelGGL(channel_attention_bwd_kernel, dim3(B), dim3(256), lds, st, dy, x, C, T, w1, b1, Cr,
                      w2, b2, dx, part);
   A2M_LAUNCH_CHECK();
-  int rc = reduce_cols(part, B, P, Cr * C, dw1, 0, st);
-  if (!rc) rc = reduce_cols(part + Cr * C, B, P, Cr, db1, 0, st);
-  if (!rc) rc = reduce_cols(part + Cr * C + Cr, B, P, C * Cr, dw2, 0, st);
-  if (!rc) rc = reduce_cols(part + 2 * Cr * C + Cr, B, P, C, db2, 0, st);
+  ColOuts outs{};
+  outs.out[0] = dw1; outs.start[0] = 0;
+  outs.out[1] = db1; outs.start[1] = Cr * C;
+  outs.out[2] = dw2; outs.start[2] = Cr * C + Cr;
+  outs.out[3] = db2; outs.start[3] = 2 * Cr * C + Cr;
+  outs.n = 4;
+  int rc = reduce_cols(part, B, P, P, outs, 0, st);
   return rc;
 }
 

@@ -505,13 +505,15 @@ extern "C" int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t 
                      nbr_ptr, nbr_idx, w0, w1, Ug, bias, ln_w, ln_b, slope, dx, ybuf, dob, part);
   A2M_LAUNCH_CHECK();
   const int cols = kind == 0 ? BPART : 3 * BF;
-  int rc = reduce_cols(part, blocks, BPART, cols, redv, 0, st);
+  // dbias | dln_w | dln_b straight into the caller's vectors, the attention partials into redv
+  ColOuts outs{};
+  outs.out[0] = dbias; outs.start[0] = 0;
+  outs.out[1] = norm_res ? dln_w : redv + BF; outs.start[1] = BF;
+  outs.out[2] = norm_res ? dln_b : redv + 2 * BF; outs.start[2] = 2 * BF;
+  outs.out[3] = redv + 3 * BF; outs.start[3] = 3 * BF;
+  outs.n = cols > 3 * BF ? 4 : 3;
+  int rc = reduce_cols(part, blocks, BPART, cols, outs, 0, st);
   if (rc) return rc;
-  A2M_CHECK_HIP(hipMemcpyAsync(dbias, redv, sizeof(float) * BF, hipMemcpyDeviceToDevice, st));
-  if (norm_res) {
-    A2M_CHECK_HIP(hipMemcpyAsync(dln_w, redv + BF, sizeof(float) * BF, hipMemcpyDeviceToDevice, st));
-    A2M_CHECK_HIP(hipMemcpyAsync(dln_b, redv + 2 * BF, sizeof(float) * BF, hipMemcpyDeviceToDevice, st));
-  }
   // weight gradients: sum over all nodes of do (x) Y
   if (kind == 0) {
     // dW_h[c][k] = sum_n dout[n][c] Y[n][h*64 + k]   (batch over heads)

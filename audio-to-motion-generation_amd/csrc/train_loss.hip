@@ -322,6 +322,34 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, int64_
   }
 }
 
+// Segment gather: dst[off_i .. off_i + n_i) = src_i[0 .. n_i) for up to GS_MAX segments per
+// launch (FlatAdam: the step's per-parameter gradients, which autograd hands over as fresh
+// tensors, land in the flat gradient buffer in one launch instead of one add or copy per
+// parameter).  Block row y = segment; float4 when the segment is 16-byte aligned at both ends.
+constexpr int GS_MAX = 48;
+struct GatherSegs {
+  const float* src[GS_MAX];
+  int64_t off[GS_MAX];
+  int64_t n[GS_MAX];
+};
+
+__global__ void gather_segments_kernel(GatherSegs segs, float* __restrict__ dst) {
+  const int s = blockIdx.y;
+  const float* src = segs.src[s];
+  float* d = dst + segs.off[s];
+  const int64_t n = segs.n[s];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = i0; i < n4; i += stride)
+      reinterpret_cast<float4*>(d)[i] = reinterpret_cast<const float4*>(src)[i];
+    for (int64_t i = n4 * 4 + i0; i < n; i += stride) d[i] = src[i];
+  } else {
+    for (int64_t i = i0; i < n; i += stride) d[i] = src[i];
+  }
+}
+
 }  // namespace a2m
 
 using namespace a2m;
@@ -409,6 +437,30 @@ int a2m_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg
                      as_stream(stream), param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps,
                      weight_decay, (float)bc1, (float)std::sqrt(bc2));
   A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_gather_segments_f32(const float* const* src, const int64_t* dst_off, const int64_t* n,
+                            int32_t count, float* dst, void* stream) {
+  A2M_CHECK_ARG(count >= 0 && (count == 0 || (src && dst_off && n && dst)), "gather_segments: bad args");
+  hipStream_t st = as_stream(stream);
+  for (int c0 = 0; c0 < count; c0 += GS_MAX) {
+    GatherSegs segs{};
+    const int m = std::min(GS_MAX, count - c0);
+    int64_t maxn = 0;
+    for (int i = 0; i < m; ++i) {
+      A2M_CHECK_ARG(src[c0 + i] && n[c0 + i] >= 0 && dst_off[c0 + i] >= 0, "gather_segments: segment %d",
+                    c0 + i);
+      segs.src[i] = src[c0 + i];
+      segs.off[i] = dst_off[c0 + i];
+      segs.n[i] = n[c0 + i];
+      maxn = std::max(maxn, n[c0 + i]);
+    }
+    if (maxn == 0) continue;
+    const unsigned gx = (unsigned)std::min<int64_t>(cdiv(maxn, 4 * 256), 64);
+    hipLaunchKernelGGL(gather_segments_kernel, dim3(gx, (unsigned)m), dim3(256), 0, st, segs, dst);
+    A2M_LAUNCH_CHECK();
+  }
   return A2M_OK;
 }
 

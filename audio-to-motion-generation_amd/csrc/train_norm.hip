@@ -324,8 +324,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* dy, int
 // out[j] (+)= sum_i part[i*stride + j] in double.  One 1024-thread workgroup per 64 columns:
 // 16 row groups per column, each summing rows g, g+16, ... with 8 loads in flight, then the 16
 // partials combined in a fixed order (bitwise reproducible).
+// Column j lands in the output segment i with start[i] <= j < start[i + 1] (up to 4 segments:
+// one launch for several gradient vectors that share a partials row, e.g. dbias | dln_w | dln_b).
 __global__ __launch_bounds__(1024) void reduce_cols_kernel(const float* part, int rows, int stride,
-                                                           int cols, float* out, int accumulate) {
+                                                           int cols, ColOuts outs, int accumulate) {
   __shared__ double red[16][64];
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + c;
@@ -340,7 +342,10 @@ __global__ __launch_bounds__(1024) void reduce_cols_kernel(const float* part, in
     double t = 0.0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) t += red[q][c];
-    out[j] = (float)(accumulate ? out[j] + t : t);
+    int seg = 0;
+    while (seg + 1 < outs.n && j >= outs.start[seg + 1]) ++seg;
+    float* o = outs.out[seg] + (j - outs.start[seg]);
+    *o = (float)(accumulate ? *o + t : t);
   }
 }
 
@@ -348,8 +353,17 @@ static int bn_slices(int64_t N) { return (int)cdiv(N, kSlice); }
 
 int reduce_cols(const float* part, int rows, int stride, int cols, float* out, int accumulate,
                 hipStream_t st) {
+  ColOuts o{};
+  o.out[0] = out;
+  o.n = 1;
+  return reduce_cols(part, rows, stride, cols, o, accumulate, st);
+}
+
+int reduce_cols(const float* part, int rows, int stride, int cols, const ColOuts& outs,
+                int accumulate, hipStream_t st) {
+  A2M_CHECK_ARG(outs.n >= 1 && outs.n <= 4 && outs.start[0] == 0, "reduce_cols: bad segments");
   hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(cols, 64)), dim3(1024), 0, st, part,
-                     rows, stride, cols, out, accumulate);
+                     rows, stride, cols, outs, accumulate);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }
@@ -552,13 +566,11 @@ int a2m_layernorm_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_d, int64_t
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(blocks), dim3(256), sizeof(float) * 8 * D, st, dy,
                      dys_b, dys_d, dys_t, T, x, R, D, w, mean, rstd, dx, part);
   A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(D, 64)), dim3(1024), 0, st, part, blocks,
-                     2 * D, D, dw, 0);
-  A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)cdiv(D, 64)), dim3(1024), 0, st, part + D,
-                     blocks, 2 * D, D, db, 0);
-  A2M_LAUNCH_CHECK();
-  return A2M_OK;
+  ColOuts outs{};
+  outs.out[0] = dw; outs.start[0] = 0;
+  outs.out[1] = db; outs.start[1] = D;
+  outs.n = 2;
+  return reduce_cols(part, blocks, 2 * D, 2 * D, outs, 0, st);
 }
 
 }  // extern "C"

@@ -338,6 +338,14 @@ int a2m_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                  void* stream);
 
+/* dst[dst_off[i] .. dst_off[i] + n[i]) = src[i][0 .. n[i]) for i < count (host arrays of device
+ * pointers / element counts; segments must not overlap).  The optimiser's gradient collection:
+ * per-parameter gradient tensors into the flat gradient buffer, 48 segments per launch.
+ * Replaces torch's per-parameter AccumulateGrad add (version5_model_train.py:285-286 Adam over
+ * model.parameters()). */
+int a2m_gather_segments_f32(const float* const* src, const int64_t* dst_off, const int64_t* n,
+                            int32_t count, float* dst, void* stream);
+
 /* ---- Pose normalisation and evaluation ----
  * Poses are [n_frames][104] planar (x of 52 joints, then y), neck = joint 0.
  * a2m_pose_moments_f32: acc[0:104] += mean over the frames of (x - neck) (necksub = 1) or x,

@@ -63,6 +63,12 @@ def _patch_ops():
     AG.motion_terms = motion_terms
     AG.mse_loss = torch.nn.functional.mse_loss
     F.adam_ = adam_
+    def gather_segments_(dst, segs):
+        for o, t in segs:
+            dst[o:o + t.numel()].copy_(t.reshape(-1))
+        return dst
+
+    F.gather_segments_ = gather_segments_
 
 
 def _data():

@@ -257,7 +257,7 @@ def test_adam_matches_torch():
         opt.zero_grad()
         for p, q, g in zip(ps, pd, grads):
             p.grad = g.clone()
-            q.grad.copy_(g.to(DEV))
+            q.grad = g.to(DEV)   # a fresh tensor, as autograd hands it over: gathered by step()
         ref.step()
         opt.step()
     for p, q in zip(ps, pd):
