@@ -75,28 +75,6 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(BNArgs a, double* part) {
   }
 }
 
-__global__ void bn_finalize_kernel(const double* part, int C, int slices, int64_t N, float eps,
-                                   float momentum, float* rmean, float* rvar, float* mean_out,
-                                   float* rstd_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int s = 0; s < slices; ++s) {
-    s1 += part[2 * ((int64_t)c * slices + s)];
-    s2 += part[2 * ((int64_t)c * slices + s) + 1];
-  }
-  const double mean = s1 / (double)N;
-  double var = s2 / (double)N - mean * mean;
-  var = var > 0.0 ? var : 0.0;
-  mean_out[c] = (float)mean;
-  rstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (rmean) {
-    const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
-    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
-  }
-}
-
 __device__ __forceinline__ float act_fwd(float v, int act, float slope) {
   if (act == ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == ACT_LRELU) return v > 0.f ? v : v * slope;
@@ -107,6 +85,52 @@ __device__ __forceinline__ float act_grad(float pre, int act, float slope) {
   if (act == ACT_RELU) return pre > 0.f ? 1.f : 0.f;
   if (act == ACT_LRELU) return pre > 0.f ? 1.f : slope;
   return 1.f;
+}
+
+// The per-channel finalize (mean, rstd, running statistics) folded into the apply pass (one
+// launch fewer per BatchNorm layer): every workgroup of channel c reduces the channel's slice
+// partials in the same fixed order (so every workgroup gets the same mean / rstd bits), and the
+// slice-0 workgroup publishes them and updates the running statistics.
+__global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNArgs a, const double* part, float eps,
+                                                             float momentum, float* rmean,
+                                                             float* rvar, float* mean_out,
+                                                             float* rstd_out, const float* gamma,
+                                                             const float* beta, int act, float slope,
+                                                             float* y, int64_t ys_b, int64_t ys_c) {
+  __shared__ float stat[2];
+  const int c = blockIdx.x / a.slices, s = blockIdx.x % a.slices;
+  const int64_t N = (int64_t)a.B * a.L;
+  if (threadIdx.x == 0) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int q = 0; q < a.slices; ++q) {
+      s1 += part[2 * ((int64_t)c * a.slices + q)];
+      s2 += part[2 * ((int64_t)c * a.slices + q) + 1];
+    }
+    const double mean = s1 / (double)N;
+    double var = s2 / (double)N - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    stat[0] = (float)mean;
+    stat[1] = (float)(1.0 / sqrt(var + (double)eps));
+    if (s == 0) {
+      mean_out[c] = stat[0];
+      rstd_out[c] = stat[1];
+      if (rmean) {
+        const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
+        rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+        rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
+  const float mu = stat[0], rs = stat[1], g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int b = (int)(i / a.L), l = (int)(i % a.L);
+    const float z = a.x[b * a.xs_b + c * a.xs_c + l] * pre_drop(a, b, c, l);
+    float v = act_fwd((z - mu) * rs * g + bt, act, slope);
+    if (a.mode == DROP_AFTER) v *= drop_scale(a.seed, ((uint64_t)b * a.C + c) * a.L + l, a.p);
+    y[b * ys_b + c * ys_c + l] = v;
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_apply_kernel(BNArgs a, const float* mean, const float* rstd,
@@ -165,21 +189,6 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(BNBwdArgs a, double* 
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const double* part, int C, int slices, float* sums,
-                                       float* dgamma, float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sg = 0.0, sgx = 0.0;
-  for (int s = 0; s < slices; ++s) {
-    sg += part[2 * ((int64_t)c * slices + s)];
-    sgx += part[2 * ((int64_t)c * slices + s) + 1];
-  }
-  sums[2 * c] = (float)sg;
-  sums[2 * c + 1] = (float)sgx;
-  if (dgamma) dgamma[c] = (float)sgx;
-  if (dbeta) dbeta[c] = (float)sg;
-}
-
 // dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)); dx_raw = dz * drop-before scale;
 // partial sums of dx_raw (the conv bias gradient) per (channel, slice)
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a, const float* sums, float* dx,
@@ -203,6 +212,49 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a, const fl
   }
   sd = block_sum_d(sd, red);
   if (threadIdx.x == 0) part[(int64_t)c * f.slices + s] = sd;
+}
+
+// The backward's per-channel finalize folded into the apply pass, as in the forward: each workgroup reduces
+// its channel's (sum g, sum g xhat) partials in the fixed slice order, the slice-0 workgroup
+// writes dgamma / dbeta; the dbias partials go to their own region (dpart) because other
+// workgroups may still be reading `part`.
+__global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(BNBwdArgs a, const double* part,
+                                                                 float* dgamma, float* dbeta,
+                                                                 float* dx, double* dpart) {
+  __shared__ double red[4];
+  __shared__ float sums[2];
+  const BNArgs& f = a.f;
+  const int c = blockIdx.x / f.slices, s = blockIdx.x % f.slices;
+  if (threadIdx.x == 0) {
+    double sg = 0.0, sgx = 0.0;
+    for (int q = 0; q < f.slices; ++q) {
+      sg += part[2 * ((int64_t)c * f.slices + q)];
+      sgx += part[2 * ((int64_t)c * f.slices + q) + 1];
+    }
+    sums[0] = (float)sg;
+    sums[1] = (float)sgx;
+    if (s == 0) {
+      if (dgamma) dgamma[c] = sums[1];
+      if (dbeta) dbeta[c] = sums[0];
+    }
+  }
+  __syncthreads();
+  const int64_t N = (int64_t)f.B * f.L;
+  const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
+  const float mu = a.mean[c], rs = a.rstd[c], gm = a.gamma ? a.gamma[c] : 1.f;
+  const float mg = sums[0] / a.n_div, mgx = sums[1] / a.n_div;
+  double sd = 0.0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int b = (int)(i / f.L), l = (int)(i % f.L);
+    const float ds = pre_drop(f, b, c, l);
+    const float xhat = (f.x[b * f.xs_b + c * f.xs_c + l] * ds - mu) * rs;
+    const float g = bn_g(a, b, c, l, xhat);
+    const float v = gm * rs * (g - mg - xhat * mgx) * ds;
+    dx[((int64_t)b * f.C + c) * f.L + l] = v;
+    sd += v;
+  }
+  sd = block_sum_d(sd, red);
+  if (threadIdx.x == 0) dpart[(int64_t)c * f.slices + s] = sd;
 }
 
 // SyncBN helpers: per-channel float64 (sum, sum2) pairs over the slices (all-reduced by the
@@ -390,11 +442,9 @@ int a2m_bn_train_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, 
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL(bn_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
   A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C, S, N,
-                     eps, momentum, running_mean, running_var, save_mean, save_rstd);
-  A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(C * S), dim3(256), 0, st, a, save_mean, save_rstd, gamma,
-                     beta, act, slope, y, ys_b, ys_c);
+  hipLaunchKernelGGL(bn_apply_fused_kernel, dim3(C * S), dim3(256), 0, st, a, part, eps, momentum,
+                     running_mean, running_var, save_mean, save_rstd, gamma, beta, act, slope, y,
+                     ys_b, ys_c);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }
@@ -408,7 +458,7 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
   A2M_CHECK_ARG(dy && x && dx && save_mean && save_rstd && B > 0 && C > 0 && L > 0, "bn_train_bwd: bad args");
   const int64_t N = (int64_t)B * L;
   const int S = bn_slices(N);
-  const size_t need = sizeof(double) * 2 * (size_t)C * S + sizeof(float) * 2 * (size_t)C + 16;
+  const size_t need = sizeof(double) * 3 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_train_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNBwdArgs a;
   a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
@@ -417,16 +467,14 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
   a.n_div = (float)N;
   hipStream_t st = as_stream(stream);
   double* part = static_cast<double*>(ws);
-  float* sums = reinterpret_cast<float*>(part + 2 * (size_t)C * S);
+  double* dpart = part + 2 * (size_t)C * S;
   hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
   A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C, S,
-                     sums, dgamma, dbeta);
-  A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(C * S), dim3(256), 0, st, a, sums, dx, part);
+  hipLaunchKernelGGL(bn_bwd_apply_fused_kernel, dim3(C * S), dim3(256), 0, st, a, part, dgamma, dbeta,
+                     dx, dpart);
   A2M_LAUNCH_CHECK();
   if (dbias) {
-    hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, part, C,
+    hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, dpart, C,
                        S, dbias);
     A2M_LAUNCH_CHECK();
   }
