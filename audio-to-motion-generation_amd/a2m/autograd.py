@@ -63,11 +63,39 @@ class _ConvBNAct(torch.autograd.Function):
         return dx, dw, dbias, dg, db, None
 
 
+# BatchNorm's num_batches_tracked += 1 is one tiny int64 kernel per layer per forward (~150 an
+# iteration); inside a whole-model forward the increments are deferred and applied in one
+# multi-tensor launch at its end (torch._foreach_add_).
+_NBT = {'defer': 0, 'pending': []}
+
+
+def _count_batch(norm):
+    t = norm.num_batches_tracked
+    if t is None:
+        return
+    if _NBT['defer']:
+        _NBT['pending'].append(t)
+    else:
+        t.add_(1)
+
+
+class _deferred_batch_counters:
+    def __enter__(self):
+        _NBT['defer'] += 1
+
+    def __exit__(self, *exc):
+        _NBT['defer'] -= 1
+        if _NBT['defer'] == 0 and _NBT['pending']:
+            with torch.no_grad():
+                torch._foreach_add_(_NBT['pending'], 1)
+            _NBT['pending'].clear()
+        return False
+
+
 def _bn_cfg(norm, two_d, stride, pad, p, mode, act):
     if not norm.training:
         raise NotImplementedError('BatchNorm in eval mode with gradients: run evaluation under torch.no_grad()')
-    if norm.num_batches_tracked is not None:
-        norm.num_batches_tracked.add_(1)
+    _count_batch(norm)
     return dict(two_d=two_d, stride=stride, pad=pad, rm=norm.running_mean, rv=norm.running_var,
                 momentum=norm.momentum if norm.momentum is not None else 0.1, eps=norm.eps, p=p,
                 mode=mode, seed=next_seed() if p > 0 else 0, act=act, slope=0.2)
@@ -478,6 +506,11 @@ def graph_stack(g, part, x):
 
 
 def generator_forward(g, audio, real_pose=None):
+    with _deferred_batch_counters():
+        return _generator_forward(g, audio, real_pose)
+
+
+def _generator_forward(g, audio, real_pose=None):
     feats = g.unet(g.audio_encoder(audio))
     outs = []
     for part in ('body', 'hand'):
@@ -494,6 +527,11 @@ def generator_forward(g, audio, real_pose=None):
 
 
 def discriminator_forward(d, x):
+    with _deferred_batch_counters():
+        return _discriminator_forward(d, x)
+
+
+def _discriminator_forward(d, x):
     h = x.transpose(-1, -2)
     if h.shape[2] < 4:
         h = torch.nn.functional.pad(h, (0, 4 - h.shape[2] % 4))
