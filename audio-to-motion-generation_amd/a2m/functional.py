@@ -300,7 +300,7 @@ def pose_losses(gen, real=None):
     _check_dev(gen, real)
     B, T, Fd = gen.shape
     assert Fd == 104 and gen.stride(2) == 1
-    out = torch.zeros(2, device=gen.device)
+    out = torch.empty(2, device=gen.device)  # the final kernel writes both entries
     rs = real.stride() if real is not None else (0, 0, 1)
     if real is not None:
         assert real.stride(2) == 1

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void pose_loss_final_kernel(const float* part,
   const float Hs = block_sum(hs, red);
   const float Bs = block_sum(bs, red);
   if (threadIdx.x == 0) {
-    if (has_real) out[0] = Bn / (float)(B * kBones);
+    out[0] = has_real ? Bn / (float)(B * kBones) : 0.f;
     out[1] = 0.7f * (Hs / (float)(B * T * 30)) + 0.3f * (Bs / (float)(B * T * 5));
   }
 }

@@ -190,7 +190,7 @@ int a2m_graph_layer_fwd_f32(const float* x, int32_t F, int32_t J, int32_t kind,
  * compute_bone_length_loss (real_motion_model.py:307-347) and
  * compute_comprehensive_angle_loss (:449-461, hand :350-392, body :394-447) on interleaved
  * (x, y) poses [B][T][104] with element (b,t,f) at p + b*ps_b + t*ps_t + f.
- * out[0] = bone loss (only if real != NULL), out[1] = 0.7*hand + 0.3*body angle loss. */
+ * out[0] = bone loss (0 if real == NULL), out[1] = 0.7*hand + 0.3*body angle loss. */
 int a2m_pose_losses_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
                         int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float* out,
                         void* ws, size_t ws_bytes, void* stream);

@@ -279,7 +279,7 @@ def test_pose_losses_vs_reference():
     out = F.pose_losses(torch.from_numpy(z['gen']).to(DEV), torch.from_numpy(z['real']).to(DEV)).cpu()
     assert rel_err(out[0], z['bone']) < TOL and rel_err(out[1], z['angle']) < TOL
     out2 = F.pose_losses(torch.from_numpy(z['gen']).to(DEV)).cpu()
-    assert rel_err(out2[1], z['angle']) < TOL
+    assert rel_err(out2[1], z['angle']) < TOL and out2[0].item() == 0.0  # no real pose: bone 0
 
 
 # ------------------------------------------------------------------------------ full model
