@@ -308,8 +308,16 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # A2M_BENCH_BACKEND=gloo rehearses the N>1 path (barriers, max-over-ranks timing, the DP
+    # all-reduce) with several ranks sharing the GPUs of a smaller box; RCCL is the default
+    backend = os.environ.get('A2M_BENCH_BACKEND', 'nccl')
+    if backend != 'nccl':
+        local = local % torch.cuda.device_count()
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
     import a2m
