@@ -51,6 +51,7 @@ SIGNATURES = {
     'a2m_graph_layer_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32, P, P,
                                                P, P, SZ, P]),
     'a2m_pose_losses_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, P, P, SZ, P]),
+    'a2m_pose_losses_w_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, F32, F32, P, P, SZ, P]),
     # ---- training step
     'a2m_bn_train_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, P, P, F32, F32, F32, I32,
                                             U64, I32, F32, P, I64, I64, P, P, P, SZ, P]),
@@ -81,6 +82,7 @@ SIGNATURES = {
                                                P, P, P, P, P, P, P, SZ, P]),
     'a2m_interp_time_bwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, I32, P]),
     'a2m_pose_losses_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, P, P, P, SZ, P]),
+    'a2m_pose_losses_w_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, F32, F32, P, P, P, SZ, P]),
     'a2m_motion_losses_f32': (ctypes.c_int, [P, P, I32, I32, I32, P, P, P, P, SZ, P]),
     'a2m_mse_loss_f32': (ctypes.c_int, [P, P, I64, P, P, P, P, SZ, P]),
     'a2m_diff_time_f32': (ctypes.c_int, [P, I32, I32, I32, P, P]),

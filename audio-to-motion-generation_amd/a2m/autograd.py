@@ -417,17 +417,25 @@ def pos_to_motion(x):
 
 class _PoseLosses(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gen, real):
+    def forward(ctx, gen, real, angle_w=F.ANGLE_W):
         gen = gen.contiguous()
         ctx.save_for_backward(gen, real)
-        return F.pose_losses(gen, real)
+        ctx.angle_w = angle_w
+        return F.pose_losses(gen, real, angle_w)
 
     @staticmethod
     def backward(ctx, dl):
         gen, real = ctx.saved_tensors
         dgen = torch.zeros_like(gen)
-        F.pose_losses_bwd(gen, real, dl.contiguous(), dgen)
-        return dgen, None
+        F.pose_losses_bwd(gen, real, dl.contiguous(), dgen, ctx.angle_w)
+        return dgen, None, None
+
+
+def pose_losses(gen, real=None, angle_w=F.ANGLE_W):
+    """[bone, angle] with autograd when an input needs it (the plain HIP op otherwise)."""
+    if torch.is_grad_enabled() and (gen.requires_grad or (real is not None and real.requires_grad)):
+        return _PoseLosses.apply(gen, real, angle_w)
+    return F.pose_losses(gen.contiguous(), real.contiguous() if real is not None else None, angle_w)
 
 
 class _MotionTerms(torch.autograd.Function):
@@ -520,7 +528,7 @@ def _generator_forward(g, audio, real_pose=None):
         lg = getattr(g, f'{part}_logits')
         outs.append(conv1d(x, lg.weight, lg.bias))
     out = torch.cat(outs, 1).transpose(1, 2).contiguous()
-    losses = _PoseLosses.apply(out, real_pose)
+    losses = _PoseLosses.apply(out, real_pose, F.ANGLE_W)
     internal = [losses[0]] if real_pose is not None else []
     internal.append(losses[1])
     return out, internal

@@ -188,13 +188,16 @@ def repeat_time(x, out, scale=1.0):
 
 
 # ------------------------------------------------------------------------- attention
-# Parameters updated outside torch's in-place ops (FlatAdam's HIP kernel) do not bump
-# torch's version counters; the optimiser bumps this epoch instead.  Derived weight layouts
-# (stacked QKV, phase-packed convT) are cached under (epoch, data_ptr, _version) keys.
+# Derived weight layouts (stacked QKV, phase-packed convT) are cached under
+# (epoch, data_ptr, _version) keys.  Parameters written outside torch's version counters --
+# FlatAdam's HIP update, or any in-place write through `p.data` (p.data.copy_, an EMA) --
+# must call bump_weights_epoch(); FlatAdam.step() does, and every module that caches bumps it
+# from a load_state_dict post-hook.  torch.optim updates and p.copy_() under no_grad bump
+# the parameter's own _version and need nothing.
 WEIGHTS_EPOCH = [0]
 
 
-def bump_weights_epoch():
+def bump_weights_epoch(*_):
     WEIGHTS_EPOCH[0] += 1
 
 
@@ -295,8 +298,12 @@ def graph_layer(x, J, kind, nbr_ptr, nbr_idx, w0, w1, att_src, att_dst, bias, ln
 
 
 # ------------------------------------------------------------------------- losses
-def pose_losses(gen, real=None):
-    """Returns a [2] tensor: (bone loss or 0 if real is None, comprehensive angle loss)."""
+ANGLE_W = (0.7, 0.3)   # compute_comprehensive_angle_loss (real_motion_model.py:449-461)
+
+
+def pose_losses(gen, real=None, angle_w=ANGLE_W):
+    """Returns a [2] tensor: (bone loss or 0 if real is None, angle loss weighted
+    angle_w[0] * hand + angle_w[1] * body)."""
     _check_dev(gen, real)
     B, T, Fd = gen.shape
     assert Fd == 104 and gen.stride(2) == 1
@@ -304,9 +311,9 @@ def pose_losses(gen, real=None):
     rs = real.stride() if real is not None else (0, 0, 1)
     if real is not None:
         assert real.stride(2) == 1
-    _with_ws(gen.device, lambda wp, wn: N.lib.a2m_pose_losses_f32(
-        _p(gen), gen.stride(0), gen.stride(1), _p(real), rs[0], rs[1], B, T, _p(out), wp, wn,
-        _stream()))
+    _with_ws(gen.device, lambda wp, wn: N.lib.a2m_pose_losses_w_f32(
+        _p(gen), gen.stride(0), gen.stride(1), _p(real), rs[0], rs[1], B, T, angle_w[0], angle_w[1],
+        _p(out), wp, wn, _stream()))
     return out
 
 
@@ -621,13 +628,13 @@ def interp_time_bwd(dy, H, W):
     return dx
 
 
-def pose_losses_bwd(gen, real, grad_out, dgen):
+def pose_losses_bwd(gen, real, grad_out, dgen, angle_w=ANGLE_W):
     _check_dev(gen, real, grad_out, dgen)
     B, T, _ = gen.shape
     rs = real.stride() if real is not None else (0, 0, 1)
-    _with_ws(gen.device, lambda wp, wn: N.lib.a2m_pose_losses_bwd_f32(
-        _p(gen), gen.stride(0), gen.stride(1), _p(real), rs[0], rs[1], B, T, _p(grad_out.contiguous()),
-        _p(dgen), wp, wn, _stream()))
+    _with_ws(gen.device, lambda wp, wn: N.lib.a2m_pose_losses_w_bwd_f32(
+        _p(gen), gen.stride(0), gen.stride(1), _p(real), rs[0], rs[1], B, T, angle_w[0], angle_w[1],
+        _p(grad_out.contiguous()), _p(dgen), wp, wn, _stream()))
     return dgen
 
 

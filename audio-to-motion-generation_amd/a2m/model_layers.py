@@ -34,6 +34,38 @@ def _autograd():
     return autograd
 
 
+_MOVED_WARNED = []
+
+
+def stage_inputs(module, *tensors):
+    """Host-tensor entry for the top-level modules (generate_motion_video.py:257 calls
+    `generator(audio)` on CPU tensors with a CPU-constructed generator).  There is no CPU
+    compute path: a module whose parameters are still on the host is moved to the current
+    GPU once (in place, as `module.cuda()` would), and host inputs are copied to it.  Returns
+    (device tensors, the device the caller's first input lives on) so results can be handed
+    back there."""
+    p = next(module.parameters())
+    if not p.is_cuda:
+        if not torch.cuda.is_available():
+            raise RuntimeError('a2m modules compute on the GPU only (no CPU fallback) and no GPU is visible')
+        if not _MOVED_WARNED:
+            import warnings
+            warnings.warn(f'{type(module).__name__} had its parameters on the host: moved to '
+                          f'cuda:{torch.cuda.current_device()} (a2m computes on the GPU only)')
+            _MOVED_WARNED.append(True)
+        module.cuda()
+        p = next(module.parameters())
+    home = next((t.device for t in tensors if t is not None), p.device)
+    out = tuple(None if t is None else (t if t.device == p.device else t.to(p.device, non_blocking=True))
+                for t in tensors)
+    return out, home
+
+
+def to_home(home, *ts):
+    """Hand results back on the caller's device (no-op when it is the compute device)."""
+    return tuple(t if (t is None or t.device == home) else t.to(home) for t in ts)
+
+
 class ConvNormRelu(nn.Module):
     def __init__(self, in_channels, out_channels, type='1d', leaky=False, downsample=False,
                  kernel_size=None, stride=None, padding=None, p=0, groups=1):
@@ -98,6 +130,7 @@ class SelfAttention(nn.Module):
         self.value_conv = nn.Conv1d(in_channels, in_channels, kernel_size=1)
         self.gamma = nn.Parameter(torch.zeros(1))
         self._pack = {}   # stacked QKV weights for the eval path (functional.stacked_qkv)
+        self.register_load_state_dict_post_hook(F.bump_weights_epoch)
 
     def weights(self):
         return (self.query_conv.weight, self.query_conv.bias, self.key_conv.weight,
@@ -147,6 +180,7 @@ class ConvTranspose1D(nn.Module):
         self.bn = nn.BatchNorm1d(out_channels)
         self.relu = nn.ReLU(inplace=True)
         self._pack = {}   # phase-packed weights for the eval path (functional.convt_packed)
+        self.register_load_state_dict_post_hook(F.bump_weights_epoch)
 
     def forward(self, x, out=None):
         if _grad_path(self, x):

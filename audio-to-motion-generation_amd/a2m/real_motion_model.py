@@ -15,7 +15,7 @@ from . import functional as F
 from . import skeleton as S
 from .graph_layers import GATConv, GraphConv
 from .model_layers import (AudioEncoder, ChannelAttention, ConvNormRelu, ResBlock, SelfAttention,
-                           UNet1D, _autograd, _grad_path)
+                           UNet1D, _autograd, _grad_path, stage_inputs, to_home)
 
 
 class _GraphTopology(nn.Module):
@@ -126,6 +126,13 @@ class SelfAttention_G(_GraphTopology):
         F.conv1d(x, lg.weight, lg.bias, out=pose_out[:, :, f0:f0 + nf].permute(0, 2, 1))
 
     def forward(self, audio, real_pose=None):
+        (audio, real_pose), home = stage_inputs(self, audio, real_pose)
+        out, losses = self._forward(audio, real_pose)
+        if home != out.device:
+            out, *losses = to_home(home, out, *losses)
+        return out, list(losses)
+
+    def _forward(self, audio, real_pose=None):
         if _grad_path(self, audio):
             return _autograd().generator_forward(self, audio, real_pose)
         B, T, _ = audio.shape
@@ -151,11 +158,27 @@ class SelfAttention_G(_GraphTopology):
         return out, internal
 
     # ------------------------------------------------------------------ reference loss API
+    # real_motion_model.py:307-461; differentiable in gen_pose, host tensors staged like forward
+    def _pose_loss(self, gen_pose, real_pose, angle_w, which):
+        (gen_pose, real_pose), home = stage_inputs(self, gen_pose, real_pose)
+        assert gen_pose.shape[-1] == len(self.parents) * 2, 'Pose dimension mismatch'
+        loss = _autograd().pose_losses(gen_pose, real_pose, angle_w)[which]
+        return to_home(home, loss)[0]
+
     def compute_bone_length_loss(self, real_pose, gen_pose):
-        return F.pose_losses(gen_pose.contiguous(), real_pose.contiguous())[0]
+        assert real_pose.shape[-1] == len(self.parents) * 2, 'Pose dimension mismatch'
+        return self._pose_loss(gen_pose, real_pose, F.ANGLE_W, 0)
+
+    def compute_hand_joint_angle_loss(self, gen_pose):
+        return self._pose_loss(gen_pose, None, (1.0, 0.0), 1)
+
+    def compute_body_joint_angle_loss(self, gen_pose):
+        if gen_pose.shape[-1] != len(self.parents) * 2:   # :403-404
+            return torch.tensor(0.0, device=gen_pose.device)
+        return self._pose_loss(gen_pose, None, (0.0, 1.0), 1)
 
     def compute_comprehensive_angle_loss(self, gen_pose):
-        return F.pose_losses(gen_pose.contiguous())[1]
+        return self._pose_loss(gen_pose, None, F.ANGLE_W, 1)
 
 
 _BRANCH_STREAMS = os.environ.get('A2M_BRANCH_STREAMS', '1') != '0'
@@ -226,6 +249,11 @@ class SelfAttention_D(_GraphTopology):
         if audio is not None or aux_labels is not None:
             raise NotImplementedError('audio fusion / aux classifier are off the training path '
                                       '(version5_model_train.py never passes them)')
+        (x,), home = stage_inputs(self, x)
+        out, aux = self._forward(x)
+        return to_home(home, out)[0], aux
+
+    def _forward(self, x):
         if _grad_path(self, x):
             return _autograd().discriminator_forward(self, x), []
         h = x.transpose(-1, -2)

@@ -87,14 +87,30 @@ class DynamicGANTraining:
             grp['lr'] = d_lr
 
     def get_smooth_labels(self, epoch, batch_size, device, is_real=True, generator=None):
-        progress = min(max(epoch / 60.0, 0.0), 1.0)
-        noise_std = 0.01 - progress * (0.01 - 0.002)
+        """Annealed smoothed labels with Gaussian noise (version5_model_train.py:137-180): the
+        noise std falls linearly 0.01 -> 0.002 over epochs 0..60, the label value starts 0.05
+        further from 0/1; with dynamic_smooth a strong D (G) widens the real (fake) labels.
+        Same draw as the reference (torch.normal over [B, 4]), so a shared seed gives the same
+        labels; DP ranks draw the global batch from a shared generator and slice their shard."""
+        if epoch < 0:
+            progress, noise_std = 0.0, 0.01
+        elif epoch > 60:
+            progress, noise_std = 1.0, 0.002
+        else:
+            progress = epoch / 60
+            noise_std = 0.01 - progress * (0.01 - 0.002)
+        recent_d, recent_g = self.get_recent_avg_loss() if len(self.d_loss_history) >= 10 else (0.5, 0.5)
         if is_real:
             val, lo, hi = self.real_label_smooth - 0.05 * (1 - progress), 0.85, 1.0
+            if self.dynamic_smooth and recent_d < self.d_strong_threshold:
+                val, noise_std = max(0.97, val - 0.1), noise_std + 0.01
         else:
             val, lo, hi = self.fake_label_smooth + 0.05 * (1 - progress), 0.0, 0.15
-        noise = torch.randn(batch_size, 4, device=device, generator=generator) * noise_std
-        return (torch.full((batch_size, 4), val, device=device) + noise).clamp_(lo, hi)
+            if self.dynamic_smooth and recent_g < self.g_strong_threshold:
+                val, noise_std = min(0.03, val + 0.1), noise_std + 0.01
+        labels = torch.ones(batch_size, 4, device=device).fill_(val)
+        noise = torch.normal(0, noise_std, labels.shape, device=device, generator=generator)
+        return torch.clamp(labels + noise, lo, hi).requires_grad_(False)
 
 
 def pos_to_motion(pose):

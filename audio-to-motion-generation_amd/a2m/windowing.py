@@ -60,9 +60,29 @@ class PatsClip:
         for (mod, data), fn in zip(sequences.items(), fs_new):
             self.index[mod] = window_index(data.shape[0], mod, fn, time, window_hop)
         self.norm_stats = norm_stats or {}
+        self.fs_new = tuple(fs_new)
 
     def __len__(self):
         return min(len(ix[0]) for ix in self.index.values())
+
+    @staticmethod
+    def window_times(first_index, last_index, fs_new, idx):
+        """__getitem__'s meta start / end seconds (dataUtils.py:660,718-725): the start counts
+        the LAST modality's strided samples before its window (len(data[0:start:interval]),
+        the loop variable left over from the modality loop), the duration is the FIRST
+        modality's window length; both over fs_new[-1]."""
+        s_last, _, i_last = last_index
+        s_first, w_first, i_first = first_index
+        out = []
+        for k in np.asarray(idx, np.int64).reshape(-1):
+            start = len(range(0, int(s_last[k]), i_last)) / fs_new[-1]
+            dur = len(range(int(s_first[k]), int(s_first[k]) + w_first, i_first)) / fs_new[-1]
+            out.append((start, start + dur))
+        return np.array(out, dtype=np.float64).reshape(-1, 2)
+
+    def meta(self, idx):
+        mods = list(self.seq)
+        return self.window_times(self.index[mods[0]], self.index[mods[-1]], self.fs_new, idx)
 
     def batch(self, idx):
         idx = np.asarray(idx, np.int64)

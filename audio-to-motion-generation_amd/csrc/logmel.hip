@@ -50,8 +50,11 @@ static void plan_layout(int win, int nfft, int n_mels, int nnz, int n_w4, PlanHe
 }
 
 static bool geometry(int sr, double win_s, double hop_s, int* win, int* hop, int* nfft) {
-  *win = (int)std::lround(sr * win_s);
-  *hop = (int)std::lround(sr * hop_s);
+  // int(round(sr * secs)) (mel_features.py:212-213): Python rounds the double product half to
+  // even, which nearbyint does under the default FE_TONEAREST mode (lround would not: 44.1 kHz x
+  // 25 ms = 1102.5 -> 1102, 22.05 kHz x 10 ms = 220.5 -> 220)
+  *win = (int)std::nearbyint((double)sr * win_s);
+  *hop = (int)std::nearbyint((double)sr * hop_s);
   if (*win < 2 || *hop < 1) return false;
   *nfft = 1 << (int)std::ceil(std::log((double)*win) / std::log(2.0));
   return *nfft >= 4 && *nfft <= 16384;

@@ -90,7 +90,8 @@ __global__ __launch_bounds__(256) void pose_loss_partial_kernel(const float* gen
 }
 
 __global__ __launch_bounds__(256) void pose_loss_final_kernel(const float* part, int B, int T,
-                                                              int has_real, float* out) {
+                                                              int has_real, float hand_w,
+                                                              float body_w, float* out) {
   __shared__ float red[4];
   float bone = 0.f, hs = 0.f, bs = 0.f;
   for (int i = threadIdx.x; i < B * kBones; i += blockDim.x) {
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(256) void pose_loss_final_kernel(const float* part,
   const float Bs = block_sum(bs, red);
   if (threadIdx.x == 0) {
     out[0] = has_real ? Bn / (float)(B * kBones) : 0.f;
-    out[1] = 0.7f * (Hs / (float)(B * T * 30)) + 0.3f * (Bs / (float)(B * T * 5));
+    out[1] = hand_w * (Hs / (float)(B * T * 30)) + body_w * (Bs / (float)(B * T * 5));
   }
 }
 
@@ -116,9 +117,10 @@ __global__ __launch_bounds__(256) void pose_loss_final_kernel(const float* part,
 
 using namespace a2m;
 
-extern "C" int a2m_pose_losses_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
-                                   int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float* out,
-                                   void* ws, size_t ws_bytes, void* stream) {
+extern "C" int a2m_pose_losses_w_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
+                                     int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float hand_w,
+                                     float body_w, float* out, void* ws, size_t ws_bytes,
+                                     void* stream) {
   A2M_CHECK_ARG(gen && out && B > 0 && T > 0, "pose_losses: bad args");
   const size_t need = sizeof(float) * (size_t)B * kPart;
   if (!ws || ws_bytes < need) {
@@ -131,7 +133,14 @@ extern "C" int a2m_pose_losses_f32(const float* gen, int64_t gs_b, int64_t gs_t,
                      rs_b, rs_t, T, part);
   A2M_LAUNCH_CHECK();
   hipLaunchKernelGGL(pose_loss_final_kernel, dim3(1), dim3(256), 0, st, part, B, T,
-                     real != nullptr ? 1 : 0, out);
+                     real != nullptr ? 1 : 0, hand_w, body_w, out);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
+}
+
+extern "C" int a2m_pose_losses_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
+                                   int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float* out,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  return a2m_pose_losses_w_f32(gen, gs_b, gs_t, real, rs_b, rs_t, B, T, 0.7f, 0.3f, out, ws,
+                               ws_bytes, stream);
 }

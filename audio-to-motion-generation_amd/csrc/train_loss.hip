@@ -63,6 +63,7 @@ __device__ __forceinline__ void angle_grad(const float* p, int a, int j, int c, 
 __global__ __launch_bounds__(256) void pose_loss_bwd_kernel(const float* gen, int64_t gs_b,
                                                             int64_t gs_t, const float* real,
                                                             int64_t rs_b, int64_t rs_t, int B, int T,
+                                                            float hand_w, float body_w,
                                                             const float* grad_out, float* dgen) {
   __shared__ float lg[51], lr[51], coef[51];
   __shared__ float acc[kTC * 104];
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(256) void pose_loss_bwd_kernel(const float* gen, in
   for (int k = threadIdx.x; k < 51; k += blockDim.x)
     coef[k] = real ? gbone * 2.f * (lg[k] - lr[k]) / (float)(B * 51) / (float)T : 0.f;
   __syncthreads();
-  const float gh = gang * 0.7f / (float)(B * T * 30), gb = gang * 0.3f / (float)(B * T * 5);
+  const float gh = gang * hand_w / (float)(B * T * 30), gb = gang * body_w / (float)(B * T * 5);
   for (int t0 = 0; t0 < T; t0 += kTC) {
     const int nt = min(kTC, T - t0);
     for (int i = threadIdx.x; i < kTC * 104; i += blockDim.x) acc[i] = 0.f;
@@ -356,15 +357,23 @@ using namespace a2m;
 
 extern "C" {
 
-int a2m_pose_losses_bwd_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
-                            int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, const float* grad_out,
-                            float* dgen, void* ws, size_t ws_bytes, void* stream) {
+int a2m_pose_losses_w_bwd_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
+                              int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float hand_w,
+                              float body_w, const float* grad_out, float* dgen, void* ws,
+                              size_t ws_bytes, void* stream) {
   (void)ws; (void)ws_bytes;
   A2M_CHECK_ARG(gen && grad_out && dgen && B > 0 && T > 0, "pose_losses_bwd: bad args");
   hipLaunchKernelGGL(pose_loss_bwd_kernel, dim3(B), dim3(256), 0, as_stream(stream), gen, gs_b, gs_t,
-                     real, rs_b, rs_t, B, T, grad_out, dgen);
+                     real, rs_b, rs_t, B, T, hand_w, body_w, grad_out, dgen);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
+}
+
+int a2m_pose_losses_bwd_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
+                            int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, const float* grad_out,
+                            float* dgen, void* ws, size_t ws_bytes, void* stream) {
+  return a2m_pose_losses_w_bwd_f32(gen, gs_b, gs_t, real, rs_b, rs_t, B, T, 0.7f, 0.3f, grad_out,
+                                   dgen, ws, ws_bytes, stream);
 }
 
 int a2m_motion_losses_f32(const float* fake, const float* real, int32_t B, int32_t T, int32_t Fd,

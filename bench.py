@@ -41,6 +41,33 @@ def synth_wave(B, n, seed, device):
     return w.float().to(device)
 
 
+def infer_step(g, wave):
+    """One bench step: HIP log-mel over the resident waveforms + SelfAttention_G forward."""
+    from a2m.mel_features import log_mel_batch
+
+    def step():
+        mel = log_mel_batch(wave)
+        out, _ = g(mel)
+        return out
+    return step
+
+
+def capture_step(dev, step):
+    """Warm the step up on a side stream, then capture it in one HIP graph (the decoder
+    branches' fork/join streams are recorded with it).  Returns (graph, static output)."""
+    step()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_out = step()
+    return graph, static_out
+
+
 def g_forward_flops(B, T, C=256):
     """Useful FLOPs of one G forward: 2*MACs of every conv/linear/bmm,
     encoder counted over live columns only."""
@@ -175,13 +202,39 @@ def run_mel_kernel(dev, wave, iters=50):
     return ms, nbytes
 
 
-def cpu_baseline(B=8, T=64, max_s=20.0):
-    """torch-CPU fp32 oracle port (numpy float64 mel + functional G) on a bounded sample."""
+def host_cpu():
+    """CPU model and core counts of the host the baseline runs on."""
+    model = 'unknown'
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        import psutil
+        phys = psutil.cpu_count(logical=False)
+    except Exception:
+        phys = None
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return model, phys, avail
+
+
+def cpu_baseline(B=64, T=64, max_s=40.0):
+    """torch-CPU fp32 oracle port (numpy float64 mel + functional G) on the bench's own
+    workload shape (B clips x T frames), timed on this host's cores: one warm-up, then the
+    median of up to 5 runs within max_s."""
     sys.path.insert(0, REPO)
     import numpy as np
     from oracle import mel as omel, model as omodel, synth, weights
     from a2m.real_motion_model import SelfAttention_G
     threads = torch.get_num_threads()
+    model_name, phys, avail = host_cpu()
     shapes = {k: tuple(v.shape) for k, v in SelfAttention_G(p=0.0).state_dict().items()}
     sd = weights.make_state_dict(shapes, seed=7)
     wav = synth.speech_like(B, synth.samples_for_frames(T), seed=1)
@@ -198,8 +251,9 @@ def cpu_baseline(B=8, T=64, max_s=20.0):
         times.append(time.perf_counter() - t0)
     med = sorted(times)[len(times) // 2]
     return {'value': round(B * T / med, 1), 'unit': 'pose-frames/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{B} clips x {T} frames (numpy fp64 log-mel + torch-CPU fp32 G forward), '
-                      f'median of {len(times)} runs, {threads} threads'}
+            'cpu_model': model_name, 'host_physical_cores': phys, 'host_cpus_available': avail,
+            'sample': f'{B} clips x {T} frames, the bench workload (numpy fp64 log-mel + torch-CPU fp32 '
+                      f'G forward), median of {len(times)} runs, {threads} torch threads'}
 
 
 # dense FLOPs of one training iteration at T=64 measured with torch's
@@ -264,6 +318,8 @@ def run_train(args, world, rank, dev):
                           'gflop_per_iteration': round(flops * world / 1e9, 1),
                           'flop_source': 'SURVEY.md 8(d) FlopCounter count, dense'},
     }
+    if args.rehearsal:
+        result['rehearsal'] = args.rehearsal
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -289,6 +345,20 @@ def roofline_entry(gt, peak=None):
             'splitk_reduce_ms_per_step': round(gt.ms_reduce, 4)}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N ranks as fresh child processes of
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) before anything touches the
+    GPU, and exit with their status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -305,12 +375,19 @@ def main():
                     help='GEMM operand precision (bf16: configs[4], fp32 accumulation/storage)')
     args = ap.parse_args()
 
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != args.gpus:
+        sys.exit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU')
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     # A2M_BENCH_BACKEND=gloo rehearses the N>1 path (barriers, max-over-ranks timing, the DP
     # all-reduce) with several ranks sharing the GPUs of a smaller box; RCCL is the default
     backend = os.environ.get('A2M_BENCH_BACKEND', 'nccl')
+    args.rehearsal = None if backend == 'nccl' else (
+        f'{backend} rehearsal: {world} ranks share {torch.cuda.device_count()} GPU(s); '
+        f'not an N-GPU throughput')
     if backend != 'nccl':
         local = local % torch.cuda.device_count()
     if world > 1:
@@ -325,7 +402,6 @@ def main():
     if args.mode == 'train':
         return run_train(args, world, rank, dev)
 
-    from a2m.mel_features import log_mel_batch
     from a2m.real_motion_model import SelfAttention_G
 
     B, T = args.batch, args.frames
@@ -338,24 +414,9 @@ def main():
     g = g.to(dev).eval()
     wave = synth_wave(B, n, seed=rank, device=dev)
 
-    def step():
-        mel = log_mel_batch(wave)
-        out, _ = g(mel)
-        return out
-
+    step = infer_step(g, wave)
     with torch.no_grad():
-        step()
-        torch.cuda.synchronize()
-        graph = None
-        if not args.no_graph:
-            s = torch.cuda.Stream(dev)
-            s.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(s):
-                step()
-            torch.cuda.current_stream(dev).wait_stream(s)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                static_out = step()
+        graph, static_out = capture_step(dev, step) if not args.no_graph else (None, None)
         run = graph.replay if graph is not None else step
         for _ in range(args.warmup):
             run()
@@ -413,6 +474,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline()
+    if args.rehearsal:
+        result['rehearsal'] = args.rehearsal
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

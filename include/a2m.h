@@ -194,6 +194,12 @@ int a2m_graph_layer_fwd_f32(const float* x, int32_t F, int32_t J, int32_t kind,
 int a2m_pose_losses_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
                         int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float* out,
                         void* ws, size_t ws_bytes, void* stream);
+/* The same with the angle weights explicit: out[1] = hand_w * hand + body_w * body.
+ * (1, 0) is compute_hand_joint_angle_loss (real_motion_model.py:350-392), (0, 1)
+ * compute_body_joint_angle_loss (:394-447), (0.7, 0.3) the comprehensive loss (:449-461). */
+int a2m_pose_losses_w_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
+                          int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float hand_w,
+                          float body_w, float* out, void* ws, size_t ws_bytes, void* stream);
 
 /* ================================================================ training step
  * Forward-in-train-mode and backward entry points for the per-clip GAN step
@@ -305,6 +311,10 @@ int a2m_pose_losses_bwd_f32(const float* gen, int64_t gs_b, int64_t gs_t, const 
                             int64_t rs_b, int64_t rs_t, int32_t B, int32_t T,
                             const float* grad_out, float* dgen, void* ws, size_t ws_bytes,
                             void* stream);
+int a2m_pose_losses_w_bwd_f32(const float* gen, int64_t gs_b, int64_t gs_t, const float* real,
+                              int64_t rs_b, int64_t rs_t, int32_t B, int32_t T, float hand_w,
+                              float body_w, const float* grad_out, float* dgen, void* ws,
+                              size_t ws_bytes, void* stream);
 /* terms = [L1(diff(real), diff(fake)), mean||accel||, mean||jerk||] on [B][T][Fd] (contiguous).
  * If grad_terms (device [3], the incoming dL/dterms) and dfake are given, also
  * dfake = sum_i grad_terms[i] * dterms[i]/dfake (overwritten). */

@@ -9,7 +9,8 @@ reference in fp32 by tests/test_oracle_golden.py) in float64 at the SAME sampled
 as tests/golden/train_step_b2t64.npz, so the GPU test can measure both implementations
 against the exact gradient: the GPU must be as close to it as the reference itself is.
 
-    python oracle/make_f64_grads.py     # writes tests/golden/train_step_b2t64_f64.npz
+    python oracle/make_f64_grads.py [train_step_b2t64 | train_step_b16t64]
+        # writes tests/golden/<name>_f64.npz (default train_step_b2t64)
 """
 import json
 import os
@@ -46,19 +47,20 @@ def _sample(state, t, prefix):
     return np.stack(vals)
 
 
-def main():
+def main(name='train_step_b2t64'):
     torch.set_default_dtype(torch.float64)
     with open(os.path.join(GOLDEN, 'state_dict_keys.json')) as f:
         keys = json.load(f)
-    z = np.load(os.path.join(GOLDEN, 'g_eval_b2t64.npz'))
-    t = dict(np.load(os.path.join(GOLDEN, 'train_step_b2t64.npz')))
+    t = dict(np.load(os.path.join(GOLDEN, name + '.npz')))
+    z = t if 'audio' in t else np.load(os.path.join(GOLDEN, 'g_eval_b2t64.npz'))
     gs, ds = _state(keys['G'], 1234), _state(keys['D'], 1235)
     audio = torch.from_numpy(z['audio']).double()
     pose = torch.from_numpy(z['real_pose']).double()
+    B = audio.shape[0]
     fake, internal = model.generator(gs, audio, real_pose=pose, train=True)
     fd = model.discriminator(ds, torch.diff(fake, dim=1), train=True)
     l1, sm, jk = model.motion_terms(pose, fake)
-    loss = l1 + torch.nn.functional.mse_loss(fd, torch.full((2, 4), 0.93)) + 0.1 * sm + 0.05 * jk \
+    loss = l1 + torch.nn.functional.mse_loss(fd, torch.full((B, 4), 0.93)) + 0.1 * sm + 0.05 * jk \
         + internal[0] + internal[1]
     loss.backward()
     out = {'gG_val': _sample(gs, t, 'gG'), 'G_loss': loss.detach().numpy()}
@@ -68,15 +70,15 @@ def main():
         fp2, _ = model.generator(gs, audio, train=True)
     fd2 = model.discriminator(ds, torch.diff(fp2, dim=1), train=True)
     rd2 = model.discriminator(ds, torch.diff(pose, dim=1), train=True)
-    dl = torch.nn.functional.mse_loss(rd2, torch.full((2, 4), 0.93)) + \
-        torch.nn.functional.mse_loss(fd2, torch.full((2, 4), 0.07))
+    dl = torch.nn.functional.mse_loss(rd2, torch.full((B, 4), 0.93)) + \
+        torch.nn.functional.mse_loss(fd2, torch.full((B, 4), 0.07))
     dl.backward()
     out.update(gD_val=_sample(ds, t, 'gD'), D_loss=dl.detach().numpy())
     rel = abs(dl.item() - float(t['D_loss'])) / abs(float(t['D_loss']))
     assert rel < 1e-4, f'fp64 D loss disagrees with the reference fixture: {rel}'
-    np.savez_compressed(os.path.join(GOLDEN, 'train_step_b2t64_f64.npz'), **out)
-    print('wrote train_step_b2t64_f64.npz', {k: v.shape for k, v in out.items()})
+    np.savez_compressed(os.path.join(GOLDEN, name + '_f64.npz'), **out)
+    print('wrote', name + '_f64.npz', {k: v.shape for k, v in out.items()})
 
 
 if __name__ == '__main__':
-    main()
+    main(*sys.argv[1:])

@@ -16,9 +16,9 @@ def samples_for_frames(n_frames, win=WIN, hop=HOP):
     return (n_frames - 1) * hop + win
 
 
-def speech_like(n_clips, n_samples, seed=0, f0_range=(90.0, 250.0)):
+def speech_like(n_clips, n_samples, seed=0, f0_range=(90.0, 250.0), sr=SR):
     rng = np.random.default_rng(seed)
-    t = np.arange(n_samples, dtype=np.float64) / SR
+    t = np.arange(n_samples, dtype=np.float64) / sr
     out = np.empty((n_clips, n_samples), dtype=np.float32)
     for c in range(n_clips):
         f0 = rng.uniform(*f0_range)

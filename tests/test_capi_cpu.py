@@ -40,6 +40,37 @@ def test_logmel_geometry_and_frames():
     assert N.lib.a2m_logmel_num_frames(513141, 2048, 1067) == 480
 
 
+def test_logmel_geometry_rounds_like_python():
+    """window/hop = int(round(sr * secs)) with Python's half-to-even rounding of the double
+    product, fft_len = 2 ** ceil(log2(window)) (mel_features.py:212-214), over a sweep of rates
+    and durations that includes the .5 cases (44.1 kHz x 25 ms = 1102.5, 22.05 kHz x 10 ms =
+    220.5)."""
+    from a2m import _native as N
+    w, h, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    rates = [8000, 11025, 16000, 22050, 24000, 32000, 44100, 48000, 96000]
+    secs = [0.001, 0.0025, 0.005, 0.01, 0.015, 0.02, 0.025, 0.03, 0.032, 0.04, 0.05, 0.064,
+            0.1, 0.128, 1 / 15, 1 / 30, 0.0125, 0.0375]
+    seen_half = 0
+    for sr in rates:
+        for ws in secs:
+            for hs in secs:
+                rc = N.lib.a2m_logmel_geometry(sr, ws, hs, ctypes.byref(w), ctypes.byref(h), ctypes.byref(n))
+                ew, eh = int(round(sr * ws)), int(round(sr * hs))
+                if ew < 2 or eh < 1:
+                    continue
+                ef = 2 ** int(np.ceil(np.log(ew) / np.log(2.0)))
+                if ef > 16384:
+                    continue
+                assert rc == 0, (sr, ws, hs)
+                assert (w.value, h.value, n.value) == (ew, eh, ef), (sr, ws, hs)
+                seen_half += (sr * ws) % 1 == 0.5
+    assert seen_half > 0
+    N.lib.a2m_logmel_geometry(44100, 0.025, 0.010, ctypes.byref(w), ctypes.byref(h), ctypes.byref(n))
+    assert (w.value, h.value, n.value) == (1102, 441, 2048)
+    N.lib.a2m_logmel_geometry(22050, 0.025, 0.010, ctypes.byref(w), ctypes.byref(h), ctypes.byref(n))
+    assert (w.value, h.value, n.value) == (551, 220, 1024)
+
+
 def _plan_arrays(sr, win, hop, nm, lo, hi):
     from a2m import _native as N
     nb = N.lib.a2m_logmel_plan_bytes(sr, win, hop, nm, lo, hi)

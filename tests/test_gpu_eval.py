@@ -99,3 +99,26 @@ def test_window_gather_matches_slicing():
     ref_p = np.stack([(pose.numpy()[s:s + 64] - mean.numpy()) / sd for s in sp]).astype(np.float32)
     assert np.abs(b['pose/data'].cpu().numpy() - ref_p).max() <= 1e-6 * np.abs(ref_p).max()
     assert b['audio/log_mel_512'].shape == (n, 64, 128)
+
+
+def test_window_batches_match_reference_getitem():
+    """PatsClip.batch / meta against the reference's own MiniData.__getitem__ outputs
+    (tests/golden/windowing.npz, oracle/make_fixtures_r2.py): the gathered windows with the
+    cached pose standardisation, and the start / end seconds."""
+    from a2m.windowing import PatsClip
+    from oracle.drivers import window_case_data
+    z = golden('windowing.npz')
+    lp, la, tm, hop, f0, f1 = z['cases'][0]
+    pose, audio, mean, std = window_case_data(0, int(lp), int(la))
+    clip = PatsClip({'pose/data': torch.from_numpy(pose).cuda(), 'audio/log_mel_512': torch.from_numpy(audio).cuda()},
+                    (int(f0), int(f1)), float(tm), int(hop),
+                    norm_stats={'pose/data': (torch.from_numpy(mean).cuda(), torch.from_numpy(std).cuda())})
+    assert len(clip) == int(z['c0_len'])
+    picks = z['c0_picks']
+    b = clip.batch(picks)
+    for k in range(len(picks)):
+        ref_p = z[f'c0_item{k}_pose']
+        assert np.abs(b['pose/data'][k].cpu().numpy() - ref_p).max() <= 1e-6 * np.abs(ref_p).max()
+        assert np.array_equal(b['audio/log_mel_512'][k].cpu().numpy(), z[f'c0_item{k}_audio'])
+    assert np.allclose(clip.meta(picks), np.stack([z[f'c0_item{k}_meta'] for k in range(len(picks))]),
+                       rtol=0, atol=1e-12)

@@ -69,6 +69,21 @@ def test_logmel_reference_signature_and_edges():
         log_mel_spectrogram(z['mel_oneframe_wave'], **{**build, 'upper_edge_hertz': 9000.0})
 
 
+def test_logmel_half_even_rates_vs_reference():
+    """44.1 kHz and 22.05 kHz, where int(round(sr * secs)) lands on .5 (window 1102.5 -> 1102,
+    hop 220.5 -> 220, mel_features.py:212-213): frame count and values against the
+    reference's own outputs (tests/golden/mel_rates.npz)."""
+    from a2m.mel_features import log_mel_spectrogram
+    z = golden('mel_rates.npz')
+    for i, (sr, ws, hs, nm, lo, hi) in enumerate(z['cases']):
+        ref = z[f'out{i}']
+        out = log_mel_spectrogram(z[f'wave{i}'], audio_sample_rate=int(sr), log_offset=0.01,
+                                  window_length_secs=ws, hop_length_secs=hs, num_mel_bins=int(nm),
+                                  lower_edge_hertz=lo, upper_edge_hertz=hi)
+        assert out.shape == ref.shape, (i, out.shape, ref.shape)
+        assert rel_err(out, ref) < TOL, (i, rel_err(out, ref))
+
+
 # ------------------------------------------------------------------------------ per op
 @pytest.mark.parametrize('B,Ci,Co,T,k,s,p', [(3, 16, 24, 20, 3, 1, 1), (2, 32, 64, 17, 4, 2, 1),
                                              (4, 40, 8, 9, 1, 1, 0), (2, 256, 512, 64, 3, 1, 1),
@@ -222,6 +237,23 @@ def test_derived_weight_caches_follow_updates():
     with torch.no_grad():
         ra, rc = refs()
         assert rel_err(att(x).cpu(), ra) < TOL and rel_err(ct(xc).cpu(), rc) < TOL
+    # load_state_dict writes through p.copy_ under no_grad; its post-hook bumps the epoch too
+    sa = {k: v.clone() * (1.3 if k.endswith('weight') else 1.0) for k, v in att.state_dict().items()}
+    sc = {k: v.clone() * (0.7 if k.endswith('weight') else 1.0) for k, v in ct.state_dict().items()}
+    att.load_state_dict(sa)
+    ct.load_state_dict(sc)
+    with torch.no_grad():
+        ra, rc = refs()
+        assert rel_err(att(x).cpu(), ra) < TOL and rel_err(ct(xc).cpu(), rc) < TOL
+    # a write through p.data (e.g. an EMA) is invisible to torch's version counter: the writer
+    # calls bump_weights_epoch() (documented contract, functional.py)
+    from a2m import functional as F
+    att.value_conv.weight.data.mul_(0.5)
+    ct.conv_transpose.weight.data.mul_(-1.0)
+    F.bump_weights_epoch()
+    with torch.no_grad():
+        ra, rc = refs()
+        assert rel_err(att(x).cpu(), ra) < TOL and rel_err(ct(xc).cpu(), rc) < TOL
 
 
 def test_channel_attention_layernorm_mean_repeat():
@@ -280,6 +312,60 @@ def test_pose_losses_vs_reference():
     assert rel_err(out[0], z['bone']) < TOL and rel_err(out[1], z['angle']) < TOL
     out2 = F.pose_losses(torch.from_numpy(z['gen']).to(DEV)).cpu()
     assert rel_err(out2[1], z['angle']) < TOL and out2[0].item() == 0.0  # no real pose: bone 0
+
+
+def test_angle_loss_methods_vs_reference(g_state):
+    """SelfAttention_G.compute_{bone_length, hand_joint_angle, body_joint_angle,
+    comprehensive_angle}_loss (real_motion_model.py:307-461) against the reference's values,
+    on device and on host tensors, and differentiable in gen_pose."""
+    from a2m.real_motion_model import SelfAttention_G
+    z = golden('losses.npz')
+    g = SelfAttention_G(p=0.0).to(DEV)
+    gen, real = torch.from_numpy(z['gen']), torch.from_numpy(z['real'])
+    for dev in (DEV, 'cpu'):
+        gd, rd = gen.to(dev), real.to(dev)
+        vals = {'bone': g.compute_bone_length_loss(rd, gd), 'hand': g.compute_hand_joint_angle_loss(gd),
+                'body': g.compute_body_joint_angle_loss(gd), 'angle': g.compute_comprehensive_angle_loss(gd)}
+        for k, v in vals.items():
+            assert v.device.type == torch.device(dev).type, (k, dev)
+            assert rel_err(v.detach().cpu(), z[k]) < TOL, (k, dev)
+    from oracle import model as OM
+    for name, fn, ref_fn in (('hand', g.compute_hand_joint_angle_loss, OM.hand_angle_loss),
+                             ('body', g.compute_body_joint_angle_loss, OM.body_angle_loss)):
+        x = gen.clone().to(DEV).requires_grad_(True)
+        fn(x).backward()
+        x64 = gen.double().requires_grad_(True)
+        ref_fn(x64).backward()
+        assert rel_err(x.grad.cpu().double(), x64.grad) < 2e-5, name
+    assert g.compute_body_joint_angle_loss(gen[..., :100].to(DEV)).item() == 0.0   # :403-404
+
+
+def test_host_tensor_entry_generator_and_discriminator(g_state, d_state):
+    """generate_motion_video.py:235-257: a generator constructed on the host, loaded from a
+    checkpoint, called on host tensors, left in train mode under no_grad.  The module moves
+    itself to the GPU once; results come back on the host; eval-mode values match the
+    device path."""
+    from a2m.real_motion_model import SelfAttention_D, SelfAttention_G
+    z = golden('g_eval_b2t64.npz')
+    g = SelfAttention_G(p=0.0)
+    g.load_state_dict(g_state, strict=False)
+    audio = torch.from_numpy(z['audio'])
+    with torch.no_grad():
+        pose, losses = g(audio)          # train mode, as the script leaves it
+    assert pose.device.type == 'cpu' and all(l.device.type == 'cpu' for l in losses)
+    assert next(g.parameters()).is_cuda and pose.shape == (2, 64, 104) and torch.isfinite(pose).all()
+    g.load_state_dict(g_state, strict=False)   # the train-mode call moved the BN running stats
+    g.eval()
+    with torch.no_grad():
+        pose_e, losses_e = g(audio, real_pose=torch.from_numpy(z['real_pose']))
+    assert pose_e.device.type == 'cpu' and len(losses_e) == 2
+    assert rel_err(pose_e, z['pose']) < TOL
+    d = SelfAttention_D(out_channels=64, p=0.0)
+    d.load_state_dict(d_state, strict=False)
+    d.eval()
+    with torch.no_grad():
+        dr, aux = d(torch.diff(torch.from_numpy(z['real_pose']), dim=1))
+    assert dr.device.type == 'cpu' and aux == [] and rel_err(dr, z['d_real']) < TOL
 
 
 # ------------------------------------------------------------------------------ full model
@@ -350,3 +436,30 @@ def test_full_size_batch_invariance(g_state):
     assert torch.isfinite(out).all() and torch.isfinite(losses[0])
     assert rel_err(out[17:18].cpu(), solo.cpu()) < TOL
     assert rel_err(out[63:64].cpu(), solo2.cpu()) < TOL
+
+
+def test_headline_b64_bench_step_vs_reference(g_state):
+    """configs[1] at its real size: the exact bench step (bench.infer_step: HIP log-mel over
+    64 resident 69,269-sample waveforms + SelfAttention_G eval, captured in one HIP graph by
+    bench.capture_step and replayed) against the reference's own mel and pose for the same
+    waveforms (tests/golden/g_eval_b64t64.npz, oracle/make_fixtures_r2.py)."""
+    import bench
+    from a2m.mel_features import log_mel_batch
+    from a2m.real_motion_model import SelfAttention_G
+    from oracle import synth
+    z = golden('g_eval_b64t64.npz')
+    wav = synth.speech_like(64, synth.samples_for_frames(64), seed=int(z['seed']))
+    wave = torch.from_numpy(wav).to(DEV)
+    g = SelfAttention_G(p=0.0)
+    g.load_state_dict(g_state, strict=False)
+    g = g.to(DEV).eval()
+    with torch.no_grad():
+        graph, out = bench.capture_step(torch.device(DEV), bench.infer_step(g, wave))
+        out.zero_()
+        graph.replay()
+        graph.replay()
+        torch.cuda.synchronize()
+        mel = log_mel_batch(wave)
+    assert out.shape == (64, 64, 104)
+    assert rel_err(mel.cpu().numpy(), z['mel']) < TOL
+    assert rel_err(out.cpu().numpy(), z['pose']) < TOL, rel_err(out.cpu().numpy(), z['pose'])

@@ -12,7 +12,6 @@ from conftest import golden, rel_err
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 TOL = 1e-4
-TOL_D = 4e-4  # train-mode D on G's output at B=2 (see test_train_step_vs_reference)
 GTOL = 2e-4   # gradients: deeper fp32 chains, relative to max |ref|
 
 
@@ -205,7 +204,7 @@ def test_losses_and_plumbing_train():
     z = golden('losses.npz')
     gd, gc = _leaf(torch.from_numpy(z['gen']))
     real = torch.from_numpy(z['real'])
-    ld = AG._PoseLosses.apply(gd, real.to(DEV))
+    ld = AG._PoseLosses.apply(gd, real.to(DEV), (0.7, 0.3))
     lc = torch.stack([OM.bone_length_loss(real, gc), OM.angle_loss(gc)])
     assert rel_err(ld.detach().cpu(), lc.detach()) < TOL
     w = torch.tensor([0.7, 1.3])
@@ -299,61 +298,71 @@ def _bn_cancelled(name):
         re.fullmatch(r'conv[123](\.\d)?\.(0|4|9)\.bias', name) is not None
 
 
-def _grad_check_vs_golden(module, t, prefix):
-    """Sampled gradients against the EXACT gradient (fp64 oracle, train_step_b2t64_f64.npz,
-    made by oracle/make_f64_grads.py).  Tolerance per parameter: 2e-3 of the gradient's scale,
-    or twice the reference's own fp32 error against the exact value where that is larger —
-    the encoder's gradients sit ~60 layers / 20 batch-norms below the loss, where the
-    reference itself is 0.2-0.5 % off; an fp32 GPU summing in another order cannot track
-    the reference's rounding, only the true gradient.
-
-    Why the bound is a multiple of the reference's own error: at B=2 the step is badly
-    conditioned in fp32 (batch-statistics BN over as few as 16 values in the discriminator,
-    LayerNorm after GAT): a 1.4e-5 relative forward difference in the fake pose — the GPU
-    forward is as close to fp64 as the reference's (tools/grad_diag.py) — moves dL/dfake by
-    0.2-0.4 %, and that is what reaches the encoder.  Each backward op on identical inputs
-    agrees to <=2e-4 (the per-op tests above), the encoder chain to 1e-6
-    (test_encoder_chain_vs_fp64) and every loss term's dL/dfake to 1e-5 at the reference's own
-    fake pose (test_loss_gradients_vs_fp64).  What is left for this test is the compounding,
-    and it is chaotic in the summation order: re-running the step under forced GEMM plans
-    (tools/order_spread.py only re-associates the engine's K sums; profiles/r01_order_spread.log)
-    moves the generator's median error between 1.6x and 6.6x the reference's own and the worst
-    parameter (a scalar attention gamma: one sum over every element) between 9 % and 52 %;
-    torch-CPU fp32 itself is 0.2-0.4 % (median) from fp64 even under a FIXED upstream gradient,
-    at B = 2, 8 and 32 alike.  The bounds are set by that spread -- median within 8x the
-    reference's own, no parameter beyond 60 % or 10x the reference's own error -- and the
-    tight claims live in the isolation tests.  A wrong kernel shows up as O(1) errors."""
-    f64 = golden('train_step_b2t64_f64.npz')
-    bad, errs, ref_errs = [], [], []
+def _grad_errors(module, t, f64, prefix):
+    """Per sampled parameter: (name, GPU error vs the exact gradient, reference fp32 error vs the
+    exact gradient), both relative to the gradient's scale.  The exact gradient is the fp64
+    oracle at the fixture's sampled indices (oracle/make_f64_grads.py)."""
+    out = []
+    params = dict(module.named_parameters())
     for i, n in enumerate(t[f'{prefix}_names']):
         if _bn_cancelled(n):
             continue
-        p = dict(module.named_parameters())[n]
-        g = p.grad.detach().double().reshape(-1).cpu().numpy()
+        g = params[n].grad.detach().double().reshape(-1).cpu().numpy()
         ix = t[f'{prefix}_idx'][i]
         ok = ix >= 0
         ref = t[f'{prefix}_val'][i][ok]
         exact = f64[f'{prefix}_val'][i][ok]
         scale = max(np.sqrt(t[f'{prefix}_sumsq'][i] / max(g.size, 1)), np.abs(exact).max(), 1e-12)
-        err = np.abs(g[ix[ok]] - exact).max() / scale
-        ref_err = np.abs(ref - exact).max() / scale
-        errs.append(err)
-        ref_errs.append(ref_err)
-        if err > max(0.6, 10.0 * ref_err):
-            bad.append((n, err, ref_err))
-    print(f'{prefix}: median err vs exact {np.median(errs):.2e} (reference fp32 {np.median(ref_errs):.2e}), '
-          f'max {np.max(errs):.2e} (reference {np.max(ref_errs):.2e})')
+        out.append((str(n), np.abs(g[ix[ok]] - exact).max() / scale, np.abs(ref - exact).max() / scale))
+    return out
+
+
+def _check_grad_errors(errs, prefix, med_ratio, max_floor, max_ratio):
+    """Median GPU error <= med_ratio x the reference's median error; every parameter within
+    max(max_floor, max_ratio x the reference's own error on that parameter)."""
+    e = np.array([x[1] for x in errs])
+    r = np.array([x[2] for x in errs])
+    bad = [x for x in errs if x[1] > max(max_floor, max_ratio * x[2])]
+    print(f'{prefix}: median err vs exact {np.median(e):.2e} (reference fp32 {np.median(r):.2e}, '
+          f'ratio {np.median(e) / max(np.median(r), 1e-30):.2f}), max {e.max():.2e} '
+          f'(reference {r.max():.2e}); worst {sorted(errs, key=lambda x: -x[1])[:3]}')
     assert not bad, bad[:10]
-    assert np.median(errs) < 8.0 * np.median(ref_errs) + 1e-3
+    assert np.median(e) <= med_ratio * np.median(r), (np.median(e), np.median(r))
 
 
-def test_train_step_vs_reference(g_state, d_state):
+# Train-step fixtures (oracle/make_fixtures.py, oracle/make_fixtures_r2.py) and the bounds each
+# is held to.  Forward values are held to north_star's 1e-4 at B=16; gradients against the
+# exact (fp64) gradient, as multiples of the reference's own fp32 error -- see
+# test_train_step_vs_reference.
+STEP_CASES = {
+    # B=16: the gradient bounds DESIGN.md 2.3 states
+    'b16': dict(fixture='train_step_b16t64', tol_out=1e-4, med=2.0, floor=0.05, ratio=8.0),
+    # B=2: batch-statistics BN over 8-16 values in D; outputs at 4e-4 and the loose gradient
+    # bounds of the round-1 test (kept as a second, smaller case)
+    'b2': dict(fixture='train_step_b2t64', tol_out=4e-4, med=8.0, floor=0.6, ratio=10.0),
+}
+
+
+@pytest.mark.parametrize('case', ['b16', 'b2'])
+def test_train_step_vs_reference(case, g_state, d_state):
     """One G-step (G + D forward in train mode, all G losses, backward) and one D-step, p=0,
-    fixed labels, against the reference's outputs and sampled gradients."""
+    fixed labels (version5_model_train.py:350-405), against the reference's outputs and sampled
+    gradients.
+
+    Gradients are measured against the EXACT gradient (the fp64 oracle at the same indices)
+    and bounded by multiples of the reference's own fp32 error there: the G-step is
+    ill-conditioned in fp32 (the reference's own gradients sit a median 0.3-0.5 % from the
+    exact ones, up to 3-7 % on single parameters; tests/golden/*_f64.npz), so an fp32
+    implementation with another summation order cannot track the reference's rounding, only
+    the true gradient.  Each backward op on identical inputs agrees to <= 2e-4 (the per-op tests
+    above), the encoder chain to 2e-5 (test_encoder_chain_vs_fp64) and every loss term's
+    dL/dfake to 2e-5 (test_loss_gradients_vs_fp64)."""
     from a2m import autograd as AG
     from a2m.real_motion_model import SelfAttention_D, SelfAttention_G
-    z = golden('g_eval_b2t64.npz')
-    t = golden('train_step_b2t64.npz')
+    c = STEP_CASES[case]
+    t = golden(c['fixture'] + '.npz')
+    f64 = golden(c['fixture'] + '_f64.npz')
+    z = t if 'audio' in t.files else golden('g_eval_b2t64.npz')
     g = SelfAttention_G(p=0.0)
     g.load_state_dict(g_state, strict=False)
     d = SelfAttention_D(out_channels=64, p=0.0)
@@ -361,31 +370,37 @@ def test_train_step_vs_reference(g_state, d_state):
     g, d = g.to(DEV).train(), d.to(DEV).train()
     audio = torch.from_numpy(z['audio']).to(DEV)
     pose = torch.from_numpy(z['real_pose']).to(DEV)
+    B = audio.shape[0]
+    tol = c['tol_out']
     fake_pose, internal = g(audio, real_pose=pose)
     assert rel_err(fake_pose.detach().cpu(), t['fake_pose']) < TOL
     fake_d, _ = d(AG.pos_to_motion(fake_pose))
-    # the train-mode discriminator on the generator's output: BN over 16 values per channel;
-    # measured 5e-5..1.5e-4 from the reference across GEMM summation orders (order_spread)
-    assert rel_err(fake_d.detach().cpu(), t['fake_d']) < TOL_D
+    print(f'{case}: fake_d {rel_err(fake_d.detach().cpu(), t["fake_d"]):.2e}')
+    assert rel_err(fake_d.detach().cpu(), t['fake_d']) < tol
     terms = AG.motion_terms(fake_pose, pose)
-    loss = terms[0] + AG.mse_loss(fake_d, torch.full((2, 4), 0.93, device=DEV)) + 0.1 * terms[1] + \
-        0.05 * terms[2] + internal[0] + internal[1]
-    parts = torch.stack([terms[0], AG.mse_loss(fake_d, torch.full((2, 4), 0.93, device=DEV)), terms[1], terms[2],
-                         internal[0], internal[1]]).detach().cpu().numpy()
-    assert np.abs(parts - t['parts']).max() / np.abs(t['parts']).max() < TOL_D
-    assert rel_err(loss.detach().cpu(), t['G_loss']) < TOL_D
+    valid = torch.full((B, 4), 0.93, device=DEV)
+    adv = AG.mse_loss(fake_d, valid)
+    loss = terms[0] + adv + 0.1 * terms[1] + 0.05 * terms[2] + internal[0] + internal[1]
+    parts = torch.stack([terms[0], adv, terms[1], terms[2], internal[0], internal[1]]).detach().cpu().numpy()
+    print(f'{case}: parts {np.abs(parts - t["parts"]) / np.abs(t["parts"])}')
+    assert np.all(np.abs(parts - t['parts']) <= tol * np.abs(t['parts']))
+    assert rel_err(loss.detach().cpu(), t['G_loss']) < tol
     loss.backward()
-    _grad_check_vs_golden(g, t, 'gG')
+    eg = _grad_errors(g, t, f64, 'gG')
     d.zero_grad()
     with torch.no_grad():
         fp2, _ = g(audio)
     fd2, _ = d(AG.pos_to_motion(fp2))
     rd2, _ = d(AG.pos_to_motion(pose))
-    dl = AG.mse_loss(rd2, torch.full((2, 4), 0.93, device=DEV)) + AG.mse_loss(fd2, torch.full((2, 4), 0.07, device=DEV))
-    assert rel_err(fd2.detach().cpu(), t['d_fake']) < TOL_D and rel_err(rd2.detach().cpu(), t['d_real']) < TOL
-    assert rel_err(dl.detach().cpu(), t['D_loss']) < TOL_D
+    dl = AG.mse_loss(rd2, valid) + AG.mse_loss(fd2, torch.full((B, 4), 0.07, device=DEV))
+    print(f'{case}: d_fake {rel_err(fd2.detach().cpu(), t["d_fake"]):.2e} d_real '
+          f'{rel_err(rd2.detach().cpu(), t["d_real"]):.2e} D_loss {rel_err(dl.detach().cpu(), t["D_loss"]):.2e}')
+    assert rel_err(fd2.detach().cpu(), t['d_fake']) < tol and rel_err(rd2.detach().cpu(), t['d_real']) < TOL
+    assert rel_err(dl.detach().cpu(), t['D_loss']) < tol
     dl.backward()
-    _grad_check_vs_golden(d, t, 'gD')
+    ed = _grad_errors(d, t, f64, 'gD')
+    _check_grad_errors(eg, f'{case} gG', c['med'], c['floor'], c['ratio'])
+    _check_grad_errors(ed, f'{case} gD', c['med'], c['floor'], c['ratio'])
 
 
 def test_encoder_chain_vs_fp64(g_state):
@@ -440,8 +455,8 @@ def test_loss_gradients_vs_fp64(d_state):
     gpu = {'l1': lambda x: AG.motion_terms(x, pose.to(DEV))[0],
            'smooth': lambda x: AG.motion_terms(x, pose.to(DEV))[1],
            'jerk': lambda x: AG.motion_terms(x, pose.to(DEV))[2],
-           'bone': lambda x: AG._PoseLosses.apply(x, pose.to(DEV))[0],
-           'angle': lambda x: AG._PoseLosses.apply(x, pose.to(DEV))[1],
+           'bone': lambda x: AG._PoseLosses.apply(x, pose.to(DEV), (0.7, 0.3))[0],
+           'angle': lambda x: AG._PoseLosses.apply(x, pose.to(DEV), (0.7, 0.3))[1],
            'adv': lambda x: AG.mse_loss(d(AG.pos_to_motion(x))[0], torch.full((2, 4), lbl, device=DEV))}
     for name in cpu:
         x64 = X.double().requires_grad_(True)
@@ -470,3 +485,85 @@ def test_trainer_iteration_runs_and_learns():
     assert torch.isfinite(dl) and torch.isfinite(gl)
     assert not torch.equal(w0, g.unet.final_conv.weight.detach())
     assert len(tr.dyn.d_loss_history) == 1
+
+
+# version5_model_train.py:208-248 as written: the drop-in modules must train under the
+# reference's own loop body, torch.optim.Adam and torch.nn losses (not a2m's fused ones)
+def _pos_to_motion(pose_batch):
+    return torch.diff(pose_batch, n=1, dim=1)
+
+
+def _temporal_smoothness(motion_seq):
+    acceleration = motion_seq[:, 1:] - motion_seq[:, :-1]
+    return torch.mean(torch.norm(acceleration, dim=-1))
+
+
+def _jerk(motion_seq):
+    acceleration = motion_seq[:, 1:] - motion_seq[:, :-1]
+    jerk = acceleration[:, 1:] - acceleration[:, :-1]
+    return torch.mean(torch.norm(jerk, dim=-1))
+
+
+def test_reference_loop_body_with_torch_adam(g_state, d_state):
+    """One iteration of version5_model_train.py:350-405 unchanged (3 G-steps, 1 D-step,
+    torch.optim.Adam(lr=1e-3) over all parameters, L1/MSE from torch.nn, p=0, fixed labels) on
+    the a2m G / D, against the reference's own run (tests/golden/loop_b16t64.npz).
+
+    The first G_loss is the step's forward (held at 1e-4).  Later losses follow Adam updates:
+    Adam's first step moves every weight by ~lr*sign(grad), so weights whose exact gradient is
+    below the fp32 noise of the ill-conditioned G-step (test_train_step_vs_reference) move
+    either way in any fp32 implementation, and the loop is chaotic from there.  Measured with
+    rounding alone (tools/loop_spread.py, profiles/r02_loop_spread.txt; two runs, since CPU
+    fp32 is itself thread-order dependent): the fp32 vs the fp64 oracle on CPU, same weights
+    and inputs, have G-step 2 / 3 losses 0.1-0.5 % apart and the D loss 0.6-1.7 %; the
+    reference's own fp32 run and the fp32 oracle's differ by up to 2.0 % at G-step 3, and the
+    pose after the iteration differs by 79-150 % between any two of them.  Steps 2-3 and the D
+    loss are held at 5e-2; the pose after the iteration only to its magnitude."""
+    from a2m.real_motion_model import SelfAttention_D, SelfAttention_G
+    t = golden('train_step_b16t64.npz')
+    ref = golden('loop_b16t64.npz')
+    generator = SelfAttention_G(p=0.0)
+    generator.load_state_dict(g_state, strict=False)
+    discriminator = SelfAttention_D(out_channels=64, p=0.0)
+    discriminator.load_state_dict(d_state, strict=False)
+    generator, discriminator = generator.to(DEV).train(), discriminator.to(DEV).train()
+    audio = torch.from_numpy(t['audio']).to(DEV)
+    real_pose = torch.from_numpy(t['real_pose']).to(DEV)
+    optimizer_G = torch.optim.Adam(generator.parameters(), lr=10e-4)
+    optimizer_D = torch.optim.Adam(discriminator.parameters(), lr=10e-4)
+    motion_reg_loss, g_loss = torch.nn.L1Loss(), torch.nn.MSELoss()
+    d_loss1, d_loss2 = torch.nn.MSELoss(), torch.nn.MSELoss()
+    valid = torch.full((audio.shape[0], 4), 0.93, device=DEV)
+    fake = torch.full((audio.shape[0], 4), 0.07, device=DEV)
+    real_motion = _pos_to_motion(real_pose)
+    g_losses = []
+    for gen_step in range(3):
+        optimizer_G.zero_grad()
+        fake_pose, internal_losses = generator(audio, real_pose=real_pose)
+        fake_motion = _pos_to_motion(fake_pose)
+        fake_d, _ = discriminator(fake_motion)
+        G_loss = motion_reg_loss(real_motion, fake_motion) + 1.0 * g_loss(fake_d, valid)
+        G_loss += 0.1 * _temporal_smoothness(fake_motion) + 0.05 * _jerk(fake_motion)
+        for loss in internal_losses:
+            G_loss += loss
+        G_loss.backward()
+        optimizer_G.step()
+        g_losses.append(G_loss.item())
+    optimizer_D.zero_grad()
+    with torch.no_grad():
+        fake_pose_detached, _ = generator(audio)
+        fake_motion_detached = _pos_to_motion(fake_pose_detached)
+    fake_d, _ = discriminator(fake_motion_detached.detach())
+    real_d, _ = discriminator(real_motion)
+    D_loss = d_loss1(real_d, valid) + 1.0 * d_loss2(fake_d, fake)
+    D_loss.backward()
+    optimizer_D.step()
+    with torch.no_grad():
+        fp_after, _ = generator(audio)
+    rg = np.abs(np.array(g_losses) - ref['g_losses']) / np.abs(ref['g_losses'])
+    rd = abs(D_loss.item() - ref['d_losses'][0]) / abs(ref['d_losses'][0])
+    print(f'loop: G_loss rel err {rg}, D_loss {rd:.2e}, pose after {rel_err(fp_after.cpu(), ref["fake_pose_after"]):.2e}')
+    assert rg[0] < TOL
+    assert np.all(rg[1:] < 5e-2) and rd < 5e-2
+    a, b = np.abs(fp_after.cpu().numpy()).max(), np.abs(ref['fake_pose_after']).max()
+    assert np.isfinite(fp_after.cpu().numpy()).all() and 0.5 < a / b < 2.0

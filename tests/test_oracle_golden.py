@@ -37,6 +37,16 @@ def test_mel_other_configs_and_edges():
         assert str(e.value) == msg
 
 
+def test_mel_half_even_rates_oracle():
+    z = golden('mel_rates.npz')
+    for i, (sr, ws, hs, nm, lo, hi) in enumerate(z['cases']):
+        from oracle import mel as omel
+        out = omel.log_mel(z[f"wave{i}"], sample_rate=int(sr), log_offset=0.01, window_secs=ws, hop_secs=hs,
+                           num_mel_bins=int(nm), lower_hz=lo, upper_hz=hi)
+        assert out.shape == z[f'out{i}'].shape
+        assert np.abs(out - z[f'out{i}']).max() < 1e-9 * np.abs(z[f'out{i}']).max()
+
+
 def test_losses_oracle():
     from oracle import model
     z = golden('losses.npz')

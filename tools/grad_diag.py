@@ -186,7 +186,7 @@ def loss_isolated(d_gpu=None):
 
     def gpu_terms(x):
         m = AG.motion_terms(x, pose.cuda())
-        pl = AG._PoseLosses.apply(x, pose.cuda())
+        pl = AG._PoseLosses.apply(x, pose.cuda(), (0.7, 0.3))
         fd, _ = d(AG.pos_to_motion(x))
         return {'l1': m[0], 'smooth': m[1], 'jerk': m[2], 'bone': pl[0], 'angle': pl[1],
                 'adv': AG.mse_loss(fd, torch.full((2, 4), lbl, device='cuda'))}
