@@ -6,13 +6,19 @@ over clips with one process per GPU.
   pos_to_motion        :208-213        compute_temporal_smoothness_loss :216-230
   compute_jerk_loss    :233-248        one iteration (G steps, then D steps) :342-414
 
-Data parallelism (SURVEY.md 8(e)): every rank runs the step on its shard of the batch;
-gradients of the network being stepped are averaged with ONE all-reduce over the
-optimiser's flat gradient buffer (RCCL over xGMI on MI355X, gloo in CPU tests).  The two
-scalar losses are averaged before they enter the schedule so every rank takes identical
-branches.  BatchNorm uses per-rank batch statistics (PyTorch DDP default, no SyncBN).
-The discriminator's parameters are frozen during the G steps: the reference computes their
-gradients there and throws them away (optimizer_D.zero_grad() at :388).
+Data parallelism: every rank runs the step on its shard of the batch.
+Gradients of the network being stepped are averaged by GradReducer: the optimiser's flat
+gradient buffer is cut into ~25 MB buckets in reverse parameter order (the order backward
+produces them), and each bucket's all-reduce (RCCL over xGMI on MI355X, gloo in CPU tests)
+is launched from a post-accumulate-grad hook as soon as its last gradient lands, so it runs
+on the communication stream while the rest of the backward computes.  Buckets launch strictly
+in order, so every rank issues the same collective sequence.  Optionally the buckets travel
+in bf16 (configs[4]).  The two scalar losses are averaged before they enter the schedule so
+every rank takes identical branches; smoothed labels are drawn for the global batch from a
+generator seeded identically on every rank and sliced per rank.  BatchNorm uses per-rank
+batch statistics by default (PyTorch DDP default) or SyncBN.  The discriminator's parameters
+are frozen during the G steps: the reference computes their gradients there and throws them
+away (optimizer_D.zero_grad() at :388).
 """
 import numpy as np
 import torch
@@ -122,11 +128,129 @@ def compute_temporal_smoothness_loss_and_jerk(fake_pose, real_pose):
     return AG.motion_terms(fake_pose, real_pose)
 
 
+class GradReducer:
+    """Bucketed, backward-overlapped gradient averaging over a FlatAdam's flat gradient.
+
+    Buckets are contiguous slices of `opt.flat_grad` holding whole parameters, filled from the
+    last parameter backwards (~bucket_mb each).  A post-accumulate-grad hook on every parameter
+    counts arrivals; when a bucket's last expected gradient has landed, the bucket's gradients
+    are gathered into its slice (one segment-gather launch) and an async all-reduce of the slice
+    is started -- but only in bucket order, so all ranks issue identical collective sequences.
+    The set of parameters that receive gradients is learnt on the first backward (which reduces
+    everything at finish()); afterwards a parameter arriving in an already launched bucket is an
+    error, never a silent miss.  finish() gathers and reduces what is left, waits, and divides
+    by the world size.  reduce_dtype=torch.bfloat16 halves the bytes on the wire (configs[4]).
+    """
+
+    def __init__(self, opt, world, group=None, bucket_mb=25.0, reduce_dtype=None):
+        self.opt, self.world, self.group = opt, world, group
+        self.reduce_dtype = reduce_dtype
+        spans = list(opt._spans())
+        cap = max(int(bucket_mb * (1 << 20) / 4), 1)
+        # buckets tile [0, numel) of the flat gradient (alignment padding included: it stays
+        # zero), closed from the end of the buffer towards its start
+        self.buckets = []          # (lo, hi, member parameter indices), in launch order
+        hi, cur = opt.flat_grad.numel(), []
+        for i in reversed(range(len(spans))):
+            cur.append(i)
+            if hi - spans[i][0] >= cap or i == 0:
+                lo = 0 if i == 0 else spans[i][0]
+                self.buckets.append((lo, hi, cur))
+                hi, cur = lo, []
+        self.bucket_of = {}
+        for b, (_, _, members) in enumerate(self.buckets):
+            for i in members:
+                self.bucket_of[i] = b
+        self.expected = None       # learnt: parameter indices that receive gradients
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i))
+                       for i, p in enumerate(opt.params)]
+        self._reset()
+
+    def _reset(self):
+        self.arrived = set()
+        self.pending = [None] * len(self.buckets)
+        if self.expected is not None:
+            self.pending = [sum(1 for i in m if i in self.expected) for _, _, m in self.buckets]
+        self.next = 0
+        self.handles = []
+        self.active = False
+        self.in_backward = 0       # buckets launched from hooks, i.e. overlapped with backward
+
+    def begin(self):
+        """Arm the hooks for one backward (call after zero_grad, before backward)."""
+        self._reset()
+        self.active = self.world > 1
+
+    def _make_hook(self, i):
+        def hook(p):
+            if not self.active:
+                return
+            self.arrived.add(i)
+            if self.expected is None:
+                return
+            b = self.bucket_of[i]
+            if i not in self.expected or b < self.next:
+                raise RuntimeError(f'GradReducer: gradient of parameter {i} arrived after its bucket '
+                                   f'was reduced (the set of parameters with gradients changed)')
+            self.pending[b] -= 1
+            while self.next < len(self.buckets) and self.pending[self.next] == 0:
+                self._launch(self.next)
+                self.next += 1
+                self.in_backward += 1
+        return hook
+
+    def _gather(self, b):
+        o_spans = list(self.opt._spans())
+        segs, seat = [], []
+        for i in self.buckets[b][2]:
+            p = self.opt.params[i]
+            o, k = o_spans[i]
+            view = self.opt.flat_grad[o:o + k]
+            if p.grad is None:
+                seat.append((p, view))
+            elif p.grad.data_ptr() != view.data_ptr():
+                segs.append((o, p.grad.contiguous()))
+                seat.append((p, view))
+        F.gather_segments_(self.opt.flat_grad, segs)
+        for p, view in seat:
+            p.grad = view.view_as(p)
+
+    def _launch(self, b):
+        self._gather(b)
+        lo, hi, _ = self.buckets[b]
+        sl = self.opt.flat_grad[lo:hi]
+        buf = sl if self.reduce_dtype is None else sl.to(self.reduce_dtype)
+        work = dist.all_reduce(buf, group=self.group, async_op=True)
+        self.handles.append((sl, buf, work))
+
+    @torch.no_grad()
+    def finish(self):
+        """Reduce the buckets not yet launched, wait for all, average.  Returns flat_grad."""
+        if not self.active:
+            self.opt.collect_grads()
+            return self.opt.flat_grad
+        while self.next < len(self.buckets):
+            self._launch(self.next)
+            self.next += 1
+        if self.expected is None:
+            self.expected = set(self.arrived)
+        elif not self.arrived <= self.expected:
+            raise RuntimeError('GradReducer: parameters outside the learnt set received gradients')
+        for sl, buf, work in self.handles:
+            work.wait()
+            if buf is not sl:
+                sl.copy_(buf)
+        self.opt.flat_grad.div_(self.world)
+        self.active = False
+        return self.opt.flat_grad
+
+
 class GANTrainer:
     """One version5_model_train.py iteration per call, optionally data-parallel."""
 
     def __init__(self, generator, discriminator, lr=10e-4, lambda_gan=1.0, lambda_d=1.0,
-                 dynamic=None, fixed_labels=None, process_group=None, sync_bn=False):
+                 dynamic=None, fixed_labels=None, process_group=None, sync_bn=False,
+                 bucket_mb=25.0, grad_reduce_dtype=None, label_seed=0):
         self.G, self.D = generator, discriminator
         self.opt_G = FlatAdam(generator.parameters(), lr=lr)
         self.opt_D = FlatAdam(discriminator.parameters(), lr=lr)
@@ -134,10 +258,16 @@ class GANTrainer:
         self.lambda_gan, self.lambda_d = lambda_gan, lambda_d
         self.fixed_labels = fixed_labels          # (valid, fake) values for deterministic runs
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        dp = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(process_group) if dp else 1
+        self.rank = dist.get_rank(process_group) if dp else 0
         # SyncBN: BatchNorm statistics all-reduced over the DP group, so the
         # ranks normalise over the whole batch like the single-device reference step
         self.sync_bn = bool(sync_bn) and self.world > 1
+        self.red_G = GradReducer(self.opt_G, self.world, process_group, bucket_mb, grad_reduce_dtype)
+        self.red_D = GradReducer(self.opt_D, self.world, process_group, bucket_mb, grad_reduce_dtype)
+        self.label_seed = label_seed
+        self._label_gen = None
         self.last_d_loss = None
 
     def _allreduce_(self, t):
@@ -146,14 +276,22 @@ class GANTrainer:
             t.div_(self.world)
 
     def _labels(self, epoch, B, dev):
+        """Labels for this rank's shard: the global batch (B x world) is drawn from a generator
+        seeded identically on every rank and sliced, so a DP run sees the labels of the
+        single-device run of the whole batch."""
         if self.fixed_labels is not None:
             v, f = self.fixed_labels
             return torch.full((B, 4), v, device=dev), torch.full((B, 4), f, device=dev)
-        return (self.dyn.get_smooth_labels(epoch, B, dev, True),
-                self.dyn.get_smooth_labels(epoch, B, dev, False))
+        if self._label_gen is None or self._label_gen.device != torch.device(dev):
+            self._label_gen = torch.Generator(device=dev).manual_seed(self.label_seed)
+        Bg, lo = B * self.world, B * self.rank
+        real = self.dyn.get_smooth_labels(epoch, Bg, dev, True, generator=self._label_gen)
+        fake = self.dyn.get_smooth_labels(epoch, Bg, dev, False, generator=self._label_gen)
+        return real[lo:lo + B], fake[lo:lo + B]
 
     def g_step(self, audio, real_pose, valid):
         self.opt_G.zero_grad()
+        self.red_G.begin()
         fake_pose, internal = self.G(audio, real_pose=real_pose)
         fake_d, _ = self.D(pos_to_motion(fake_pose))
         terms = compute_temporal_smoothness_loss_and_jerk(fake_pose, real_pose)
@@ -161,8 +299,7 @@ class GANTrainer:
         for loss in internal:
             g_loss = g_loss + loss
         g_loss.backward()
-        self.opt_G.collect_grads()
-        self._allreduce_(self.opt_G.flat_grad)
+        self.red_G.finish()
         self.opt_G.step()
         return g_loss.detach()
 
@@ -171,12 +308,12 @@ class GANTrainer:
         with torch.no_grad():
             fp, _ = self.G(audio)
             fm = pos_to_motion(fp)
+        self.red_D.begin()
         fake_d, _ = self.D(fm.detach())
         real_d, _ = self.D(real_motion)
         d_loss = AG.mse_loss(real_d, valid) + self.lambda_d * AG.mse_loss(fake_d, fake)
         d_loss.backward()
-        self.opt_D.collect_grads()
-        self._allreduce_(self.opt_D.flat_grad)
+        self.red_D.finish()
         self.opt_D.step()
         return d_loss.detach()
 

@@ -272,7 +272,8 @@ def run_train(args, world, rank, dev):
     torch.manual_seed(1234)                           # identical initial weights on every rank
     g = SelfAttention_G(time_steps=T, p=0.2).to(dev).train()
     d = SelfAttention_D(out_channels=64).to(dev).train()
-    tr = GANTrainer(g, d, lr=10e-4, sync_bn=args.sync_bn)
+    tr = GANTrainer(g, d, lr=10e-4, sync_bn=args.sync_bn, bucket_mb=args.bucket_mb, label_seed=7,
+                    grad_reduce_dtype=torch.bfloat16 if args.dtype == 'bf16' else None)
     gen = torch.Generator(device='cpu').manual_seed(100 + rank)
     audio = torch.randn(B, T, 128, generator=gen).to(dev)
     pose = torch.randn(B, T, 104, generator=gen).to(dev)
@@ -312,6 +313,9 @@ def run_train(args, world, rank, dev):
         'config': {'workload': cfg + ': version5_model_train.py iteration (G x3 + D x1, Adam, '
                                'smoothed noisy labels), DP over ranks',
                    'batchnorm': 'sync' if tr.sync_bn else 'per-rank statistics',
+                   'grad_allreduce': (f'{len(tr.red_G.buckets)} G / {len(tr.red_D.buckets)} D buckets of '
+                                      f'<= {args.bucket_mb:g} MB, overlapped with backward, '
+                                      f'{"bf16" if args.dtype == "bf16" else "fp32"} on the wire'),
                    'global_batch': Bg, 'seq_len': T, 'parallelism': f'dp{world}'},
         'path_roofline': {'bound': 'mfma', 'achieved': round(tf, 2), 'peak': peak,
                           'unit': 'TFLOP/s', 'frac': round(tf / peak / world, 4),
@@ -371,6 +375,8 @@ def main():
     ap.add_argument('--mode', choices=('infer', 'train'), default='infer')
     ap.add_argument('--sync-bn', action='store_true',
                     help='train mode: SyncBN over the DP ranks (SURVEY 8(e)); default per-rank statistics')
+    ap.add_argument('--bucket-mb', type=float, default=25.0,
+                    help='train mode: gradient all-reduce bucket size (MB)')
     ap.add_argument('--dtype', choices=('fp32', 'bf16'), default='fp32',
                     help='GEMM operand precision (bf16: configs[4], fp32 accumulation/storage)')
     args = ap.parse_args()
