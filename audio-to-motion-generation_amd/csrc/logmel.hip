@@ -25,6 +25,7 @@ struct PlanHeader {
   int32_t off_window, off_twiddle, off_start, off_len, off_woff, off_weights;  // byte offsets
   int32_t off_tw1, off_tw2;  // fft_len == 2048 only: per-lane stage twiddles (0 otherwise)
   int32_t n_w4, off_band, off_w4;  // fft_len == 2048 only: band rows padded to float4 (see build_plan)
+  int32_t la, lb;                   // fft_len == 2048 only: float4 rows per lane for bands A / B
 };
 
 static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
@@ -43,7 +44,7 @@ static void plan_layout(int win, int nfft, int n_mels, int nnz, int n_w4, PlanHe
     h->off_tw1 = (int32_t)off; off = align16(off + sizeof(float) * 2 * 16 * 64);
     h->off_tw2 = (int32_t)off; off = align16(off + sizeof(float) * 2 * 16 * 4);
     h->n_w4 = n_w4;
-    h->off_band = (int32_t)off; off = align16(off + sizeof(int32_t) * 2 * n_mels);
+    h->off_band = (int32_t)off; off = align16(off + sizeof(int32_t) * 4 * 64);
     h->off_w4 = (int32_t)off; off = align16(off + sizeof(float) * 4 * (size_t)n_w4);
   }
   *total = off;
@@ -193,58 +194,86 @@ __global__ __launch_bounds__(256) void logmel_kernel(const float* __restrict__ w
 }
 
 
-// ---------------------------------------------------------------------------------------
-// fft_len == 2048 (the build configuration, W = 2048, M = 1024): one wave64 per frame, the
-// FFT register-resident.  M = 1024 is split 16 x 16 x 4:
-//   z[n0 + 64 n1]                                    lane n0 holds n1 = 0..15
-//   stage 1  B[n0][k1] = DFT16_n1, C = B * W1024^(n0 k1)          (registers)
-//   LDS transpose (re/im planes, pitch 68: conflict-free both ways)
-//   stage 2  lane (k1, m0): D[k2] = DFT16_m1 C[m0 + 4 m1][k1], E = D * W64^(m0 k2)
-//   stage 3  DFT4 over m0 across the lane quad (two DPP butterflies, xor 2 then xor 1):
-//            lane m0 = a + 2b ends with Z[k1 + 16 k2 + 256 (b + 2a)]
-// then the real-input split / magnitude (:71-92) and the banded mel + log as above.
-// LDS per frame: 2 x 1088 floats (exchange, then Z, then magnitudes) = 8.7 KB.
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ float2 c_add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 c_sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 
-// forward DFT4 in place (W4 = -i)
-__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
-  const float2 s02 = c_add(a0, a2), d02 = c_sub(a0, a2);
-  const float2 s13 = c_add(a1, a3), d13 = c_sub(a1, a3);
-  a0 = c_add(s02, s13);
-  a2 = c_sub(s02, s13);
-  a1 = make_float2(d02.x + d13.y, d02.y - d13.x);  // d02 - i d13
-  a3 = make_float2(d02.x - d13.y, d02.y + d13.x);  // d02 + i d13
+// LDS ordering between the lanes of ONE wave (each wave owns its exchange region): a
+// wavefront-scope fence pair around a wave barrier (the rocPRIM wave_barrier form).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// v * W16^m for a compile-time m in 1..9
-template <int m>
-__device__ __forceinline__ float2 tw16(float2 v) {
-  constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R2 = 0.70710678118654752f;
-  if constexpr (m == 4) return make_float2(v.y, -v.x);  // -i
-  else if constexpr (m == 2) return make_float2(R2 * (v.x + v.y), R2 * (v.y - v.x));
-  else if constexpr (m == 6) return make_float2(R2 * (v.y - v.x), -R2 * (v.x + v.y));
-  else {
-    constexpr float c = m == 1 ? C1 : m == 3 ? S1 : m == 9 ? -C1 : 0.f;
-    constexpr float s = m == 1 ? S1 : m == 3 ? C1 : m == 9 ? -S1 : 0.f;
-    static_assert(m == 1 || m == 3 || m == 9, "tw16");
-    // W16^m = c - i s
-    return make_float2(c * v.x + s * v.y, c * v.y - s * v.x);
+// ---- packed complex arithmetic: (re, im) in one 64-bit register pair, so every add / mul /
+// fma is one v_pk_*_f32 (two fp32 results per lane and instruction).  Swaps are op_sel
+// modifiers; where a partial negation rides on a swapped or single half (conj, +-i, the
+// complex product) the backend does not fold it into neg_lo / neg_hi and would emit
+// v_xor + v_mov first, so those forms are written out as single instructions.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pmul(f2 a, f2 b) {  // a * b: (a.x b.x - a.y b.y, a.x b.y + a.y b.x)
+  const f2 t = a.xx * b;
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+__device__ __forceinline__ f2 add_mi(f2 a, f2 b) {  // a - i b = (a.x + b.y, a.y - b.x)
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 sub_mi(f2 a, f2 b) {  // a + i b = (a.x - b.y, a.y + b.x)
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 add_conj(f2 a, f2 b) {  // a + conj b
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 sub_conj(f2 a, f2 b) {  // a - conj b
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+constexpr float kR2 = 0.70710678118654752f;
+
+__device__ __forceinline__ void dft4p(f2& a0, f2& a1, f2& a2, f2& a3) {  // W4 = -i
+  const f2 s02 = a0 + a2, d02 = a0 - a2, s13 = a1 + a3, d13 = a1 - a3;
+  a0 = s02 + s13;
+  a2 = s02 - s13;
+  a1 = add_mi(d02, d13);
+  a3 = sub_mi(d02, d13);
+}
+
+template <int m>  // v * W16^m, m in {1, 2, 3, 4, 6, 9}
+__device__ __forceinline__ f2 tw16p(f2 v) {
+  if constexpr (m == 4) {
+    return (f2){1.f, -1.f} * v.yx;                                                 // -i
+  } else if constexpr (m == 2) {
+    return __builtin_elementwise_fma(v.yx, (f2){kR2, -kR2}, kR2 * v);             // (1 - i)/sqrt 2
+  } else if constexpr (m == 6) {
+    return __builtin_elementwise_fma(v.yx, (f2){kR2, -kR2}, -kR2 * v);            // (-1 - i)/sqrt 2
+  } else {
+    constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f;
+    constexpr float c = m == 1 ? C1 : m == 3 ? S1 : -C1;
+    constexpr float s = m == 1 ? S1 : m == 3 ? C1 : -S1;
+    static_assert(m == 1 || m == 3 || m == 9, "tw16p");
+    return __builtin_elementwise_fma(v.yx, (f2){s, -s}, c * v);                    // (c - i s) v
   }
 }
 
-// in place: on return v[k] = sum_j v_in[j] W16^(j k)
-__device__ __forceinline__ void dft16(float2 (&v)[16]) {
+__device__ __forceinline__ void dft16p(f2 (&v)[16]) {  // v[k] = sum_j v[j] W16^(j k)
 #pragma unroll
-  for (int j0 = 0; j0 < 4; ++j0) dft4(v[j0], v[j0 + 4], v[j0 + 8], v[j0 + 12]);  // v[j0+4ka] = T[j0][ka]
-  v[5] = tw16<1>(v[5]); v[9] = tw16<2>(v[9]); v[13] = tw16<3>(v[13]);
-  v[6] = tw16<2>(v[6]); v[10] = tw16<4>(v[10]); v[14] = tw16<6>(v[14]);
-  v[7] = tw16<3>(v[7]); v[11] = tw16<6>(v[11]); v[15] = tw16<9>(v[15]);
+  for (int j0 = 0; j0 < 4; ++j0) dft4p(v[j0], v[j0 + 4], v[j0 + 8], v[j0 + 12]);
+  v[5] = tw16p<1>(v[5]); v[9] = tw16p<2>(v[9]); v[13] = tw16p<3>(v[13]);
+  v[6] = tw16p<2>(v[6]); v[10] = tw16p<4>(v[10]); v[14] = tw16p<6>(v[14]);
+  v[7] = tw16p<3>(v[7]); v[11] = tw16p<6>(v[11]); v[15] = tw16p<9>(v[15]);
 #pragma unroll
-  for (int ka = 0; ka < 4; ++ka) dft4(v[4 * ka], v[4 * ka + 1], v[4 * ka + 2], v[4 * ka + 3]);
-  // position kb + 4 ka holds B[ka + 4 kb]: transpose the 4x4 index
-  float2 t[16];
+  for (int ka = 0; ka < 4; ++ka) dft4p(v[4 * ka], v[4 * ka + 1], v[4 * ka + 2], v[4 * ka + 3]);
+  f2 t[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) t[i] = v[i];
 #pragma unroll
@@ -253,59 +282,71 @@ __device__ __forceinline__ void dft16(float2 (&v)[16]) {
     for (int kb = 0; kb < 4; ++kb) v[ka + 4 * kb] = t[kb + 4 * ka];
 }
 
-template <int CTRL>
-__device__ __forceinline__ float2 dpp_c(float2 v) {
-  return make_float2(dpp_f<CTRL>(v.x), dpp_f<CTRL>(v.y));
-}
-
-// Compile-time twiddles: W16^j, W16^j * W2048 (Hann window from the lane's W1024^lane for
-// samples 2(lane + 64 j) and 2(lane + 64 j) + 1), W32^i (split twiddles W2048^(lane + 64 i)).
+// Compile-time twiddles W16^j and W16^j W2048: the periodic Hann window of samples
+// 2(lane + 64 j) and 2(lane + 64 j) + 1 from the lane's W1024^lane.
 __constant__ const float HANN_C0_RE[16] = {1.f, 0.92387953251128674f, 0.70710678118654757f, 0.38268343236508984f, 6.123233995736766e-17f, -0.38268343236508973f, -0.70710678118654746f, -0.92387953251128674f, -1.f, -0.92387953251128685f, -0.70710678118654768f, -0.38268343236509034f, -1.8369701987210297e-16f, 0.38268343236509f, 0.70710678118654735f, 0.92387953251128652f};
 __constant__ const float HANN_C0_IM[16] = {0.f, -0.38268343236508978f, -0.70710678118654746f, -0.92387953251128674f, -1.f, -0.92387953251128674f, -0.70710678118654757f, -0.38268343236508989f, -1.2246467991473532e-16f, 0.38268343236508967f, 0.70710678118654746f, 0.92387953251128652f, 1.f, 0.92387953251128663f, 0.70710678118654768f, 0.38268343236509039f};
 __constant__ const float HANN_C1_RE[16] = {0.99999529380957619f, 0.92270112833387863f, 0.70493408037590499f, 0.37984720892405111f, -0.0030679567629660156f, -0.3855160538439189f, -0.70927282643886547f, -0.92504924078267747f, -0.99999529380957619f, -0.92270112833387863f, -0.7049340803759051f, -0.37984720892405144f, 0.0030679567629661149f, 0.38551605384391857f, 0.70927282643886569f, 0.92504924078267747f};
 __constant__ const float HANN_C1_IM[16] = {-0.0030679567629659761f, -0.38551605384391885f, -0.70927282643886558f, -0.92504924078267758f, -0.99999529380957619f, -0.92270112833387852f, -0.7049340803759051f, -0.37984720892405138f, 0.0030679567629657324f, 0.38551605384391863f, 0.70927282643886547f, 0.92504924078267747f, 0.99999529380957619f, 0.92270112833387874f, 0.70493408037590488f, 0.37984720892405149f};
-__constant__ const float W32_RE[9] = {1.f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f, 0.70710678118654757f, 0.55557023301960229f, 0.38268343236508984f, 0.19509032201612833f, 6.123233995736766e-17f};
-__constant__ const float W32_IM[9] = {0.f, -0.19509032201612825f, -0.38268343236508978f, -0.55557023301960218f, -0.70710678118654746f, -0.83146961230254524f, -0.92387953251128674f, -0.98078528040323043f, -1.f};
 
-// p[k] = b^k, k = 1..15, by a product tree (each power at most 4 roundings from the table value)
-__device__ __forceinline__ void powers15(float2 b, float2 (&p)[16]) {
-  p[0] = make_float2(1.f, 0.f);
+// v[k] *= b^k, k = 1..15 (powers by a product tree: each at most 4 roundings from b).
+// Computed, not loaded: a wave-wide table load costs ~20 TA cycles whatever its footprint,
+// more than the 2 x 14 packed products it replaces (measured: TA-bound with table twiddles).
+__device__ __forceinline__ void twiddle15p(f2 (&v)[16], f2 b) {
+  f2 p[16];
   p[1] = b;
-  p[2] = cmul(b, b);
-  p[3] = cmul(p[2], b);
-  p[4] = cmul(p[2], p[2]);
-  p[5] = cmul(p[4], b);
-  p[6] = cmul(p[4], p[2]);
-  p[7] = cmul(p[4], p[3]);
-  p[8] = cmul(p[4], p[4]);
+  p[2] = pmul(b, b);
+  p[3] = pmul(p[2], b);
+  p[4] = pmul(p[2], p[2]);
+  p[5] = pmul(p[4], b);
+  p[6] = pmul(p[4], p[2]);
+  p[7] = pmul(p[4], p[3]);
+  p[8] = pmul(p[4], p[4]);
 #pragma unroll
-  for (int k = 9; k < 16; ++k) p[k] = cmul(p[8], p[k - 8]);
+  for (int k = 9; k < 16; ++k) p[k] = pmul(p[8], p[k - 8]);
+#pragma unroll
+  for (int k = 1; k < 16; ++k) v[k] = pmul(v[k], p[k]);
 }
 
-// LDS ordering between the lanes of ONE wave (each wave owns its exchange planes): a
-// wavefront-scope fence pair around a wave barrier (the rocPRIM wave_barrier form).
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+constexpr int LM_WAVES = 8;            // frames (one per wave) per workgroup
+constexpr int LM_P2 = 68;              // complex pitch of the stage-1 -> stage-2 exchange rows
+constexpr int LM_EP = 260;             // complex pitch of the stage-2 output planes E[m0][.]
+constexpr int LM_REGION = 16 * LM_P2;  // complex words per wave (exchange, E, then magnitudes)
+constexpr int LM_ROWS = 12;            // float4 mel-weight rows per lane kept in LDS (build config 3 + 9)
+constexpr int LM_MAX_W4 = 64 * LM_ROWS;
 
-constexpr int LM_WAVES = 8;          // frames (one per wave) per workgroup
-constexpr int LM_PLANE = 16 * 68;    // floats per exchange plane (pitch 68; Z / magnitudes reuse it)
-constexpr int LM_MAX_W4 = 640;       // float4 mel-weight rows staged in LDS (build config: ~520)
-
+// ---------------------------------------------------------------------------------------
+// fft_len == 2048 (the build configuration, W = 2048, M = 1024): one wave64 per frame, the
+// 1024-point complex FFT of z[n] = xw[2n] + i xw[2n+1] register-resident, all complex
+// arithmetic packed (v_pk_*_f32).  M = 16 x 16 x 4:
+//   stage 1  lane n0 holds z[n0 + 64 n1]: B = DFT16_n1, C[n0][k1] = B W1024^(n0 k1)
+//   LDS exchange (rows k1, pitch 68 complex: ds_*_b64 conflict-free both ways)
+//   stage 2  lane (k1, m0): DFT16 over m1 of C[m0 + 4 m1][k1], times W64^(m0 k2)
+//            -> E[m0][b], b = k1 + 16 k2, stored to LDS planes m0 (pitch 260)
+//   split    Z[b + 256 k3] = DFT4_m0 E[m0][b] (W4 = -i).  A lane takes the two bases b and
+//            256 - b (their DFT4s hold exactly the partners Z[M - k] of each other's Z[k]):
+//            units b = lane + 1 and b = lane + 65 (b = 128 pairs with itself), lane 63's
+//            second unit is {0, 128}.  Each (k, M - k) pair gives both magnitudes:
+//            s = Z[k] + conj Z[M-k], d = Z[k] - conj Z[M-k], wd = -i W2048^k d,
+//            2|X[k]| = |s + wd|, 2|X[M-k]| = |s - wd| (the 1/2 is folded into the mel rows)
+//   mel      lane owns bands lane and 127 - lane (narrow + wide: balanced), rows aligned to
+//            4 bins so weights and magnitudes are both read as float4
+// then log(mel + offset).  LDS per wave: 8.7 KB; the mel rows once per workgroup.
+// ---------------------------------------------------------------------------------------
 template <bool FULL>  // FULL: window == fft_len == 2048 (Hann from twiddles, no predicated loads)
 __global__ __launch_bounds__(64 * LM_WAVES) void logmel2048_kernel(
     const float* __restrict__ wave, int64_t clip_stride, int n_frames, int total_frames,
     const unsigned char* __restrict__ plan, float log_offset, float* __restrict__ out) {
-  constexpr int M = 1024, P = 68;
-  __shared__ float s_plane[LM_WAVES][2][LM_PLANE];
+  constexpr int M = 1024;
+  __shared__ f2 s_region[LM_WAVES][LM_REGION];
   __shared__ float4 s_w4[LM_MAX_W4];
   const PlanHeader* ph = reinterpret_cast<const PlanHeader*>(plan);
   const int win = ph->window, hop = ph->hop, n_mels = ph->n_mels, n_w4 = ph->n_w4;
+  const int la = ph->la, lb = ph->lb;
+  const bool lds_rows = la + lb <= LM_ROWS;      // else the mel rows are read from L2
   const float* window = reinterpret_cast<const float*>(plan + ph->off_window);
-  const float2* tw = reinterpret_cast<const float2*>(plan + ph->off_twiddle);
-  const int2* band = reinterpret_cast<const int2*>(plan + ph->off_band);
+  const f2* tw = reinterpret_cast<const f2*>(plan + ph->off_twiddle);   // W2048^t
+  const int4* band = reinterpret_cast<const int4*>(plan + ph->off_band);
   const float4* w4 = reinterpret_cast<const float4*>(plan + ph->off_w4);
 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -314,31 +355,39 @@ __global__ __launch_bounds__(64 * LM_WAVES) void logmel2048_kernel(
   const int frame = active ? gframe % n_frames : 0;
   const int clip = active ? gframe / n_frames : 0;
   const float* src = wave + clip * clip_stride + (int64_t)frame * hop;
-  float* s_re = s_plane[wv][0];
-  float* s_im = s_plane[wv][1];
+  f2* sx = s_region[wv];
 
   // mel weight rows: one copy per workgroup in LDS (loads issued before the frame's samples)
   float4 wst[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = threadIdx.x + i * 64 * LM_WAVES;
-    wst[i] = q < n_w4 ? w4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    wst[i] = lds_rows && q < n_w4 ? w4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // per-lane values used later, fetched now (L2-resident plan)
+  const f2 b1 = tw[2 * lane];                    // W1024^lane
+  const int k1 = lane >> 2, m0 = lane & 3;
+  const f2 b2 = tw[32 * m0];                     // W64^m0
+  const bool sp = lane == 63;                    // unit 1 of lane 63 is {0, 128}
+  const int ub0 = lane + 1, ub1 = sp ? 0 : lane + 65;
+  const f2 t0 = tw[ub0], t1 = tw[ub1], t128 = tw[128];
+  const int4 bd = band[lane];
 
-  // ---- stage 1: lane n0 = lane holds z[n0 + 64 j] = xw[2n] + i xw[2n+1], n = n0 + 64 j
-  const float2 b1 = tw[2 * lane];  // W1024^lane
-  float2 v[16];
+  // ---- stage 1
+  f2 v[16];
   {
-    float a[16], b[16];
+    f2 x[16], w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int n = 2 * (lane + 64 * j);
-      if (FULL) {
-        a[j] = src[n];
-        b[j] = src[n + 1];
+      if (FULL) {  // 0.5 - 0.5 cos(2 pi n / 2048) = 0.5 - 0.5 Re(W1024^lane W16^j [W2048])
+        x[j] = (f2){src[n], src[n + 1]};
+        const f2 cre = (f2){HANN_C0_RE[j], HANN_C1_RE[j]}, cim = (f2){HANN_C0_IM[j], HANN_C1_IM[j]};
+        const f2 r = __builtin_elementwise_fma(-b1.yy, cim, b1.xx * cre);
+        w[j] = __builtin_elementwise_fma((f2)(-0.5f), r, (f2)(0.5f));
       } else {
-        a[j] = n < win ? src[n] : 0.f;
-        b[j] = n + 1 < win ? src[n + 1] : 0.f;
+        x[j] = (f2){n < win ? src[n] : 0.f, n + 1 < win ? src[n + 1] : 0.f};
+        w[j] = (f2){n < win ? window[n] : 0.f, n + 1 < win ? window[n + 1] : 0.f};
       }
     }
 #pragma unroll
@@ -347,125 +396,113 @@ __global__ __launch_bounds__(64 * LM_WAVES) void logmel2048_kernel(
       if (q < LM_MAX_W4) s_w4[q] = wst[i];
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      float wa, wb;
-      if (FULL) {  // 0.5 - 0.5 cos(2 pi n / 2048) = 0.5 - 0.5 Re(W1024^lane W16^j [W2048])
-        wa = fmaf(-0.5f, b1.x * HANN_C0_RE[j] - b1.y * HANN_C0_IM[j], 0.5f);
-        wb = fmaf(-0.5f, b1.x * HANN_C1_RE[j] - b1.y * HANN_C1_IM[j], 0.5f);
-      } else {
-        const int n = 2 * (lane + 64 * j);
-        wa = n < win ? window[n] : 0.f;
-        wb = n + 1 < win ? window[n + 1] : 0.f;
-      }
-      v[j] = make_float2(a[j] * wa, b[j] * wb);
-    }
+    for (int j = 0; j < 16; ++j) v[j] = x[j] * w[j];
   }
-  dft16(v);
-  {
-    float2 t[16];
-    powers15(b1, t);  // W1024^(n0 k1)
+  dft16p(v);
+  twiddle15p(v, b1);                             // W1024^(n0 k1)
 #pragma unroll
-    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], t[k]);
-  }
-#pragma unroll
-  for (int k = 0; k < 16; ++k) { s_re[k * P + lane] = v[k].x; s_im[k * P + lane] = v[k].y; }
-  __syncthreads();  // also publishes s_w4 (the only workgroup-wide barrier)
+  for (int k = 0; k < 16; ++k) sx[k * LM_P2 + lane] = v[k];
+  wave_lds_sync();  // the exchange region is this wave's own
 
   // ---- stage 2: lane (k1, m0)
-  const int k1 = lane >> 2, m0 = lane & 3;
 #pragma unroll
-  for (int m1 = 0; m1 < 16; ++m1) {
-    const int a = k1 * P + m0 + 4 * m1;
-    v[m1] = make_float2(s_re[a], s_im[a]);
-  }
-  dft16(v);
-  {
-    float2 t[16];
-    powers15(tw[32 * m0], t);  // W64^(m0 k2)
+  for (int m1 = 0; m1 < 16; ++m1) v[m1] = sx[k1 * LM_P2 + m0 + 4 * m1];
+  dft16p(v);
+  twiddle15p(v, b2);                             // W64^(m0 k2)
+  wave_lds_sync();  // every stage-2 read of this wave before E overwrites the region
 #pragma unroll
-    for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], t[k]);
-  }
-
-  // ---- stage 3: DFT4 over m0 = a + 2b across the quad
-  const int qa = m0 & 1, qb = m0 >> 1;
-  const float sb = qb ? -1.f : 1.f, sa = qa ? -1.f : 1.f;
-  const bool rot = qa & qb;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const float2 p = dpp_c<DPP_XOR2>(v[k]);
-    float2 u = make_float2(fmaf(sb, v[k].x, p.x), fmaf(sb, v[k].y, p.y));
-    if (rot) u = make_float2(u.y, -u.x);  // (-i)^(a b)
-    const float2 q = dpp_c<DPP_XOR1>(u);
-    v[k] = make_float2(fmaf(sa, u.x, q.x), fmaf(sa, u.y, q.y));
-  }
-  wave_lds_sync();  // stage-2 reads done before the planes are reused for Z
-  const int k3 = qb + 2 * qa;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int idx = k1 + 16 * k + 264 * k3;  // Z index + 8 * (index >> 8)
-    s_re[idx] = v[k].x;
-    s_im[idx] = v[k].y;
-  }
+  for (int k2 = 0; k2 < 16; ++k2) sx[m0 * LM_EP + k1 + 16 * k2] = v[k2];
   wave_lds_sync();
 
-  // ---- real-input split and magnitude.  Lane pairs k with M-k: with e = (Z[k] + conj Z[M-k])/2,
-  // o = (Z[k] - conj Z[M-k])/(2i): X[k] = e + W^k o and X[M-k] = conj(e - W^k o), so one pair
-  // of Z reads gives both magnitudes (k = 0 gives X[0] and X[M]).  All Z reads finish before the
-  // magnitudes overwrite the re plane (mag[k] at plain index k).
-  const float2 bs = tw[lane];  // W2048^lane; W2048^(lane + 64 i) = bs * W32^i
-  float mk[9], mc[9];
+  // ---- split: DFT4 over m0, real-input split, magnitudes (x2)
+  float mg[17];
+  int ki[17];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int k = lane + 64 * i;
-    const int kk = k <= M / 2 ? k : 0;
-    const int ic = kk == 0 ? 0 : M - kk;
-    const int ak = kk + 8 * (kk >> 8), ac = ic + 8 * (ic >> 8);
-    const float2 zk = make_float2(s_re[ak], s_im[ak]);
-    const float2 zc = make_float2(s_re[ac], s_im[ac]);
-    const float2 e = make_float2(0.5f * (zk.x + zc.x), 0.5f * (zk.y - zc.y));
-    const float2 dd = make_float2(zk.x - zc.x, zk.y + zc.y);
-    const float2 o = make_float2(0.5f * dd.y, -0.5f * dd.x);
-    const float2 wk = i == 0 ? bs : cmul(bs, make_float2(W32_RE[i], W32_IM[i]));
-    const float2 wo = cmul(wk, o);
-    const float pr = e.x + wo.x, pi = e.y + wo.y, qr = e.x - wo.x, qi = e.y - wo.y;
-    mk[i] = __builtin_amdgcn_sqrtf(pr * pr + pi * pi);
-    mc[i] = __builtin_amdgcn_sqrtf(qr * qr + qi * qi);
-  }
-  wave_lds_sync();
-  float* s_mag = s_re;
+  for (int u = 0; u < 2; ++u) {
+    const int b = u == 0 ? ub0 : ub1;
+    const int bp = u == 0 ? 256 - ub0 : (sp ? 128 : 256 - ub1);
+    const f2 t = u == 0 ? t0 : t1;
+    f2 za[4], zb[4];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int k = lane + 64 * i;
-    if (k <= M / 2) {
-      s_mag[k] = mk[i];
-      if (k < M / 2) s_mag[M - k] = mc[i];
+    for (int q = 0; q < 4; ++q) {
+      za[q] = sx[q * LM_EP + b];
+      zb[q] = sx[q * LM_EP + bp];
     }
-  }
-  wave_lds_sync();
-
-  // ---- banded mel + log: lane owns bands lane and lane + 64 (host: n_mels <= 128), weights
-  // from the workgroup's LDS rows (zero past a band's support; magnitude index clamped)
-  if (!active) return;
-  float* dst = out + (int64_t)gframe * n_mels;
+    dft4p(za[0], za[1], za[2], za[3]);
+    dft4p(zb[0], zb[1], zb[2], zb[3]);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int m = lane + 64 * h;
-    if (m < n_mels) {
-      const int2 bd = band[m];
-      const int st = bd.x & 0xFFFF, l4 = bd.x >> 16;
-      const float4* wr = s_w4 + bd.y;
-      float acc = 0.f;
-      for (int c = 0; c < l4; ++c) {
-        const float4 wq = wr[c];
-        const int bi = st + 4 * c;
-        acc += wq.x * s_mag[min(bi, M)];
-        acc += wq.y * s_mag[min(bi + 1, M)];
-        acc += wq.z * s_mag[min(bi + 2, M)];
-        acc += wq.w * s_mag[min(bi + 3, M)];
+    for (int k3 = 0; k3 < 4; ++k3) {
+      f2 first = za[k3], second = zb[3 - k3];
+      f2 w = k3 == 0 ? t : k3 == 1 ? tw16p<2>(t) : k3 == 2 ? tw16p<4>(t) : tw16p<6>(t);  // W8^k3
+      int ka = b + 256 * k3;
+      if (u == 1) {  // lane 63: pairs (0,1024), (256,768) from Z[0..3*256]; (128,896), (384,640)
+        if (k3 < 2) {
+          second = sp ? za[(4 - k3) & 3] : second;
+        } else {
+          first = sp ? zb[k3 - 2] : first;
+          second = sp ? zb[5 - k3] : second;
+          const f2 ws = k3 == 2 ? t128 : tw16p<2>(t128);
+          w = sp ? ws : w;
+          ka = sp ? 128 + 256 * (k3 - 2) : ka;
+        }
       }
-      dst[m] = __logf(acc + log_offset);
+      const f2 s = add_conj(first, second), d = sub_conj(first, second);
+      const f2 wd = pmul(w, d);                  // X2 = s -+ i wd
+      const f2 xa = add_mi(s, wd), xb = sub_mi(s, wd);
+      const f2 qa = xa * xa, qb = xb * xb;
+      mg[8 * u + 2 * k3] = __builtin_amdgcn_sqrtf(qa.x + qa.y);
+      mg[8 * u + 2 * k3 + 1] = __builtin_amdgcn_sqrtf(qb.x + qb.y);
+      ki[8 * u + 2 * k3] = ka;
+      ki[8 * u + 2 * k3 + 1] = M - ka;
+    }
+    if (u == 1) {  // lane 63 also owns X[512] = |Z[512]| (stored x2 like the others)
+      const f2 q = za[2] * za[2];
+      mg[16] = 2.f * __builtin_amdgcn_sqrtf(q.x + q.y);
+      ki[16] = 512;
     }
   }
+  wave_lds_sync();  // every E read of this wave before the magnitudes overwrite the region
+  float* s_mag = reinterpret_cast<float*>(sx);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s_mag[ki[i]] = mg[i];
+  if (sp) s_mag[ki[16]] = mg[16];
+  s_mag[M + 1 + lane] = 0.f;  // zero tail: aligned band rows may read past bin 1024
+  wave_lds_sync();
+
+  // ---- banded mel + log: bands A = lane and B = 127 - lane, rows contiguous in s_w4.  The
+  // workgroup's only barrier publishes s_w4 here, so until now every wave ran its FFT as soon
+  // as its own samples arrived, overlapping the other frames' loads.
+  __syncthreads();
+  if (!active) return;
+  const int stA = bd.x, stB = bd.y, r0 = lane * (la + lb);
+  f2 accA = (f2)(0.f), accB = (f2)(0.f);
+  if (lds_rows) {
+    for (int c = 0; c < la; ++c) {
+      const float4 wq = s_w4[r0 + c], mq = *reinterpret_cast<const float4*>(s_mag + stA + 4 * c);
+      accA = __builtin_elementwise_fma((f2){wq.x, wq.y}, (f2){mq.x, mq.y}, accA);
+      accA = __builtin_elementwise_fma((f2){wq.z, wq.w}, (f2){mq.z, mq.w}, accA);
+    }
+    for (int c = 0; c < lb; ++c) {
+      const float4 wq = s_w4[r0 + la + c], mq = *reinterpret_cast<const float4*>(s_mag + stB + 4 * c);
+      accB = __builtin_elementwise_fma((f2){wq.x, wq.y}, (f2){mq.x, mq.y}, accB);
+      accB = __builtin_elementwise_fma((f2){wq.z, wq.w}, (f2){mq.z, mq.w}, accB);
+    }
+  } else {
+    for (int c = 0; c < la; ++c) {
+      const float4 wq = w4[r0 + c], mq = *reinterpret_cast<const float4*>(s_mag + stA + 4 * c);
+      accA = __builtin_elementwise_fma((f2){wq.x, wq.y}, (f2){mq.x, mq.y}, accA);
+      accA = __builtin_elementwise_fma((f2){wq.z, wq.w}, (f2){mq.z, mq.w}, accA);
+    }
+    for (int c = 0; c < lb; ++c) {
+      const float4 wq = w4[r0 + la + c], mq = *reinterpret_cast<const float4*>(s_mag + stB + 4 * c);
+      accB = __builtin_elementwise_fma((f2){wq.x, wq.y}, (f2){mq.x, mq.y}, accB);
+      accB = __builtin_elementwise_fma((f2){wq.z, wq.w}, (f2){mq.z, mq.w}, accB);
+    }
+  }
+  float* dst = out + (int64_t)gframe * n_mels;
+  const int mA = lane, mB = 127 - lane;
+  if (mA < n_mels) dst[mA] = __logf(accA.x + accA.y + log_offset);
+  if (mB >= 64 && mB < n_mels) dst[mB] = __logf(accB.x + accB.y + log_offset);
 }
 
 }  // namespace a2m
@@ -512,12 +549,20 @@ static int build_plan(int32_t sr, double win_s, double hop_s, int32_t n_mels, do
   PlanHeader h{};
   h.window = win; h.hop = hop; h.fft_len = nfft; h.n_mels = n_mels; h.n_bins = n_bins;
   h.nnz = (int32_t)vals.size();
-  int n_w4 = 0;
-  for (int m = 0; m < n_mels; ++m) n_w4 += (len[m] + 3) / 4;
-  A2M_CHECK_ARG(nfft != 2048 || n_mels > 128 || n_w4 <= LM_MAX_W4,
-                "logmel: %d weight rows exceed the kernel's LDS copy", n_w4);
+  // register-FFT path (fft_len 2048, <= 128 mels): lane l owns bands A = l and B = 127 - l;
+  // each band's row starts at a multiple of 4 bins and every lane's A (B) row is zero-padded
+  // to the widest A (B) row, la (lb) float4s, so the kernel's loops have uniform trip counts
+  auto row4 = [&](int m) { return m < n_mels && len[m] > 0 ? (start[m] % 4 + len[m] + 3) / 4 : 0; };
+  int la = 0, lb = 0;
+  for (int l = 0; l < 64; ++l) {
+    la = std::max(la, row4(l));
+    lb = std::max(lb, row4(127 - l));
+  }
+  const int n_w4 = 64 * (la + lb);
   size_t total;
   plan_layout(win, nfft, n_mels, h.nnz, n_w4, &h, &total);
+  h.la = la;
+  h.lb = lb;
   *need = total;
   if (host == nullptr) return A2M_OK;
   if (bytes < total) { set_error("logmel plan buffer too small (%zu < %zu)", bytes, total); return A2M_EWS; }
@@ -549,17 +594,20 @@ static int build_plan(int32_t sr, double win_s, double hop_s, int32_t n_mels, do
         t2[2 * (k2 * 4 + m0) + 1] = (float)std::sin(a);
       }
   }
-  if (nfft == 2048) {  // same CSR weights, each band's row zero-padded to whole float4s:
-    // band[m] = {start | len4 << 16, row offset in float4s}
+  if (nfft == 2048 && n_mels <= 128) {
+    // band[lane] = {A start, B start, 0, 0} (starts rounded down to a multiple of 4); rows of
+    // lane l at float4 l (la + lb): A then B; weights x 0.5 (the kernel's magnitudes are 2 |X|)
     int32_t* band = reinterpret_cast<int32_t*>(p + h.off_band);
     float* w4 = reinterpret_cast<float*>(p + h.off_w4);
-    int o4 = 0;
-    for (int m = 0; m < n_mels; ++m) {
-      const int l4 = (len[m] + 3) / 4;
-      band[2 * m] = start[m] | (l4 << 16);
-      band[2 * m + 1] = o4;
-      for (int q = 0; q < len[m]; ++q) w4[4 * o4 + q] = vals[woff[m] + q];
-      o4 += l4;
+    for (int lane = 0; lane < 64; ++lane) {
+      for (int half = 0; half < 2; ++half) {
+        const int m = half == 0 ? lane : 127 - lane;
+        const int l4 = row4(m);
+        const int st4 = l4 ? start[m] & ~3 : 0;
+        band[4 * lane + half] = st4;
+        float* row = w4 + 4 * (lane * (la + lb) + (half == 0 ? 0 : la));
+        for (int q = 0; q < (l4 ? len[m] : 0); ++q) row[(start[m] - st4) + q] = 0.5f * vals[woff[m] + q];
+      }
     }
   }
   std::memcpy(p + h.off_start, start.data(), sizeof(int32_t) * n_mels);
@@ -598,9 +646,8 @@ int a2m_logmel_f32(const float* wave, int64_t n_clips, int64_t clip_stride, int6
   const size_t lds = sizeof(float) * (2 * (size_t)fft_len + fft_len / 2 + 1 + 3);
   A2M_CHECK_ARG(lds <= 160 * 1024, "logmel: fft_len %d too large for LDS", fft_len);
   static const bool generic_only = std::getenv("A2M_LOGMEL_GENERIC") != nullptr;
-  // register-FFT path.  Its LDS copy of the band rows always fits: with strictly increasing
-  // mel edges a bin lies inside at most two triangles, so nnz <= 2 * 1025 and
-  // n_w4 <= (nnz + 3 n_mels) / 4 <= 609 < LM_MAX_W4 (build_plan asserts it).
+  // register-FFT path (its mel rows sit in LDS when each lane's fit in LM_ROWS float4s, as
+  // for the build configuration, and are read from L2 otherwise)
   if (fft_len == 2048 && n_mels <= 128 && !generic_only) {
     auto kern = window == 2048 ? logmel2048_kernel<true> : logmel2048_kernel<false>;
     const int64_t total = n_clips * nf;
