@@ -177,6 +177,10 @@ __device__ __forceinline__ float wave64_max(float v) {
 
 // Fused attention core for T <= 64, C/8 <= 64 (attn_core.hip).
 bool attn_core_fits(int C, int T);
+bool attn_core_wide_fits(int C, int T);
+int attn_core_wide(const float* qkv, int64_t qs_b, int B, int C, int T, const float* gamma,
+                   const float* x, int64_t x_bs, const float* res, float* y, float* attn_out,
+                   hipStream_t st);
 int attn_core(const float* qkv, int64_t qs_b, int B, int C, int T, const float* gamma,
               const float* x, int64_t x_bs, const float* res, float* y, float* attn_out,
               hipStream_t st);

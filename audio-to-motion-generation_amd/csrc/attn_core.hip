@@ -362,6 +362,190 @@ __global__ __launch_bounds__(256, 1) void attn_fused_eval_kernel(
 
 bool attn_fused_eval_fits(int C, int T) { return T <= AT && T % 4 == 0 && (C == 128 || C == 256); }
 
+// ---------------------------------------------------------------------------------------
+// Wide queries, short sequences: the UNet's SelfAttention(2048) at T = 16 / 32 (bottleneck and
+// up_attention, model_layers.py:336-339) and the discriminator's at T = 4: C/8 = 256 query
+// channels, T <= 32.  One workgroup per (clip, 256-channel chunk of V); the four waves split
+// the score product's K = C/8 in quarters (32 MFMAs each) and sum the partial 32 x 32 tiles
+// through LDS, one softmax, then each wave multiplies 64 V channels (fragments straight from
+// L2 into registers, issued first) by the attention tile.  Replaces the score GEMM, the
+// softmax launch and the PV GEMM of the general path (three tiny-batched launches).
+// ---------------------------------------------------------------------------------------
+constexpr int WT = 32;            // max T
+constexpr int WQ = 256;           // max C/8
+constexpr int WQP = WQ + 4;       // Q^T / K^T pitch
+constexpr int WAP = WT + 4;       // attention-tile pitch
+constexpr int WCH = 256;          // V channels per workgroup
+
+__global__ __launch_bounds__(256, 2) void attn_core_wide_kernel(
+    const float* __restrict__ qkv, int64_t qs_b, int C, int T, const float* __restrict__ gamma,
+    const float* __restrict__ x, int64_t x_bs, const float* __restrict__ res,
+    float* __restrict__ y, float* __restrict__ attn_out) {
+  __shared__ __attribute__((aligned(16))) float qs[WT * WQP];   // Q^T [i][c'], later partials
+  __shared__ __attribute__((aligned(16))) float ks[WT * WQP];   // K^T [j][c']
+  __shared__ __attribute__((aligned(16))) float as[WT * WAP];   // attention [i][j]
+  const int b = blockIdx.y, c0 = blockIdx.x * WCH;
+  const int Cq = C / 8;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const float* q = qkv + (int64_t)b * qs_b;
+  const float* k = q + (int64_t)Cq * T;
+  const float* v = q + (int64_t)2 * Cq * T;
+
+  // V fragments of this wave's 64 channels (two 32-row tiles), k = j = 16 kc + 8 lh + s
+  float4 vf[2][2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const float* vr = v + (int64_t)(c0 + wave * 64 + m * 32 + li) * T;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const int j = kc * 16 + lh * 8;
+      vf[m][kc][0] = j < T ? *reinterpret_cast<const float4*>(vr + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      vf[m][kc][1] = j + 4 < T ? *reinterpret_cast<const float4*>(vr + j + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // Q^T, K^T into LDS (float4 along t, written transposed); rows t >= T are zero
+  {
+    const int nq = Cq * (T / 4);
+    for (int e0 = 0; e0 < Cq * (WT / 4); e0 += 256 * 4) {
+      float4 qv[4], kv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + tid + u * 256;
+        const int c = e / (T / 4), tq = e % (T / 4);
+        const bool ok = e < nq;
+        qv[u] = ok ? *reinterpret_cast<const float4*>(q + (int64_t)c * T + 4 * tq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        kv[u] = ok ? *reinterpret_cast<const float4*>(k + (int64_t)c * T + 4 * tq) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + tid + u * 256;
+        if (e >= nq) continue;
+        const int c = e / (T / 4), t = 4 * (e % (T / 4));
+        qs[(t + 0) * WQP + c] = qv[u].x; qs[(t + 1) * WQP + c] = qv[u].y;
+        qs[(t + 2) * WQP + c] = qv[u].z; qs[(t + 3) * WQP + c] = qv[u].w;
+        ks[(t + 0) * WQP + c] = kv[u].x; ks[(t + 1) * WQP + c] = kv[u].y;
+        ks[(t + 2) * WQP + c] = kv[u].z; ks[(t + 3) * WQP + c] = kv[u].w;
+      }
+    }
+    for (int e = tid; e < (WT - T) * Cq; e += 256) {   // zero rows T..31
+      const int t = T + e / Cq, c = e % Cq;
+      qs[t * WQP + c] = 0.f;
+      ks[t * WQP + c] = 0.f;
+    }
+  }
+  __syncthreads();
+
+  // partial scores over this wave's quarter of c': S_w[i][j], i = query row, j = key
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  {
+    const int cq4 = Cq / 4, cb = wave * cq4;
+    for (int kc = 0; kc < cq4; kc += 16) {
+      const float* qa = qs + li * WQP + cb + kc + lh * 8;
+      const float* kb = ks + li * WQP + cb + kc + lh * 8;
+      const float4 a0 = *reinterpret_cast<const float4*>(qa), a1 = *reinterpret_cast<const float4*>(qa + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(kb), b1 = *reinterpret_cast<const float4*>(kb + 4);
+      const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+    }
+  }
+  __syncthreads();   // every Q^T / K^T read done: the partials overlay qs
+  float* part = qs;  // [wave][i][j], pitch WAP
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = (r & 3) + 8 * (r >> 2) + 4 * lh;
+    part[(wave * WT + i) * WAP + li] = acc[r];
+  }
+  __syncthreads();
+
+  // softmax over j < T: 8 threads per row (4 columns each), the four partials summed in a
+  // fixed order; rows / columns >= T are zero
+  {
+    const int i = tid >> 3, p8 = tid & 7;
+    float e[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = p8 * 4 + u;
+      float sv = part[(0 * WT + i) * WAP + j] + part[(1 * WT + i) * WAP + j];
+      sv += part[(2 * WT + i) * WAP + j];
+      sv += part[(3 * WT + i) * WAP + j];
+      e[u] = j < T ? sv : -INFINITY;
+      mx = fmaxf(mx, e[u]);
+    }
+    mx = fmaxf(mx, dpp_f<DPP_XOR1>(mx));
+    mx = fmaxf(mx, dpp_f<DPP_XOR2>(mx));
+    mx = fmaxf(mx, __shfl_xor(mx, 4));
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      e[u] = p8 * 4 + u < T ? expf(e[u] - mx) : 0.f;
+      sum += e[u];
+    }
+    sum += dpp_f<DPP_XOR1>(sum);
+    sum += dpp_f<DPP_XOR2>(sum);
+    sum += __shfl_xor(sum, 4);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = i < T ? e[u] * inv : 0.f;
+    *reinterpret_cast<float4*>(as + i * WAP + p8 * 4) = make_float4(e[0], e[1], e[2], e[3]);
+    if (attn_out && blockIdx.x == 0 && i < T) {
+      float* ar = attn_out + ((int64_t)b * T + i) * T;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (p8 * 4 + u < T) ar[p8 * 4 + u] = e[u];
+    }
+  }
+  __syncthreads();
+
+  // out[c][i] = gamma * sum_j V[c][j] A[i][j] + x[c][i] (+ res): this wave's 64 channels
+  const float g = gamma[0];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      if (kc * 16 >= T) break;
+      const float* ar = as + li * WAP + kc * 16 + lh * 8;
+      const float4 b0 = *reinterpret_cast<const float4*>(ar), b1 = *reinterpret_cast<const float4*>(ar + 4);
+      const float af[8] = {vf[m][kc][0].x, vf[m][kc][0].y, vf[m][kc][0].z, vf[m][kc][0].w,
+                           vf[m][kc][1].x, vf[m][kc][1].y, vf[m][kc][1].z, vf[m][kc][1].w};
+      const float bf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+    }
+    if (li < T) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = c0 + wave * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int64_t o = (int64_t)b * x_bs + (int64_t)c * T + li;
+        float val = g * acc[r] + x[o];
+        if (res) val += res[o];
+        y[o] = val;
+      }
+    }
+  }
+}
+
+bool attn_core_wide_fits(int C, int T) {
+  return T >= 4 && T <= WT && T % 4 == 0 && C % 8 == 0 && C % WCH == 0 && C / 8 <= WQ && (C / 8) % 64 == 0;
+}
+
+int attn_core_wide(const float* qkv, int64_t qs_b, int B, int C, int T, const float* gamma,
+                   const float* x, int64_t x_bs, const float* res, float* y, float* attn_out,
+                   hipStream_t st) {
+  dim3 grid((unsigned)(C / WCH), (unsigned)B);
+  hipLaunchKernelGGL(attn_core_wide_kernel, grid, dim3(256), 0, st, qkv, qs_b, C, T, gamma, x, x_bs,
+                     res, y, attn_out);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
 int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const float* wqkv,
                     const float* bqkv, const float* gamma, const float* res, float* y,
                     hipStream_t st) {

@@ -679,6 +679,8 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
   static const int fused_ok = std::getenv("A2M_ATTN_FUSED") ? std::atoi(std::getenv("A2M_ATTN_FUSED")) : 1;
   if (fused_ok && attn_core_fits(C, T))
     return attn_core(qkv, qs_b, B, C, T, gamma, x, x_bs, res, y, attn, st);
+  if (fused_ok && attn_core_wide_fits(C, T))   // the UNet's / D's SelfAttention(2048), T <= 32
+    return attn_core_wide(qkv, qs_b, B, C, T, gamma, x, x_bs, res, y, attn, st);
   // scores[b][i][j] = sum_c q[b][c][i] k[b][c][j]
   Gather Aq = dense_kr(qkv, T, qs_b);
   Gather Bk = dense_kr(qkv + (int64_t)Cq * T, T, qs_b);

@@ -167,10 +167,13 @@ def test_interp_time():
 
 
 @pytest.mark.parametrize('B,C,T', [(2, 256, 64), (2, 2048, 16), (1, 64, 480), (3, 16, 5), (64, 256, 64),
-                                   (3, 128, 36)])
+                                   (3, 128, 36), (2, 2048, 32), (3, 2048, 4), (2, 512, 12), (4, 2048, 20)])
 def test_self_attention(B, C, T):
     """Eval path: (B, 256, 64) / (B, 128, 36) run the fused QKV + attention kernel
-    (a2m_self_attention_eval_f32); the others the packed QKV GEMM + core / general path."""
+    (a2m_self_attention_eval_f32); C = 2048 / 512 at T <= 32 the wide attention core
+    (attn_core_wide_kernel, the UNet's and D's SelfAttention(2048)); the others the packed
+    QKV GEMM + core / general path.  The attention matrix kept for the backward pass is
+    checked against Q^T K softmax on the host."""
     from a2m import functional as F
     from oracle import model as OM
     x, res = _rand(B, C, T, seed=50), _rand(B, C, T, seed=51)
@@ -193,6 +196,14 @@ def test_self_attention(B, C, T):
                                 d['a.key_conv.weight'], d['a.key_conv.bias'], d['a.value_conv.weight'],
                                 d['a.value_conv.bias'], d['a.gamma'], res=res.to(DEV), save=save)
         assert 'qkv' in save and rel_err(out.cpu(), out2.cpu()) < 2e-6
+    save = {}
+    F.self_attention(x.to(DEV), d['a.query_conv.weight'], d['a.query_conv.bias'], d['a.key_conv.weight'],
+                     d['a.key_conv.bias'], d['a.value_conv.weight'], d['a.value_conv.bias'], d['a.gamma'],
+                     res=res.to(DEV), save=save)
+    q = torch.einsum('oc,bct->bot', sd['a.query_conv.weight'][..., 0], x) + sd['a.query_conv.bias'][None, :, None]
+    k = torch.einsum('oc,bct->bot', sd['a.key_conv.weight'][..., 0], x) + sd['a.key_conv.bias'][None, :, None]
+    att = torch.softmax(torch.einsum('bci,bcj->bij', q.double(), k.double()), dim=-1)
+    assert rel_err(save['attn'].cpu(), att) < TOL
 
 
 def test_derived_weight_caches_follow_updates():

@@ -1,0 +1,63 @@
+"""MFMA utilisation per kernel family from a rocprofv3 PMC pass of
+SQ_VALU_MFMA_BUSY_CYCLES + SQ_BUSY_CYCLES + GRBM_GUI_ACTIVE and a kernel-trace pass of the
+same command (tools/step_pmc.sh).
+
+  busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycles), cycles = GRBM_GUI_ACTIVE / 8
+  (rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs: MI355X_MICROARCH.md, DVFS give-back).
+The counter's scale is calibrated in DESIGN.md against the engine's known MFMA count
+(mfma_cycles_per_mfma below: busy cycles per v_mfma_f32_32x32x2_f32).
+
+    python tools/pmc_mfma.py MFMA_DIR TRACE_DIR [--out file.json]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+FAMILIES = ('gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'graph_layer_kernel',
+            'attn_fused_eval_kernel', 'attn_core', 'im2col', 'channel_att', 'layernorm_kernel')
+
+
+def fam_of(name):
+    return next((f for f in FAMILIES if f in name), 'other')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('mfma_dir')
+    ap.add_argument('trace_dir')
+    ap.add_argument('--out', default=None)
+    a = ap.parse_args()
+    fn = glob.glob(os.path.join(a.mfma_dir, '**', '*counter_collection.csv'), recursive=True)[0]
+    per = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for r in csv.DictReader(open(fn, newline='')):
+        f = fam_of(r['Kernel_Name'])
+        per[f][r['Counter_Name']] += float(r['Counter_Value'])
+        disp[f].add(r.get('Dispatch_Id') or r.get('Correlation_Id'))
+    tfn = glob.glob(os.path.join(a.trace_dir, '**', '*kernel_stats.csv'), recursive=True)[0]
+    dur = defaultdict(lambda: [0, 0.0])
+    for r in csv.DictReader(open(tfn, newline='')):
+        f = fam_of(r['Name'])
+        dur[f][0] += int(r['Calls'])
+        dur[f][1] += float(r['TotalDurationNs'])
+    out = {}
+    for f, d in sorted(per.items()):
+        n = len(disp[f])
+        cyc = d.get('GRBM_GUI_ACTIVE', 0.0) / 8.0
+        busy = d.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0)
+        out[f] = {'dispatches': n, 'mfma_busy_cycles_per_launch': busy / max(n, 1),
+                  'gpu_cycles_per_launch': cyc / max(n, 1),
+                  'busy_frac': busy / (1024.0 * cyc) if cyc else None,
+                  'trace_avg_us': dur[f][1] / max(dur[f][0], 1) / 1e3 if f in dur else None}
+    txt = json.dumps(out, indent=1)
+    print(txt)
+    if a.out:
+        with open(a.out, 'w') as fh:
+            fh.write(txt)
+
+
+if __name__ == '__main__':
+    main()

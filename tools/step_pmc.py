@@ -1,0 +1,43 @@
+"""Runs exactly the bench step (bench.py configs[1]: HIP log-mel + SelfAttention_G eval over
+B synthetic clips, captured in one HIP graph) and nothing else, for PMC passes whose per-launch
+averages must describe the benched code: the two eager warm-up steps of bench.capture_step
+plus R graph replays, every dispatch a bench-step kernel.
+
+    rocprofv3 --pmc FETCH_SIZE -d DIR -- python tools/step_pmc.py [R] [--dtype bf16]
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, 'audio-to-motion-generation_amd'))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    reps = int(args[0]) if args else 3
+    dev = torch.device('cuda:0')
+    import a2m
+    a2m.set_gemm_precision('bf16' if '--dtype' in sys.argv and 'bf16' in sys.argv else 'fp32')
+    from a2m.real_motion_model import SelfAttention_G
+    B, T = 64, 64
+    torch.manual_seed(1234)
+    g = SelfAttention_G(time_steps=T, p=0.2)
+    for m in g.modules():
+        if hasattr(m, 'gamma'):
+            torch.nn.init.constant_(m.gamma, 0.3)
+    g = g.to(dev).eval()
+    wave = bench.synth_wave(B, (T - 1) * bench.HOP + bench.WIN, seed=0, device=dev)
+    with torch.no_grad():
+        graph, out = bench.capture_step(dev, bench.infer_step(g, wave))
+        for _ in range(reps):
+            graph.replay()
+    torch.cuda.synchronize()
+    print(f'step_pmc: 2 eager + {reps} graph steps, out {tuple(out.shape)}')
+
+
+if __name__ == '__main__':
+    main()
