@@ -155,131 +155,151 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------------------
 // Eval-only fusion of the q/k/v 1x1 convolutions into the core (no qkv / attention outputs
 // are kept for a backward pass): one workgroup per (clip, 64-channel chunk of V), C in
-// {128, 256}, T <= 64.  The clip's x [C][T] is staged once in LDS as [t][c]; the four waves
-// compute Q^T and K^T ([64 t][C/8], bias added; waves 0-1 / 2-3) and then this chunk's V
-// ([64 c][64 t]) with B / A fragments of the stacked weights read from L2, after which the
-// score / softmax / PV / epilogue steps are those of attn_core_kernel.  Q and K are
-// recomputed by each of the C/64 chunks of a clip (C/8 of the C + C/4 projection rows), which
-// costs less than the round trip of qkv through HBM and a second launch.
+// {128, 256}, T <= 64.  Step 1 is a pipelined GEMM P[t][col] = sum_c x[c][t] W[col][c] over
+// 128 columns = Q (C/8, zero-padded to 32) | K (same) | this chunk's 64 V rows: k-tiles of 32
+// channels of x ([t][c], transposed on the way in) and of the stacked weight rows are staged
+// through double-buffered LDS shared by eight waves (two per SIMD), one barrier per k-step,
+// global loads of the next tile in flight behind the current tile's MFMAs; each wave owns one
+// 32 x 32 block of P.  Then Q^T, K^T and the V chunk move to LDS and the score (waves 0-3) /
+// softmax / PV + epilogue (waves 4-7) steps of attn_core_kernel follow.  Q and K are
+// recomputed by each of the C/64 chunks of a clip (C/4 of the 5C/4 projection rows), which
+// costs less than a second launch and a round trip of qkv through memory.
 // ---------------------------------------------------------------------------------------
-constexpr int QP = 36;  // Q^T / K^T pitch (C/8 <= 32 columns): conflict-free b128 rows
+constexpr int QP = 36;        // Q^T / K^T pitch (32 columns): conflict-free b128 rows
+constexpr int FK = 32;        // projection k-tile (channels)
+constexpr int FKP = FK + 4;   // staged tile pitch
+constexpr int FCOLS = 128;    // projection output columns: Q 32 | K 32 | V 64
 
-// One lane's weight-row fragments for all of K = C <= 256 (k = 16 kc + 8 lh + s), loaded
-// into registers before the x tile is staged: the workgroup is alone on its CU (LDS-bound), so
-// the 128 VGPRs per row buy an MFMA loop with no L2 waits.
-constexpr int KC_MAX = 256 / 16;
-__device__ __forceinline__ void load_row_frags(float4 (&f)[KC_MAX][2], const float* row, int K, int lh) {
-#pragma unroll
-  for (int kc = 0; kc < KC_MAX; ++kc) {
-    if (kc * 16 < K) {
-      f[kc][0] = *reinterpret_cast<const float4*>(row + kc * 16 + lh * 8);
-      f[kc][1] = *reinterpret_cast<const float4*>(row + kc * 16 + lh * 8 + 4);
-    } else {
-      f[kc][0] = f[kc][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-}
-
-// acc += A[32 rows][K] (this lane's LDS row) . B[32 rows][K] (this lane's register fragments)
-__device__ __forceinline__ void mfma_lds_reg(floatx16& acc, const float* arow_lds,
-                                             const float4 (&f)[KC_MAX][2], int K, int lh) {
-#pragma unroll
-  for (int kc = 0; kc < KC_MAX; ++kc) {
-    if (kc * 16 >= K) break;
-    const float4 a0 = *reinterpret_cast<const float4*>(arow_lds + kc * 16 + lh * 8);
-    const float4 a1 = *reinterpret_cast<const float4*>(arow_lds + kc * 16 + lh * 8 + 4);
-    const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float bf[8] = {f[kc][0].x, f[kc][0].y, f[kc][0].z, f[kc][0].w,
-                         f[kc][1].x, f[kc][1].y, f[kc][1].z, f[kc][1].w};
-#pragma unroll
-    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
-  }
-}
-
-__global__ __launch_bounds__(256, 1) void attn_fused_eval_kernel(
+__global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
     const float* __restrict__ x, int64_t x_bs, int C, int T, const float* __restrict__ wqkv,
     const float* __restrict__ bqkv, const float* __restrict__ gamma, const float* __restrict__ res,
     float* __restrict__ y) {
-  constexpr int XP = 256 + 4;                                    // [t][c] pitch, C <= 256
-  __shared__ __attribute__((aligned(16))) float xs[AT * XP];     // x^T, later the scores
-  __shared__ __attribute__((aligned(16))) float qs[AT * QP];     // Q^T [i][c']
-  __shared__ __attribute__((aligned(16))) float ks[AT * QP];     // K^T [j][c']
-  __shared__ __attribute__((aligned(16))) float vs[ACH * AP];    // V chunk [c][j]
-  float* ss = xs;
+  constexpr int XT = AT * FKP, WTL = FCOLS * FKP, STG = XT + WTL;  // eight waves
+  // stages (2 x (x tile + w tile)) early; Q^T, K^T, V, scores overlay them afterwards
+  __shared__ __attribute__((aligned(16))) float lds[2 * STG];
+  float* qs = lds;                     // [i][c'] pitch QP
+  float* ks = qs + AT * QP;            // [j][c']
+  float* vs = ks + AT * QP;            // [c][j]  pitch AP
+  float* ss = vs + ACH * AP;           // [i][j]  pitch AP
+  static_assert(2 * AT * QP + 2 * ACH * AP <= 2 * STG, "overlay must fit the stages");
   const int b = blockIdx.y, c0 = blockIdx.x * ACH;
   const int Cq = C / 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
-  const int wm = wave >> 1, wn = wave & 1;
+  // projection: eight waves, wave (pt, pc) = (wave >> 2, wave & 3) owns t rows 32 pt.. and
+  // columns 32 pc.. (one accumulator; two waves per SIMD hide each other's LDS and barrier
+  // waits); attention steps: waves 0-3 as (wt, wc) = (wave >> 1, wave & 1)
+  const int pt = wave >> 2, pc = wave & 3;
+  const int wt = (wave & 3) >> 1, wc = wave & 1;
   const float* xb = x + (int64_t)b * x_bs;
-  // weight fragments first: this lane's Q/K projection row (c' = li) and V row (c0 + 32 wm + li)
-  float4 fqk[KC_MAX][2], fv[KC_MAX][2];
-  load_row_frags(fqk, wqkv + (int64_t)((wave >> 1) * Cq + li) * C, C, lh);
-  load_row_frags(fv, wqkv + (int64_t)(2 * Cq + c0 + wm * 32 + li) * C, C, lh);
 
-  {  // x [C][T] -> xs [t][c]: float4 along t, lanes along c (conflict-free LDS writes)
-    const int nq = C * (AT / 4);                                 // float4 slots of the tile
-    for (int base = 0; base < nq; base += 256 * 8) {
-      float4 v[8];
+  // staging maps.  x tile [t][c] from x[c][t]: thread -> (c = e % 32, t quad = e / 32), one
+  // float4 per thread, transposed writes conflict-free (32 lanes = 32 consecutive c).
+  // w tile [col][c]: stacked rows Q 0..Cq-1 -> cols 0.., K Cq.. -> 32.., V 2Cq + c0.. -> 64..;
+  // two float4 per thread along c.
+  float4 xr[1], wr[2];
+  int wrow[2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int e = base + tid + j * 256;
-        const int c = e % C, tq = e / C;
-        v[j] = (e < nq && 4 * tq < T) ? *reinterpret_cast<const float4*>(xb + (int64_t)c * T + 4 * tq)
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+  for (int u = 0; u < 2; ++u) {
+    const int col = (tid + u * 512) >> 3;
+    wrow[u] = col < 32 ? (col < Cq ? col : -1)
+                       : col < 64 ? (col - 32 < Cq ? Cq + col - 32 : -1) : 2 * Cq + c0 + col - 64;
+  }
+  auto load_tile = [&](int kt) {
+    const int cb = kt * FK;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int e = base + tid + j * 256;
-        if (e >= nq) continue;
-        const int c = e % C, tq = e / C;
-        xs[(4 * tq + 0) * XP + c] = v[j].x;
-        xs[(4 * tq + 1) * XP + c] = v[j].y;
-        xs[(4 * tq + 2) * XP + c] = v[j].z;
-        xs[(4 * tq + 3) * XP + c] = v[j].w;
+    for (int u = 0; u < 1; ++u) {
+      const int e = tid + u * 512, c = e & 31, tq = e >> 5;
+      xr[u] = 4 * tq < T ? *reinterpret_cast<const float4*>(xb + (int64_t)(cb + c) * T + 4 * tq)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kq = ((tid + u * 512) & 7) * 4;
+      wr[u] = wrow[u] >= 0 ? *reinterpret_cast<const float4*>(wqkv + (int64_t)wrow[u] * C + cb + kq)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_tile = [&](float* st) {
+    float* xs = st;
+    float* ws = st + XT;
+#pragma unroll
+    for (int u = 0; u < 1; ++u) {
+      const int e = tid + u * 512, c = e & 31, t = 4 * (e >> 5);
+      xs[(t + 0) * FKP + c] = xr[u].x;
+      xs[(t + 1) * FKP + c] = xr[u].y;
+      xs[(t + 2) * FKP + c] = xr[u].z;
+      xs[(t + 3) * FKP + c] = xr[u].w;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + u * 512;
+      *reinterpret_cast<float4*>(ws + (e >> 3) * FKP + (e & 7) * 4) = wr[u];
+    }
+  };
+
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int nk = C / FK;
+  load_tile(0);
+  store_tile(lds);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const float* cur = lds + (kt & 1) * STG;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    float af[2][8], bf[2][8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {  // both halves' fragments first
+      const float* ap = cur + (pt * 32 + li) * FKP + half * 16 + lh * 8;
+      const float* bp = cur + XT + (pc * 32 + li) * FKP + half * 16 + lh * 8;
+      const float4 a0 = *reinterpret_cast<const float4*>(ap), a1 = *reinterpret_cast<const float4*>(ap + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(bp), b1 = *reinterpret_cast<const float4*>(bp + 4);
+      af[half][0] = a0.x; af[half][1] = a0.y; af[half][2] = a0.z; af[half][3] = a0.w;
+      af[half][4] = a1.x; af[half][5] = a1.y; af[half][6] = a1.z; af[half][7] = a1.w;
+      bf[half][0] = b0.x; bf[half][1] = b0.y; bf[half][2] = b0.z; bf[half][3] = b0.w;
+      bf[half][4] = b1.x; bf[half][5] = b1.y; bf[half][6] = b1.z; bf[half][7] = b1.w;
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[half][s], bf[half][s], acc, 0, 0, 0);
+    if (kt + 1 < nk) store_tile(lds + ((kt + 1) & 1) * STG);
+    __syncthreads();
+  }
+
+  // projection outputs (+ bias) to LDS: acc[r] = P[t][col], t = 32 pt + (r&3) + 8 (r>>2) + 4 lh,
+  // col = 32 pc + li.  Q^T / K^T rows t (zero past Cq), V chunk rows c (zero past T)
+  {
+    const int col = pc * 32 + li;
+    float bias;
+    if (col < 64) {
+      const int cq = col & 31;
+      bias = cq < Cq ? bqkv[(col < 32 ? 0 : Cq) + cq] : 0.f;
+    } else {
+      bias = bqkv[2 * Cq + c0 + col - 64];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int t = pt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (col < 64) {
+        const int cq = col & 31;
+        (col < 32 ? qs : ks)[t * QP + cq] = cq < Cq ? acc[r] + bias : 0.f;
+      } else {
+        vs[(col - 64) * AP + t] = t < T ? acc[r] + bias : 0.f;
       }
     }
   }
   __syncthreads();
 
-  floatx16 acc;
-  // Q^T (waves 0, 1) and K^T (waves 2, 3): rows t = 32 (wave & 1) + li, columns c' < Cq = 32
-  {
+  // S[i][j] = sum_c' Q^T[i][c'] K^T[j][c']: waves 0-3, wave (wt, wc) owns the 32 x 32 tile
+  floatx16 sacc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const int proj = wave >> 1, t0 = (wave & 1) * 32;            // B row c' = li (Cq = 32)
-    mfma_lds_reg(acc, xs + (t0 + li) * XP, fqk, C, lh);
-    float* dst = proj ? ks : qs;
-    const float bias = bqkv[proj * Cq + li];
+  for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+  if (wave < 4) {
+    const int ia = wt * 32 + li, jb = wc * 32 + li;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int t = t0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      dst[t * QP + li] = acc[r] + bias;
-    }
-  }
-  // V chunk: rows c = 32 wm + li of [c0, c0 + 64), columns t = 32 wn + li
-  {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    // here A (weights) comes from L2 and B (x^T) from LDS: acc^T = B . A^T, so run the helper
-    // with the roles swapped and transpose on the way out
-    mfma_lds_reg(acc, xs + (wn * 32 + li) * XP, fv, C, lh);
-    // acc[r] = out(row = t: 32 wn + (r&3) + 8 (r>>2) + 4 lh, col = c: 32 wm + li)
-    const float bias = bqkv[2 * Cq + c0 + wm * 32 + li];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int t = wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      vs[(wm * 32 + li) * AP + t] = t < T ? acc[r] + bias : 0.f;
-    }
-  }
-  __syncthreads();  // Q, K, V in LDS; x^T dead (ss reuses it)
-
-  // S[i][j] = sum_c' Q^T[i][c'] K^T[j][c']
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  {
-    const int ia = wm * 32 + li, jb = wn * 32 + li;
-    for (int kc = 0; kc < Cq; kc += 16) {
+    for (int kc = 0; kc < 32; kc += 16) {
       const float4 a0 = *reinterpret_cast<const float4*>(qs + ia * QP + kc + lh * 8);
       const float4 a1 = *reinterpret_cast<const float4*>(qs + ia * QP + kc + lh * 8 + 4);
       const float4 b0 = *reinterpret_cast<const float4*>(ks + jb * QP + kc + lh * 8);
@@ -287,17 +307,19 @@ __global__ __launch_bounds__(256, 1) void attn_fused_eval_kernel(
       const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
       const float bf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+      for (int s = 0; s < 8; ++s) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], sacc, 0, 0, 0);
     }
   }
+  if (wave < 4) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int i = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-    ss[i * AP + wn * 32 + li] = acc[r];
+    for (int r = 0; r < 16; ++r) {
+      const int i = wt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      ss[i * AP + wc * 32 + li] = sacc[r];
+    }
   }
   __syncthreads();
 
-  {  // row softmax over j < T: four lanes per row, quad reductions in DPP
+  if (tid < 256) {  // row softmax over j < T: four lanes per row, quad reductions in DPP
     const int i = tid >> 2, part = tid & 3;
     float* rowp = ss + i * AP + part * 16;
     float e[16];
@@ -329,12 +351,14 @@ __global__ __launch_bounds__(256, 1) void attn_fused_eval_kernel(
   }
   __syncthreads();
 
-  // out[c][i] = sum_j V[c][j] A[i][j]
+  // out[c][i] = sum_j V[c][j] A[i][j]: waves 4-7, wave (wt, wc) owns channels 32 wt.., queries 32 wc..
+  if (wave < 4) return;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
   {
-    const int ca = wm * 32 + li, ib = wn * 32 + li;
+    const int ca = wt * 32 + li, ib = wc * 32 + li;
     for (int kc = 0; kc < AT; kc += 16) {
+      if (kc >= T) break;
       const float4 a0 = *reinterpret_cast<const float4*>(vs + ca * AP + kc + lh * 8);
       const float4 a1 = *reinterpret_cast<const float4*>(vs + ca * AP + kc + lh * 8 + 4);
       const float4 b0 = *reinterpret_cast<const float4*>(ss + ib * AP + kc + lh * 8);
@@ -342,18 +366,17 @@ __global__ __launch_bounds__(256, 1) void attn_fused_eval_kernel(
       const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
       const float bf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+      for (int s = 0; s < 8; ++s) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], sacc, 0, 0, 0);
     }
   }
   const float g = gamma[0];
-  const int i = wn * 32 + li;
+  const int i = wc * 32 + li;
   if (i < T) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int c = c0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      if (c >= C) continue;
+      const int c = c0 + wt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
       const int64_t o = (int64_t)b * x_bs + (int64_t)c * T + i;
-      float val = g * acc[r] + xb[(int64_t)c * T + i];
+      float val = g * sacc[r] + x[o];
       if (res) val += res[o];
       y[o] = val;
     }
@@ -550,7 +573,7 @@ int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const flo
                     const float* bqkv, const float* gamma, const float* res, float* y,
                     hipStream_t st) {
   dim3 grid((unsigned)cdiv(C, ACH), (unsigned)B);
-  hipLaunchKernelGGL(attn_fused_eval_kernel, grid, dim3(256), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
+  hipLaunchKernelGGL(attn_fused_eval_kernel, grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
                      res, y);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
