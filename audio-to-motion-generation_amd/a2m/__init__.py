@@ -13,18 +13,26 @@ __version__ = '0.1.0'
 
 def set_gemm_precision(dtype):
     """Operand precision of every GEMM-engine launch issued afterwards: 'fp32' (default, the
-    parity configuration) or 'bf16' (bf16 operands, fp32 accumulation, fp32 storage -- the
-    torch.autocast(dtype=torch.bfloat16)-equivalent of BASELINE configs[4]).  Returns the
-    previous setting.  HIP graphs keep the precision they were captured with."""
-    prev = 'bf16' if _native.lib.a2m_get_gemm_precision() else 'fp32'
+    parity configuration: v_mfma_f32_32x32x2_f32), 'bf16' (bf16 operands, fp32 accumulation,
+    fp32 storage -- the torch.autocast(dtype=torch.bfloat16)-equivalent of BASELINE configs[4])
+    or 'bf16x6' (fp32 operands split exactly into three bf16 pieces on their way into LDS, the
+    six products of order >= 2^-16 accumulated in fp32 on the bf16 MFMA: fp32-class results at
+    16/6 of the f32 MFMA rate).  Returns the previous setting.  HIP graphs keep the precision
+    they were captured with."""
+    prev = _PREC_NAMES[_native.lib.a2m_get_gemm_precision()]
     if dtype in ('bf16', torch.bfloat16):
         flag = 1
     elif dtype in ('fp32', torch.float32):
         flag = 0
+    elif dtype == 'bf16x6':
+        flag = 2
     else:
-        raise ValueError(f'unsupported GEMM precision {dtype!r} (fp32 or bf16)')
+        raise ValueError(f'unsupported GEMM precision {dtype!r} (fp32, bf16 or bf16x6)')
     _native.check(_native.lib.a2m_set_gemm_precision(flag))
     return prev
+
+
+_PREC_NAMES = ('fp32', 'bf16', 'bf16x6')
 
 
 class gemm_precision:

@@ -76,9 +76,36 @@ def _bn_args(bn):
 
 
 # ------------------------------------------------------------------------------ convs
-def conv1d(x, w, b=None, stride=1, pad=0, bn=None, act=ACT_NONE, slope=0.2, out=None):
+_TAP_CONV = __import__('os').environ.get('A2M_TAP_CONV', '1') != '0'
+
+
+def _tap_eligible(x, ks, stride, pad, Ci):
+    T = x.shape[2]
+    return (_TAP_CONV and ks > 1 and stride == 1 and 2 * pad == ks - 1 and x.stride(2) == 1 and
+            T % 4 == 0 and 64 % T == 0 and pad < T and x.data_ptr() % 16 == 0 and
+            (x.stride(0) % 4 == 0 or x.shape[0] == 1) and x.stride(1) % 4 == 0)
+
+
+def conv1d_tap_packed(w, cache=None):
+    """Tap-chunked conv1d weights [Co][Ci/chunk][k][chunk] for the engine's current k-tile
+    (a2m_conv1d_tap_pack_f32), cached in `cache` per weight version and chunk."""
+    chunk = N.lib.a2m_conv1d_tap_chunk()
+    key = _wkey((w,)) + (chunk,)
+    if cache is not None and cache.get('key') == key:
+        return cache['w'], chunk
+    Co, Ci, ks = w.shape
+    packed = torch.empty(Co * Ci * ks, device=w.device)
+    N.check(N.lib.a2m_conv1d_tap_pack_f32(_p(w), Co, Ci, ks, chunk, _p(packed), _stream()))
+    if cache is not None:
+        cache.update(key=key, w=packed)
+    return packed, chunk
+
+
+def conv1d(x, w, b=None, stride=1, pad=0, bn=None, act=ACT_NONE, slope=0.2, out=None, cache=None):
     """x: [B, Ci, Tin] (any strides), w: [Co, Ci, k] (or [Co, Ci] for a linear / 1x1).
-    Returns / fills out [B, Co, Tout] (any strides)."""
+    Returns / fills out [B, Co, Tout] (any strides).  With `cache` (a dict owned by the module),
+    stride-1 same-padded convs over clips that tile the GEMM's 64 rows run on the tap-chunked
+    path (a2m_conv1d_tap_fwd_f32: no im2col matrix; packed weights kept in `cache`)."""
     _check_dev(x, w, b, out)
     B, Ci, Tin = x.shape
     Co, ks = w.shape[0], (w.shape[2] if w.dim() == 3 else 1)
@@ -90,6 +117,13 @@ def conv1d(x, w, b=None, stride=1, pad=0, bn=None, act=ACT_NONE, slope=0.2, out=
     xs, ys = list(x.stride()), list(out.stride())
     if B == 1:  # batch stride is irrelevant; make single-batch row views look uniform
         xs[0], ys[0] = Tin * xs[2], Tout * ys[2]
+    if cache is not None and _tap_eligible(x, ks, stride, pad, Ci) and \
+            Ci % N.lib.a2m_conv1d_tap_chunk() == 0:
+        packed, chunk = conv1d_tap_packed(w, cache)
+        _with_ws(x.device, lambda wp, wn: N.lib.a2m_conv1d_tap_fwd_f32(
+            _p(x), xs[0], xs[1], B, Ci, Tin, _p(packed), chunk, _p(b), Co, ks, pad,
+            *_bn_args(bn), act, slope, _p(out), ys[0], ys[1], ys[2], wp, wn, _stream()))
+        return out
     _with_ws(x.device, lambda wp, wn: N.lib.a2m_conv1d_fwd_f32(
         _p(x), xs[0], xs[1], xs[2], B, Ci, Tin, _p(w), _p(b), Co, ks, stride, pad,
         *_bn_args(bn), act, slope, _p(out), ys[0], ys[1], ys[2], wp, wn, _stream()))

@@ -86,6 +86,7 @@ class ConvNormRelu(nn.Module):
         self.type = type
         self.leaky = leaky
         self.p = p
+        self._tap = {}   # tap-chunked weights for the eval path (functional.conv1d_tap_packed)
         if type == '1d':
             self.conv = nn.Conv1d(in_channels, out_channels, kernel_size, stride, padding)
             self.norm = nn.BatchNorm1d(out_channels)
@@ -117,7 +118,7 @@ class ConvNormRelu(nn.Module):
         k, s, p = self.geometry()
         if self.type == '1d':
             return F.conv1d(x, self.conv.weight, self.conv.bias, s, p, bn=self.bn_eval(),
-                            act=self.act, out=out)
+                            act=self.act, out=out, cache=self._tap)
         return F.conv2d(x, self.conv.weight, self.conv.bias, s, tuple(p), bn=self.bn_eval(),
                         act=self.act, cols=cols, out=out)
 

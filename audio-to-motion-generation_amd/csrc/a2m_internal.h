@@ -60,6 +60,10 @@ struct Gather {
   int ar1, ar2, bk1, bk2, ch, cw;
   int divh, divw, Lh, Lw;
   int kcontig;  // 1: consecutive k are (usually) adjacent in memory -> k-major thread map
+  int tapconv;  // > 0: stride-1 conv1d operand in tap-chunked k order (loader mode 5): k =
+                // (chunk, tap, ci) with BK-channel chunks, rows n = b*R2 + t; the chunk's
+                // x[b][c][t] window is loaded once and re-stored shifted for each of the
+                // `tapconv` taps (sr0 = batch stride, sk0 = channel stride, cw = -pad)
 };
 
 inline Gather dense_rk(const float* p, int ld, int64_t bstride = 0) {  // [R][K] row-major, ld >= K
@@ -103,6 +107,8 @@ inline Epilogue epi_dense(float* out, int ldn, int64_t bstride = 0) {  // out[m]
 
 // Runs C = A . B^T-style implicit GEMM: C[m][n] = sum_k A(m,k) * B(n,k), over `batch`
 // independent problems (grid z), with optional split-K through workspace `ws`.
+// k-tile depth of the engine at the current precision (the chunk of tap-chunked conv weights)
+int gemm_k_tile();
 int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int K, int batch,
          void* ws, size_t ws_bytes, hipStream_t stream, int force_split = 0);
 size_t gemm_ws_bytes(int M, int N, int K, int batch);

@@ -124,6 +124,7 @@ static int env_int(const char* name, int dflt) {
 }
 
 static int operand_mode(const Gather& g, int K) {
+  if (g.tapconv > 0) return 5;
   if (!g.kcontig) {
     // rows 4-at-a-time contiguous: plain [K][R] (rows via r0, unit stride), or stride-1 im2col
     // rows along w (R2 % 4 == 0) or along h (R2 == 1, R1 % 4 == 0), unit element stride
@@ -163,9 +164,13 @@ struct Plan {
 // a2m_gemm_plan_override and A2M_GEMM_XCD=g override (experiments).
 // Operand precision of the engine: 0 = fp32 (v_mfma_f32_32x32x2_f32, BK 32; the default and
 // the parity configuration), 1 = bf16 (operands rounded to bf16 in LDS, fp32 accumulation,
-// BK 64; a2m_set_gemm_precision, configs[4]).  (BK = 16 measured slower end to end.)
-static int g_gemm_bf16 = 0;
-static int gemm_bk(bool bf16) { return bf16 ? 64 : 32; }
+// BK 64; a2m_set_gemm_precision, configs[4]), 2 = bf16x6 (fp32 operands split exactly into
+// three bf16 planes in LDS, the six products of order >= 2^-16 on v_mfma_f32_32x32x16_bf16 with
+// fp32 accumulation: fp32-class accuracy at 16/6 of the f32 MFMA rate; BK 32).
+// (BK = 16 measured slower end to end.)
+static int g_gemm_prec = 0;
+static int gemm_bk(int prec) { return prec == 1 ? 64 : 32; }
+int gemm_k_tile() { return gemm_bk(g_gemm_prec); }
 
 static int gemm_xcd_group() {
   static const int g = env_int("A2M_GEMM_XCD", 0);
@@ -175,41 +180,49 @@ static int gemm_xcd_group() {
 static int g_override_tile = 0, g_override_split = 0;   // a2m_gemm_plan_override (tuning)
 
 static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int tile, int kchunk,
-                           int splits, bool bf16) {
+                           int splits, int prec) {
   static const double thr64[4] = {340e3, 428e3, 435e3, 440e3};   // flop / us per CU
   static const double thr128[2] = {464e3, 500e3};
-  const int occ = tile == 128 ? 2 : 4;
+  // bf16x6 (fitted to a plan sweep of the G forward's shapes, tools/sweep_summary.py): three
+  // bf16 planes per operand halve the resident blocks (LDS: 61 KB at 64x64, 120 KB at
+  // 128x128) and the 128x128 tile gains most from the faster MFMA
+  static const double x6_thr64[2] = {272e3, 342e3};
+  static const double x6_thr128[1] = {557e3};
+  const int occ = prec == 2 ? (tile == 128 ? 1 : 2) : (tile == 128 ? 2 : 4);
   const int64_t tiles = cdiv(M, tile) * cdiv(N, tile) * (int64_t)batch;
   const int64_t per_cu = cdiv(tiles * splits, 256);
   const int c = (int)std::min<int64_t>(per_cu, occ);
-  double thr = tile == 128 ? thr128[c - 1] : thr64[c - 1];
+  double thr = prec == 2 ? (tile == 128 ? x6_thr128[c - 1] : x6_thr64[c - 1])
+                         : (tile == 128 ? thr128[c - 1] : thr64[c - 1]);
   if (gathered && tile == 64) thr *= 0.84;
-  if (bf16) thr *= 4.0;  // staging-bound rather than MFMA-bound (16x MFMA rate); rough
+  if (prec == 1) thr *= 4.0;  // staging-bound rather than MFMA-bound (16x MFMA rate); rough
   const double block_flops = 2.0 * tile * tile * (double)kchunk;
-  const double fixed = tile == 128 ? (gathered ? 16.0 : 10.0) : 3.0;
+  const double fixed = prec == 2 ? (tile == 128 ? 15.0 : 2.0)
+                                 : (tile == 128 ? (gathered ? 16.0 : 10.0) : 3.0);
   double t = per_cu * block_flops / thr + cdiv(per_cu, occ) * fixed + 4.0;
   if (splits > 1) t += (splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0;
   return t;
 }
 
-static Plan plan_for(int M, int N, int K, int batch, bool gathered, bool bf16) {
+static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, int kquant = 1) {
   static const int env_tile = env_int("A2M_GEMM_TILE", 0);
   static const int env_split = env_int("A2M_GEMM_SPLIT", 0);
   const int force_tile = g_override_tile ? g_override_tile : env_tile;
   const int force_split = g_override_split ? g_override_split : env_split;
-  const int BK = gemm_bk(bf16);
+  const int BK = gemm_bk(prec);
+  const int KQ = BK * kquant;   // split boundaries on whole k-tile groups (mode 5: all taps of a chunk)
   static const int cand_splits[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256};
-  Plan p{64, BK, 1, (int)(cdiv(std::max(K, 1), BK) * BK)};
+  Plan p{64, BK, 1, (int)(cdiv(std::max(K, 1), KQ) * KQ)};
   double best = 1e300;
   for (int tile : {64, 128}) {
     if (force_tile && tile != force_tile) continue;
     for (int s : cand_splits) {
       if (force_split && s != force_split) continue;
-      const int kchunk = (int)(cdiv(cdiv(std::max(K, 1), s), BK) * BK);
+      const int kchunk = (int)(cdiv(cdiv(std::max(K, 1), s), KQ) * KQ);
       const int se = (int)cdiv(std::max(K, 1), kchunk);
       if (!force_split && se > 1 && kchunk < 128) continue;
       if (se != s && s > 1 && !force_split) continue;   // the same plan at a smaller s
-      const double t = plan_cost_us(M, N, K, batch, gathered, tile, kchunk, se, bf16);
+      const double t = plan_cost_us(M, N, K, batch, gathered, tile, kchunk, se, prec);
       if (t < best) {
         best = t;
         p.bm = tile;
@@ -220,7 +233,7 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered, bool bf16) {
   }
   if (force_split && best == 1e300) {   // a forced split outside the candidate list
     p.bm = force_tile ? force_tile : 64;
-    p.kchunk = (int)(cdiv(cdiv(std::max(K, 1), force_split), BK) * BK);
+    p.kchunk = (int)(cdiv(cdiv(std::max(K, 1), force_split), KQ) * KQ);
     p.splits = (int)cdiv(std::max(K, 1), p.kchunk);
   }
   return p;
@@ -231,8 +244,8 @@ size_t gemm_ws_bytes(int M, int N, int K, int batch) {
   // either precision
   size_t need = 0;
   for (bool gathered : {false, true})
-    for (bool bf16 : {false, true}) {
-      const Plan p = plan_for(M, N, K, batch, gathered, bf16);
+    for (int prec : {0, 1, 2}) {
+      const Plan p = plan_for(M, N, K, batch, gathered, prec);
       if (p.splits > 1) need = std::max(need, (size_t)p.splits * batch * M * N * sizeof(float));
     }
   return need;
@@ -284,10 +297,11 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   GemmArgs a;
   a.A = A; a.B = B; a.E = E; a.M = M; a.N = N; a.K = K;
   const int ma = operand_mode(A, K), mb = operand_mode(B, K);
-  const bool bf16 = g_gemm_bf16 != 0;
-  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || mb == 3, bf16);
+  const int prec = g_gemm_prec;
+  const int kquant = mb == 5 ? B.tapconv : 1;
+  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || mb >= 3, prec, kquant);
   if (force_split > 0) {
-    p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk) * p.bk);
+    p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk * kquant) * p.bk * kquant);
     p.splits = (int)cdiv(K, p.kchunk);
   }
   if (K == 0) { p.splits = 1; p.kchunk = p.bk; }
@@ -316,16 +330,19 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                   batch, p.bm, p.splits, ma, mb);
     tm = timing_open(2.0 * M * N * (double)K * batch, desc, stream);
   }
-  if (bf16) {
-    if (p.bm == 128) launch_tile<128, 128, 64, true>(a, ma, mb, batch, stream);
-    else launch_tile<64, 64, 64, true>(a, ma, mb, batch, stream);
+  if (prec == 1) {
+    if (p.bm == 128) launch_tile<128, 128, 64, 1>(a, ma, mb, batch, stream);
+    else launch_tile<64, 64, 64, 1>(a, ma, mb, batch, stream);
+  } else if (prec == 2) {
+    if (p.bm == 128) launch_tile<128, 128, 32, 2>(a, ma, mb, batch, stream);
+    else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
   } else {
     static const int ks2 = env_int("A2M_GEMM_KS2", 1);
-    if (p.bm == 128) launch_tile<128, 128, 32, false>(a, ma, mb, batch, stream);
+    if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
     // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end
-    else if (ks2 && ma == 0 && mb == 0) launch_tile<64, 64, 32, false, 2>(a, ma, mb, batch, stream);
-    else launch_tile<64, 64, 32, false>(a, ma, mb, batch, stream);
+    else if (ks2 && ma == 0 && mb == 0) launch_tile<64, 64, 32, 0, 2>(a, ma, mb, batch, stream);
+    else launch_tile<64, 64, 32, 0>(a, ma, mb, batch, stream);
   }
   A2M_LAUNCH_CHECK();
   if (tm >= 0) timing_mark(tm, 1, false, stream);
@@ -358,13 +375,13 @@ int a2m_gemm_plan_override(int32_t tile, int32_t splits) {
   return A2M_OK;
 }
 
-int a2m_set_gemm_precision(int32_t bf16) {
-  A2M_CHECK_ARG(bf16 == 0 || bf16 == 1, "set_gemm_precision: %d (0 = fp32, 1 = bf16)", bf16);
-  a2m::g_gemm_bf16 = bf16;
+int a2m_set_gemm_precision(int32_t prec) {
+  A2M_CHECK_ARG(prec >= 0 && prec <= 2, "set_gemm_precision: %d (0 = fp32, 1 = bf16, 2 = bf16x6)", prec);
+  a2m::g_gemm_prec = prec;
   return A2M_OK;
 }
 
-int32_t a2m_get_gemm_precision(void) { return a2m::g_gemm_bf16; }
+int32_t a2m_get_gemm_precision(void) { return a2m::g_gemm_prec; }
 
 int a2m_gemm_timing_begin(void) {
   std::lock_guard<std::mutex> lk(a2m::g_timing_mu);

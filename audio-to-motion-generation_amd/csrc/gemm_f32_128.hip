@@ -1,7 +1,7 @@
-// Instantiation of the GEMM engine's launch_tile<128, 128, 32, false> (one translation unit per tile
+// Instantiation of the GEMM engine's launch_tile<128, 128, 32, 0> (one translation unit per tile
 // configuration so the kernels compile in parallel).
 #include "gemm_kernel.h"
 
 namespace a2m {
-template void launch_tile<128, 128, 32, false>(const GemmArgs&, int, int, int, hipStream_t);
+template void launch_tile<128, 128, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
 }  // namespace a2m

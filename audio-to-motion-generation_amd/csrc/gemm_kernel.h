@@ -123,11 +123,17 @@ typedef float float4u __attribute__((ext_vector_type(4), aligned(4)));
 //           (A2M_M3_TRANSPOSE, default) or kept k-major with ds_read_b32 fragments.
 //   MODE 4: k-contiguous runs (the inner k digit has unit stride, K2 % 4 == 0: wgrad operands
 //           over [B][C][T]) loaded 4 k at a time, LDS [row][k].
+//   MODE 5: stride-1 conv1d over [B][C][T] in tap-chunked k order (k-tile j = chunk j / ntap,
+//           tap j % ntap; Gather::tapconv): the chunk's x[b][c0..c0+BK)[t] rows are loaded as
+//           float4 along t once (tap 0) and stored transposed, shifted by tap - pad within each
+//           clip, for every tap -- the im2col operand without its 3x global traffic.  Tiles
+//           hold whole clips (BR % T == 0) so the shift wraps inside the tile (wrapped rows = 0).
 #ifndef A2M_M3_TRANSPOSE
 #define A2M_M3_TRANSPOSE 1
 #endif
-template <int BR, int BK, int MODE, bool H = false>
+template <int BR, int BK, int MODE, int P = 0>
 struct TileLoader {
+  static constexpr bool H = P != 0;   // bf16 LDS image (P = 1 one plane, P = 2 three planes)
   // MODE 3 with A2M_M3_TRANSPOSE: the float4 of 4 rows is written as 4 scalars into the
   // [row][k] layout (lanes spread over k so the writes stay conflict-free), and fragments are
   // the same two ds_read_b128 as the other modes.
@@ -136,7 +142,9 @@ struct TileLoader {
   // 36 dwords for BK = 64 so the ds_read_b128 fragments stay conflict-free)
   static constexpr int LDK = H ? BK + 8 : BK + 4;
   static constexpr int LDR = BR + 4;                // [k][row] pitch: 8*LDR = 32 mod 64 banks
-  static constexpr int TILE = KMAJ ? BK * LDR : (H ? BR * LDK / 2 : BR * LDK);  // in floats
+  static constexpr int PLANE = BR * LDK;             // bf16 plane size in halves (P >= 1)
+  static constexpr int NPLANE = P == 2 ? 3 : 1;      // bf16 planes (hi / mid / lo for P = 2)
+  static constexpr int TILE = KMAJ ? BK * LDR : (H ? NPLANE * BR * LDK / 2 : BR * LDK);  // in floats
   static constexpr int QPR = BK / 4;                // k-major maps: float4 quads per row
   static constexpr int RPP = 256 / QPR;             //   rows per pass
   static constexpr int NPASS = BR / RPP;
@@ -145,16 +153,30 @@ struct TileLoader {
   static constexpr int QR = BR / 4;                 // mode 3: float4 row groups per k
   static constexpr int KPP = 256 / QR;              //   k per pass
   static constexpr int NP3 = BK / KPP;
+  // bf16 images of the row-vector modes (3, 5) use a k-pair map: each thread loads the float4
+  // row groups of two adjacent k and writes each row's pair as one 32-bit LDS store per plane
+  // (not 2-byte stores); the lanes of a wave hit 16 k-pairs x 4 row groups, conflict-free
+  static constexpr bool PAIR = H && (MODE == 3 || MODE == 5);
+  static constexpr int NKE = PAIR ? BK / KPP : NP3;   // k entries (a float4 of 4 rows each)
+  static constexpr int NPP = BK / (2 * KPP);          // pair map: passes
+  // k offset (relative to kq) of k entry e
+  __device__ __forceinline__ static constexpr int eofs(int e) {
+    return PAIR ? (e >> 1) * 2 * KPP + (e & 1) : e * KPP;
+  }
   const Gather* g;
   const float* base;
   int K;
-  RowInfo ri[MODE == 2 || MODE == 3 ? 1 : NPASS];
-  int lrow[MODE == 2 || MODE == 3 ? 1 : NPASS];
+  RowInfo ri[MODE == 2 || MODE >= 3 ? 1 : NPASS];
+  int lrow[MODE == 2 || MODE >= 3 ? 1 : NPASS];
   int kq;  // k offset of this thread inside the tile
   int nrow;  // mode 3: rows of this group that exist (0..4)
   int rdim;   // mode 3: 0 rows via r0, 1 rows along h, 2 rows along w
   int rstep;  // mode 3: element step between consecutive rows (1, or 2 for stride-2 convs)
-  static constexpr int NKP = MODE == 3 ? NP3 : 1;
+  static constexpr int NKP = MODE == 3 ? NKE : 1;
+  // mode 5
+  int tt;        // t of this thread's first row within its clip
+  int64_t rb;    // element offset of (b, t) of that row
+  int st_j;      // k-tile index of the next store (its tap)
   KPos kp[NKP];   // k position of each of this thread's k groups at the next load (modes 1-3)
   KPos kstep;     // BK in (k0, k1, k2) digits
   float r[NREG];
@@ -164,13 +186,27 @@ struct TileLoader {
     g = &gg;
     base = gg.base + (int64_t)z * gg.bstride;
     K = KK;
+    if (MODE == 5) {
+      lrow[0] = (tid / KPP) * 4;
+      kq = (tid % KPP) * (PAIR ? 2 : 1);
+      // rows past R still get their true t (tiles hold whole clips, so the shifted stores of
+      // an invalid group stay inside its own clip-sized span of the tile); only the address
+      // of the (unused) load is clamped
+      const int n = row0 + lrow[0];
+      nrow = min(4, max(0, R - n));
+      const int b = n / gg.R2;
+      tt = n - b * gg.R2;
+      rb = nrow > 0 ? (int64_t)b * gg.sr0 + tt : 0;
+      st_j = kbeg / BK;
+      return;
+    }
     if (MODE == 3) {
       if (KMAJ) {
         lrow[0] = (tid % QR) * 4;
         kq = tid / QR;
       } else {
         lrow[0] = (tid / KPP) * 4;
-        kq = tid % KPP;
+        kq = (tid % KPP) * (PAIR ? 2 : 1);
       }
       ri[0] = row_info(gg, row0 + lrow[0], R);
       nrow = min(4, max(0, R - (row0 + lrow[0])));
@@ -191,11 +227,27 @@ struct TileLoader {
     if (MODE != 0) {
       kstep = kpos(gg, kstride);
 #pragma unroll
-      for (int p = 0; p < NKP; ++p) kp[p] = kpos(gg, kbeg + kq + (MODE == 3 ? p * KPP : 0));
+      for (int p = 0; p < NKP; ++p) kp[p] = kpos(gg, kbeg + kq + (MODE == 3 ? eofs(p) : 0));
     }
   }
 
   __device__ __forceinline__ void load(int k0) {
+    if (MODE == 5) {
+      const int j = k0 / BK, cc = j / g->tapconv;
+      if (j - cc * g->tapconv != 0) return;   // taps 1.. re-store the registers of tap 0
+#pragma unroll
+      for (int p = 0; p < NKE; ++p) {
+        const float* src = base + rb + (int64_t)(cc * BK + kq + eofs(p)) * g->sk0;
+        if (nrow == 4) {
+          const float4u u = *reinterpret_cast<const float4u*>(src);
+          r[p * 4 + 0] = u.x; r[p * 4 + 1] = u.y; r[p * 4 + 2] = u.z; r[p * 4 + 3] = u.w;
+        } else {
+#pragma unroll
+          for (int j2 = 0; j2 < 4; ++j2) r[p * 4 + j2] = j2 < nrow ? src[j2] : 0.f;
+        }
+      }
+      return;
+    }
     if (MODE == 0) {
 #pragma unroll
       for (int p = 0; p < NPASS; ++p) {
@@ -261,7 +313,7 @@ struct TileLoader {
       // elements are consecutive floats (rstep 1) or every other float (stride-2 convs).
       const int dh = rdim == 1 ? rstep : 0, dw = rdim == 2 ? rstep : 0;
 #pragma unroll
-      for (int p = 0; p < NP3; ++p) {
+      for (int p = 0; p < NKE; ++p) {
         const KPos q = kp[p];
         kadd(*g, kp[p], kstep);
         int h = ri[0].h + q.k1 * g->bk1;
@@ -297,14 +349,72 @@ struct TileLoader {
     }
   }
 
-  __device__ __forceinline__ void store(float* lds) const {
-    if constexpr (H) {  // round to bf16 (RNE) on the way into LDS
-      __bf16* hl = reinterpret_cast<__bf16*>(lds);
-      if (MODE == 3) {
+  // mode 5: the row (within the tile) that element e of this thread's 4-row group lands on for
+  // the shift s = tap - pad, and whether it carries data (rows whose source t + s leaves the
+  // clip take 0, written by the element that wraps onto them)
+  __device__ __forceinline__ int row5(int e, int s, bool& ok) const {
+    const int ts = tt + e;
+    int td = ts - s;
+    const int T = g->R2;
+    ok = td >= 0 && td < T;
+    td += td < 0 ? T : (td >= T ? -T : 0);
+    return lrow[0] + e + (td - ts);
+  }
+
+  __device__ __forceinline__ void store(float* lds) {
+    if constexpr (MODE == 5) {
+      const int tap = st_j % g->tapconv;
+      ++st_j;
+      const int s = tap + g->cw;   // cw = -pad
+      if constexpr (H) {
+#pragma unroll
+        for (int pp = 0; pp < NPP; ++pp)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bool ok;
+            const int o = row5(e, s, ok) * LDK + kq + pp * 2 * KPP;
+            store_pair(lds, o, ok ? r[(2 * pp) * 4 + e] : 0.f, ok ? r[(2 * pp + 1) * 4 + e] : 0.f);
+          }
+      } else {
 #pragma unroll
         for (int p = 0; p < NP3; ++p)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) hl[(lrow[0] + j) * LDK + kq + p * KPP] = (__bf16)r[p * 4 + j];
+          for (int e = 0; e < 4; ++e) {
+            bool ok;
+            const int o = row5(e, s, ok) * LDK + kq + p * KPP;
+            lds[o] = ok ? r[p * 4 + e] : 0.f;
+          }
+      }
+      return;
+    }
+    if constexpr (P == 2) {  // three-way bf16 split (hi + mid + lo == v) on the way into LDS
+      __bf16* hl = reinterpret_cast<__bf16*>(lds);
+      if (MODE == 3) {
+        store_pairs3(lds);
+      } else if (MODE == 2) {
+#pragma unroll
+        for (int j = 0; j < KPT; j += 4) {
+          uint2 q[3];
+          split4(&r[j], q);
+          const int o = lrow[0] * LDK + kq + j;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) *reinterpret_cast<uint2*>(hl + c * PLANE + o) = q[c];
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < NPASS; ++p) {
+          uint2 q[3];
+          split4(&r[p * 4], q);
+          const int o = lrow[p] * LDK + kq;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) *reinterpret_cast<uint2*>(hl + c * PLANE + o) = q[c];
+        }
+      }
+      return;
+    } else if constexpr (H) {  // round to bf16 (RNE) on the way into LDS
+      __bf16* hl = reinterpret_cast<__bf16*>(lds);
+      if (MODE == 3) {
+        store_pairs3(lds);
       } else if (MODE == 2) {
         __bf16* dst = hl + lrow[0] * LDK + kq;
 #pragma unroll
@@ -347,9 +457,69 @@ struct TileLoader {
                           ((uint32_t)__builtin_bit_cast(uint16_t, d) << 16));
   }
 
-  // bf16: the 8 k-values k = 16*sub + 8*lh + s of tile row `row` (one ds_read_b128)
-  __device__ __forceinline__ static bf16x8 hfrag(const float* lds, int row, int sub, int lh) {
-    const __bf16* q = reinterpret_cast<const __bf16*>(lds) + row * LDK + sub * 16 + lh * 8;
+  // Three-way split of an fp32 value: hi = rne_bf16(v), mid = rne_bf16(v - hi),
+  // lo = rne_bf16(v - hi - mid).  Both differences are exact in fp32 (each removes the leading
+  // 8 significant bits), so hi + mid + lo == v for every finite v whose pieces stay normal, and
+  // |mid| <= 2^-8 |v|, |lo| <= 2^-16 |v|.
+  __device__ __forceinline__ static void split3(float v, __bf16* o) {
+    const __bf16 h = (__bf16)v;
+    const float r1 = v - (float)h;
+    const __bf16 m = (__bf16)r1;
+    o[0] = h;
+    o[1] = m;
+    o[2] = (__bf16)(r1 - (float)m);
+  }
+  // split3 of two values at once, each piece as a packed bf16 pair (v_cvt_pk_bf16_f32 and
+  // v_pk_add_f32 do both lanes: ~9 instructions per pair)
+  __device__ __forceinline__ static void split_pair(float a, float b, uint32_t* q) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+    const f2 v = {a, b};
+    const uint32_t hu = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h2));
+    const f2 hf = {__builtin_bit_cast(float, hu << 16), __builtin_bit_cast(float, hu & 0xffff0000u)};
+    const f2 r1 = v - hf;
+    const uint32_t mu = __builtin_bit_cast(uint32_t, __builtin_convertvector(r1, h2));
+    const f2 mf = {__builtin_bit_cast(float, mu << 16), __builtin_bit_cast(float, mu & 0xffff0000u)};
+    const f2 r2 = r1 - mf;
+    q[0] = hu;
+    q[1] = mu;
+    q[2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, h2));
+  }
+  __device__ __forceinline__ static void split4(const float* v, uint2* q) {
+    uint32_t a[3], b[3];
+    split_pair(v[0], v[1], a);
+    split_pair(v[2], v[3], b);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) q[c] = make_uint2(a[c], b[c]);
+  }
+  // one k-pair of one row into the bf16 image(s) at half offset o (o even)
+  __device__ __forceinline__ static void store_pair(float* lds, int o, float v0, float v1) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(lds);
+    if constexpr (P == 2) {
+      uint32_t q[3];
+      split_pair(v0, v1, q);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) w[(c * PLANE + o) >> 1] = q[c];
+    } else {
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+      const f2 v = {v0, v1};
+      w[o >> 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h2));
+    }
+  }
+  // mode 3, bf16 images: the k-pair map's row groups
+  __device__ __forceinline__ void store_pairs3(float* lds) const {
+#pragma unroll
+    for (int pp = 0; pp < NPP; ++pp)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        store_pair(lds, (lrow[0] + j) * LDK + kq + pp * 2 * KPP, r[(2 * pp) * 4 + j],
+                   r[(2 * pp + 1) * 4 + j]);
+  }
+
+  // bf16: the 8 k-values k = 16*sub + 8*lh + s of tile row `row` (one ds_read_b128) of plane c
+  __device__ __forceinline__ static bf16x8 hfrag(const float* lds, int row, int sub, int lh, int c = 0) {
+    const __bf16* q = reinterpret_cast<const __bf16*>(lds) + c * PLANE + row * LDK + sub * 16 + lh * 8;
     return *reinterpret_cast<const bf16x8*>(q);
   }
 
@@ -404,21 +574,33 @@ __device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int
 // The next tile's first fragments are read while this tile's second half is on the matrix
 // pipe, so no LDS latency sits between k-steps.  LDS[(i+1)&1] is free at the start of step i:
 // its last reads (tile i-1, half 1) preceded step i-1's barrier.
-template <int TM, int TN, bool H>
+template <int TM, int TN, int P>
 struct Frags;
 template <int TM, int TN>
-struct Frags<TM, TN, false> {  // fp32: 16 k per half, 8 per lane
+struct Frags<TM, TN, 0> {  // fp32: 16 k per half, 8 per lane
   float a[TM][8], b[TN][8];
 };
 template <int TM, int TN>
-struct Frags<TM, TN, true> {   // bf16: 32 k per half = two K16 chunks, 8 per lane each
+struct Frags<TM, TN, 1> {   // bf16: 32 k per half = two K16 chunks, 8 per lane each
   bf16x8 a[TM][2], b[TN][2];
 };
+template <int TM, int TN>
+struct Frags<TM, TN, 2> {   // bf16x6: 16 k per half (one K16 chunk), the three planes
+  bf16x8 a[TM][3], b[TN][3];
+};
 
-template <int BM, int BN, int TM, int TN, bool H, class LA, class LB>
+template <int BM, int BN, int TM, int TN, int P, class LA, class LB>
 __device__ __forceinline__ void read_frags(const float* As, const float* Bs, int half, int wm, int wn,
-                                           int li, int lh, Frags<TM, TN, H>& f) {
-  if constexpr (H) {
+                                           int li, int lh, Frags<TM, TN, P>& f) {
+  if constexpr (P == 2) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) f.a[t][c] = LA::hfrag(As, wm * (BM / 2) + t * 32 + li, half, lh, c);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) f.b[u][c] = LB::hfrag(Bs, wn * (BN / 2) + u * 32 + li, half, lh, c);
+    }
+  } else if constexpr (P == 1) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
 #pragma unroll
@@ -435,8 +617,27 @@ __device__ __forceinline__ void read_frags(const float* As, const float* Bs, int
 }
 
 // MFMA sub-steps [S0, S1) of a half (fp32: s = 0..7, bf16: c = 0..1)
+// bf16x6: the six products of the split operands whose order is >= 2^-16 (a_i b_j, i + j <= 2),
+// smallest first; the dropped a1 b2, a2 b1, a2 b2 are below 2^-24 |a b|.  Term j of the list:
+__device__ __forceinline__ constexpr int x6_ia(int j) { return j == 0 ? 2 : j == 1 ? 1 : j == 2 ? 0 : j == 3 ? 1 : j == 4 ? 0 : 0; }
+__device__ __forceinline__ constexpr int x6_ib(int j) { return j == 0 ? 0 : j == 1 ? 1 : j == 2 ? 2 : j == 3 ? 0 : j == 4 ? 1 : 0; }
 template <int S0, int S1, int TM, int TN>
-__device__ __forceinline__ void mfma_part(const Frags<TM, TN, false>& f, floatx16 (&acc)[TM][TN]) {
+__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 2>& f, floatx16 (&acc)[TM][TN]) {
+#pragma unroll
+  for (int j = S0; j < S1; ++j)
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][x6_ia(j)], f.b[u][x6_ib(j)], acc[t][u], 0, 0, 0);
+}
+template <int TM, int TN>
+__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 2>& f, floatx16 (&acc)[TM][TN]) {
+  mfma_part<0, 6>(f, acc);
+}
+
+template <int S0, int S1, int TM, int TN>
+__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 0>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
   for (int s = S0; s < S1; ++s)
 #pragma unroll
@@ -446,7 +647,7 @@ __device__ __forceinline__ void mfma_part(const Frags<TM, TN, false>& f, floatx1
         acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[t][s], f.b[u][s], acc[t][u], 0, 0, 0);
 }
 template <int S0, int S1, int TM, int TN>
-__device__ __forceinline__ void mfma_part(const Frags<TM, TN, true>& f, floatx16 (&acc)[TM][TN]) {
+__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 1>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
   for (int c = S0; c < S1; ++c)
 #pragma unroll
@@ -457,7 +658,7 @@ __device__ __forceinline__ void mfma_part(const Frags<TM, TN, true>& f, floatx16
 }
 
 template <int TM, int TN>
-__device__ __forceinline__ void mfma_half(const Frags<TM, TN, false>& f, floatx16 (&acc)[TM][TN]) {
+__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 0>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
   for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -468,7 +669,7 @@ __device__ __forceinline__ void mfma_half(const Frags<TM, TN, false>& f, floatx1
 }
 
 template <int TM, int TN>
-__device__ __forceinline__ void mfma_half(const Frags<TM, TN, true>& f, floatx16 (&acc)[TM][TN]) {
+__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 1>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -486,12 +687,13 @@ __device__ __forceinline__ void mfma_half(const Frags<TM, TN, true>& f, floatx16
 // other's issue gaps at one block per CU); the groups stage alternate k-tiles, the partial
 // accumulators are summed through LDS before the epilogue.  (The k-halves of one k-tile are added in a
 // different order than KS = 1: results agree to fp32 rounding, not bitwise.)
-template <int BM, int BN, int BK, int MA, int MB, bool H, int KS = 1>
+template <int BM, int BN, int BK, int MA, int MB, int P, int KS = 1>
 __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
-  static_assert(BK == (H ? 64 : 32), "the k-step pipeline assumes two halves per k-tile");
+  static_assert(BK == (P == 1 ? 64 : 32), "the k-step pipeline assumes two halves per k-tile");
+  static_assert(KS == 1 || P == 0, "two wave groups: fp32 tiles only");
   constexpr int TM = BM / 64, TN = BN / 64;
-  using LA = TileLoader<BM, BK, MA, H>;
-  using LB = TileLoader<BN, BK, MB, H>;
+  using LA = TileLoader<BM, BK, MA, P>;
+  using LB = TileLoader<BN, BK, MB, P>;
   constexpr int STAGE = LA::TILE + LB::TILE;
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
   static_assert(KS == 1 || (TM * TN * 16 * 256 <= 2 * STAGE), "KS = 2 partials must fit the stages");
@@ -543,7 +745,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
 
   const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
   if constexpr (KS == 1) {
-    Frags<TM, TN, H> f0, f1;
+    Frags<TM, TN, P> f0, f1;
     if (nk > 0) {
       la.load(kbeg);
       lb.load(kbeg);
@@ -555,7 +757,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       }
     }
     __syncthreads();
-    if (nk > 0) read_frags<BM, BN, TM, TN, H, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
+    if (nk > 0) read_frags<BM, BN, TM, TN, P, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
     for (int i = 0; i < nk; ++i) {
       const float* cur = lds + (i & 1) * STAGE;
       float* nxt = lds + ((i + 1) & 1) * STAGE;
@@ -568,7 +770,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
         la.load(kbeg + (i + 2) * BK);
         lb.load(kbeg + (i + 2) * BK);
       }
-      read_frags<BM, BN, TM, TN, H, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
+      read_frags<BM, BN, TM, TN, P, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
       mfma_half(f0, acc);
       // The step's barrier, pinned after the first half's MFMAs (left to itself the compiler
       // hoists it above them, and __syncthreads' fence would also wait for the second half's
@@ -583,19 +785,20 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       // the next tile's first fragments are read behind the first MFMAs of this second half
       // (issued right after the barrier they would be waited for before any MFMA: the compiler
       // cannot tell them apart from the second half's own reads in the LDS counter)
-      constexpr int SPLIT = H ? 1 : 2;
+      constexpr int SPLIT = P == 1 ? 1 : 2;
+      constexpr int NSUB = P == 0 ? 8 : (P == 1 ? 2 : 6);
       mfma_part<0, SPLIT>(f1, acc);
       __builtin_amdgcn_sched_barrier(0);
-      if (i + 1 < nk) read_frags<BM, BN, TM, TN, H, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
+      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_part<SPLIT, H ? 2 : 8>(f1, acc);
+      mfma_part<SPLIT, NSUB>(f1, acc);
     }
     __syncthreads();  // the m-contiguous epilogue reuses the stages
   } else {
     // The groups take turns staging: group j % 2 loads k-tile j three steps ahead and stores it
     // one step ahead, so a tile's global loads have two k-steps to land (one with a single
     // staging group) at no extra registers.
-    Frags<TM, TN, H> f;
+    Frags<TM, TN, P> f;
     if (nk > 0) {
       if (grp == 0) {
         la.load(kbeg);
@@ -612,7 +815,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       }
     }
     __syncthreads();
-    if (nk > 0) read_frags<BM, BN, TM, TN, H, LA, LB>(lds, lds + LA::TILE, grp, wm, wn, li, lh, f);
+    if (nk > 0) read_frags<BM, BN, TM, TN, P, LA, LB>(lds, lds + LA::TILE, grp, wm, wn, li, lh, f);
     for (int i = 0; i < nk; ++i) {
       float* nxt = lds + ((i + 1) & 1) * STAGE;
       if (grp == ((i + 1) & 1)) {
@@ -627,7 +830,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       }
       mfma_half(f, acc);
       __syncthreads();
-      if (i + 1 < nk) read_frags<BM, BN, TM, TN, H, LA, LB>(nxt, nxt + LA::TILE, grp, wm, wn, li, lh, f);
+      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, LA, LB>(nxt, nxt + LA::TILE, grp, wm, wn, li, lh, f);
     }
     // sum the two groups' partial accumulators (group 1 -> LDS -> group 0)
     __syncthreads();
@@ -717,11 +920,11 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
 
 // Launch one tile configuration for the operand modes (ma, mb).  Instantiated per (tile, type)
 // in its own translation unit (gemm_f32_64.hip, ...), so the 25 mode pairs compile in parallel.
-template <int BM, int BN, int BK, bool H, int KS = 1>
+template <int BM, int BN, int BK, int P, int KS = 1>
 void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
-  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, H, KS>), grid, dim3(256 * KS), 0, st, a); return; }
+  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3(256 * KS), 0, st, a); return; }
   if constexpr (KS == 2) {  // dense operands only (gemm.hip)
     A2M_L(0, 0)
     return;
@@ -731,13 +934,16 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3) A2M_L(2, 4)
   A2M_L(3, 0) A2M_L(3, 1) A2M_L(3, 2) A2M_L(3, 3) A2M_L(3, 4)
   A2M_L(4, 0) A2M_L(4, 1) A2M_L(4, 2) A2M_L(4, 3) A2M_L(4, 4)
+  A2M_L(0, 5)
 #undef A2M_L
 }
 
-extern template void launch_tile<64, 64, 32, false>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<64, 64, 32, false, 2>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<128, 128, 32, false>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<64, 64, 64, true>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<128, 128, 64, true>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<64, 64, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<64, 64, 32, 0, 2>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<128, 128, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<64, 64, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<128, 128, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<64, 64, 32, 2>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<128, 128, 32, 2>(const GemmArgs&, int, int, int, hipStream_t);
 
 }  // namespace a2m

@@ -1,0 +1,7 @@
+// Instantiation of the GEMM engine's launch_tile<64, 64, 32, 2> (bf16x6: fp32 operands split
+// into three bf16 planes, six MFMA products per k-chunk; one translation unit per tile configuration).
+#include "gemm_kernel.h"
+
+namespace a2m {
+template void launch_tile<64, 64, 32, 2>(const GemmArgs&, int, int, int, hipStream_t);
+}  // namespace a2m

@@ -251,6 +251,19 @@ __global__ void convt_pack_kernel(const float* w, int Ci, int Co, int ks, int s,
   }
 }
 
+// Conv1d weights [Co][Ci][ks] -> tap-chunked [Co][Ci/CH][ks][CH] (the k order of loader mode 5)
+__global__ void conv1d_tap_pack_kernel(const float* w, int Co, int Ci, int ks, int ch, float* out) {
+  const int64_t total = (int64_t)Co * Ci * ks;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int tap = (int)(i % ks);
+    const int64_t t = i / ks;
+    const int ci = (int)(t % Ci), co = (int)(t / Ci);
+    const int cc = ci / ch, cl = ci - cc * ch;
+    out[(((int64_t)co * (Ci / ch) + cc) * ks + tap) * ch + cl] = w[i];
+  }
+}
+
 // [wq; wk; wv] -> wcat [C/4 + C][C], biases -> bcat (zeros where a bias pointer is NULL)
 __global__ void stack_qkv_kernel(const float* wq, const float* bq, const float* wk, const float* bk,
                                  const float* wv, const float* bv, int C, float* wcat, float* bcat) {
@@ -481,6 +494,52 @@ int a2m_convt1d_packed_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32
     off += (size_t)Co * ntap * Ci;
   }
   return A2M_OK;
+}
+
+int a2m_conv1d_tap_pack_f32(const float* w, int32_t Co, int32_t Ci, int32_t ks, int32_t chunk,
+                            float* packed, void* stream) {
+  A2M_CHECK_ARG(w && packed && Co > 0 && Ci > 0 && ks > 0 && (chunk == 32 || chunk == 64) &&
+                    Ci % chunk == 0,
+                "conv1d_tap_pack: bad args Co=%d Ci=%d k=%d chunk=%d", Co, Ci, ks, chunk);
+  A2M_CHECK_ARG(fits32((int64_t)Co * Ci * ks), "conv1d_tap_pack: too large");
+  hipLaunchKernelGGL(conv1d_tap_pack_kernel,
+                     dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Co * Ci * ks, 256), 8192)),
+                     dim3(256), 0, as_stream(stream), w, Co, Ci, ks, chunk, packed);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int32_t a2m_conv1d_tap_chunk(void) { return gemm_k_tile(); }
+
+int a2m_conv1d_tap_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
+                           int32_t T, const float* packed, int32_t chunk, const float* bias,
+                           int32_t Co, int32_t ks, int32_t pad, const float* bn_w,
+                           const float* bn_b, const float* bn_rm, const float* bn_rv, float bn_eps,
+                           int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
+                           int64_t ys_t, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && packed && y, "conv1d_tap: null pointer");
+  A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && ks > 1 && 2 * pad == ks - 1,
+                "conv1d_tap: bad shape B=%d Ci=%d Co=%d k=%d p=%d (stride 1, same padding)", B, Ci,
+                Co, ks, pad);
+  A2M_CHECK_ARG(chunk == gemm_k_tile() && Ci % chunk == 0,
+                "conv1d_tap: weights packed in %d-channel chunks, the engine's k-tile is %d (Ci=%d)",
+                chunk, gemm_k_tile(), Ci);
+  A2M_CHECK_ARG(T > 0 && T % 4 == 0 && 64 % T == 0 && pad < T,
+                "conv1d_tap: clip length %d must divide the 64-row tile and be a multiple of 4", T);
+  A2M_CHECK_ARG(fits32(xs_b) && fits32(xs_c) && fits32((int64_t)B * xs_b) &&
+                    fits32((int64_t)B * ys_b) && fits32(ys_c) && fits32(ys_t),
+                "conv1d_tap: tensor too large for 32-bit offsets");
+  A2M_CHECK_ARG((reinterpret_cast<uintptr_t>(x) % 16) == 0 && xs_b % 4 == 0 && xs_c % 4 == 0,
+                "conv1d_tap: x rows must be 16-byte aligned");
+  Gather A = dense_rk(packed, Ci * ks);
+  Gather Bg{};
+  Bg.base = x; Bg.bstride = 0;
+  Bg.sr0 = (int)xs_b; Bg.R1 = 1; Bg.R2 = T; Bg.sk0 = (int)xs_c;
+  Bg.K1 = Bg.K2 = 1; Bg.divh = Bg.divw = 1; Bg.Lh = Bg.Lw = 1;
+  Bg.cw = -pad; Bg.tapconv = ks;
+  Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+  E.N1 = 1; E.N2 = T; E.so0 = (int)ys_b; E.so1 = 0; E.so2 = (int)ys_t; E.som = (int)ys_c;
+  return gemm(A, Bg, E, Co, B * T, Ci * ks, 1, ws, ws_bytes, as_stream(stream));
 }
 
 int a2m_convt1d_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int32_t stride,

@@ -331,7 +331,9 @@ def run_train(args, world, rank, dev):
 
 
 def mfma_peak(dtype):
-    return FP32_MFMA_PEAK_TFLOPS if dtype == 'fp32' else BF16_MFMA_PEAK_TFLOPS
+    # bf16x6: six bf16 MFMAs per fp32-class product -> the fp32-equivalent ceiling is bf16 / 6
+    return {'fp32': FP32_MFMA_PEAK_TFLOPS, 'bf16': BF16_MFMA_PEAK_TFLOPS,
+            'bf16x6': BF16_MFMA_PEAK_TFLOPS / 6}[dtype]
 
 
 def roofline_entry(gt, peak=None):
@@ -377,7 +379,7 @@ def main():
                     help='train mode: SyncBN over the DP ranks (SURVEY 8(e)); default per-rank statistics')
     ap.add_argument('--bucket-mb', type=float, default=25.0,
                     help='train mode: gradient all-reduce bucket size (MB)')
-    ap.add_argument('--dtype', choices=('fp32', 'bf16'), default='fp32',
+    ap.add_argument('--dtype', choices=('fp32', 'bf16', 'bf16x6'), default='fp32',
                     help='GEMM operand precision (bf16: configs[4], fp32 accumulation/storage)')
     args = ap.parse_args()
 

@@ -83,6 +83,24 @@ int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, i
                         const float* bn_rv, float bn_eps, int32_t act, float slope,
                         float* y, int64_t ys_b, int64_t ys_c,
                         void* ws, size_t ws_bytes, void* stream);
+/* Tap-chunked conv1d (stride 1, "same" padding 2*pad == ks-1): the forward of
+ * model_layers.py ConvNormRelu(type='1d') / ResBlock convs (nn.Conv1d(k=3, s=1, p=1),
+ * model_layers.py:75-120) without an im2col matrix.  Weights are packed once per weight version
+ * by a2m_conv1d_tap_pack_f32 as [Co][Ci/chunk][ks][chunk] with chunk = a2m_conv1d_tap_chunk()
+ * (the engine's k-tile at the current precision: 32 fp32 / bf16x6, 64 bf16); the GEMM's B
+ * loader reads each chunk's x[b][c][t] window once and re-stores it shifted for every tap.
+ * x: [B][Ci][T] with unit t stride and 16-byte aligned rows; T % 4 == 0 and 64 % T == 0 (the
+ * tiles hold whole clips).  Epilogue (bias, BN-eval, activation) and output strides as
+ * a2m_conv1d_fwd_f32. */
+int32_t a2m_conv1d_tap_chunk(void);
+int a2m_conv1d_tap_pack_f32(const float* w, int32_t Co, int32_t Ci, int32_t ks, int32_t chunk,
+                            float* packed, void* stream);
+int a2m_conv1d_tap_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
+                           int32_t T, const float* packed, int32_t chunk, const float* bias,
+                           int32_t Co, int32_t ks, int32_t pad, const float* bn_w,
+                           const float* bn_b, const float* bn_rm, const float* bn_rv, float bn_eps,
+                           int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
+                           int64_t ys_t, void* ws, size_t ws_bytes, void* stream);
 /* The same split in two: the per-phase weight packing (packed: Ci*Co*k floats) and the
  * forward on packed weights (callers cache the packing while the weights are unchanged). */
 int a2m_convt1d_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int32_t stride,
@@ -392,9 +410,12 @@ int a2m_gemm_plan_override(int32_t tile, int32_t splits);
 /* Operand precision of every GEMM-engine launch (convs, linears, attention products and their
  * backward) issued after the call: 0 = fp32 (default; the parity configuration), 1 = bf16
  * operands with fp32 accumulation (BASELINE configs[4], torch.autocast(bfloat16)-equivalent:
- * weights and activations stay fp32 in HBM, rounded to bf16 where they enter the MFMA).
+ * weights and activations stay fp32 in HBM, rounded to bf16 where they enter the MFMA),
+ * 2 = bf16x6 (fp32 operands split exactly into hi + mid + lo bf16 pieces where they enter LDS;
+ * the six products a_i b_j with i + j <= 2 accumulate in fp32 on the bf16 MFMA: fp32-class
+ * results, each dropped term below 2^-24 |a b|).
  * Process-wide; not thread-safe against concurrent launches. */
-int a2m_set_gemm_precision(int32_t bf16);
+int a2m_set_gemm_precision(int32_t prec);
 int32_t a2m_get_gemm_precision(void);
 int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                         int64_t* reduces);

@@ -1,0 +1,127 @@
+"""Tap-chunked conv1d (a2m_conv1d_tap_fwd_f32, GEMM loader mode 5) and the bf16x6 engine precision.
+
+The tap path is the forward of nn.Conv1d(k, stride=1, padding=(k-1)/2) (model_layers.py:75-120,
+the ConvNormRelu / ResBlock convs of the UNet and both decoders) without an im2col matrix: the
+B loader stages each channel chunk's x window once and re-stores it shifted per tap.  It must
+agree with an fp64 convolution at fp32 accuracy, wrap nothing across clip boundaries, and
+match the im2col path it replaces.  bf16x6 (three-way bf16 operand split, six products) must
+be fp32-class against fp64.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+# fp32-class accuracy against fp64, relative to max |ref| (measured ~1e-6 at K <= 6144)
+TOL32 = 1e-5
+
+
+def _conv_ref(x, w, b, pad):
+    return torch.nn.functional.conv1d(x.double(), w.double(), None if b is None else b.double(),
+                                      padding=pad)
+
+
+@pytest.mark.parametrize('prec', ['fp32', 'bf16x6', 'bf16'])
+@pytest.mark.parametrize('B,Ci,Co,T,k', [(64, 256, 256, 64, 3), (8, 512, 1024, 32, 3),
+                                         (5, 1024, 2048, 16, 3), (1, 256, 512, 16, 3),
+                                         (3, 64, 96, 8, 5), (2, 32, 20, 4, 3)])
+def test_tap_conv1d_matches_fp64(prec, B, Ci, Co, T, k):
+    import a2m
+    from a2m import functional as F
+    g = torch.Generator().manual_seed(B * 7 + Ci + T)
+    x = torch.randn(B, Ci, T, generator=g)
+    w = torch.randn(Co, Ci, k, generator=g) / np.sqrt(Ci * k)
+    b = torch.randn(Co, generator=g)
+    pad = (k - 1) // 2
+    with a2m.gemm_precision(prec):
+        if Ci % a2m._native.lib.a2m_conv1d_tap_chunk():
+            pytest.skip('Ci not a multiple of the k-tile at this precision')
+        cache = {}
+        y = F.conv1d(x.to(DEV), w.to(DEV), b.to(DEV), 1, pad, cache=cache)
+        assert 'w' in cache, 'tap path not taken'
+    ref = _conv_ref(x, w, b, pad)
+    if prec == 'bf16':
+        ref = _conv_ref(x.bfloat16().float(), w.bfloat16().float(), b, pad)
+    e = rel_err(y.cpu().double(), ref)
+    assert e < TOL32, e
+
+
+def test_tap_conv1d_epilogue_views_and_cache():
+    """BN-eval + LeakyReLU epilogue, x a channel slice of a concat buffer, out a strided view;
+    the packed weights are rebuilt when the weight changes in place."""
+    from a2m import functional as F
+    g = torch.Generator().manual_seed(3)
+    B, Ci, Co, T = 16, 256, 128, 64
+    cat = torch.randn(B, 2 * Ci, T, generator=g).to(DEV)
+    x = cat[:, Ci:]
+    w = (torch.randn(Co, Ci, 3, generator=g) * 0.05).to(DEV)
+    bias = torch.randn(Co, generator=g).to(DEV)
+    bn = tuple(t.to(DEV) for t in (torch.rand(Co) + 0.5, torch.randn(Co), torch.randn(Co) * 0.1,
+                                   torch.rand(Co) + 0.5)) + (1e-5,)
+    outbuf = torch.zeros(B, T, 2 * Co, device=DEV)
+    out = outbuf[:, :, Co:].permute(0, 2, 1)
+    cache = {}
+    F.conv1d(x, w, bias, 1, 1, bn=bn, act=F.ACT_LRELU, slope=0.2, out=out, cache=cache)
+    ref = F.conv1d(x, w, bias, 1, 1, bn=bn, act=F.ACT_LRELU, slope=0.2)   # im2col path
+    assert rel_err(out.cpu(), ref.cpu()) < 1e-6
+    assert outbuf[:, :, :Co].abs().max().item() == 0.0
+    with torch.no_grad():
+        w.mul_(-1.0)
+    F.conv1d(x, w, bias, 1, 1, bn=bn, act=F.ACT_LRELU, slope=0.2, out=out, cache=cache)
+    ref = F.conv1d(x, w, bias, 1, 1, bn=bn, act=F.ACT_LRELU, slope=0.2)
+    assert rel_err(out.cpu(), ref.cpu()) < 1e-6
+
+
+def test_tap_conv1d_rejects_ineligible():
+    """T that does not tile the 64-row GEMM tile (the long-form 480-frame clips) or a chunk
+    packed for another precision is refused by the C-ABI (the Python layer then takes the
+    im2col path)."""
+    import a2m
+    from a2m import _native as N
+    from a2m import functional as F
+    x = torch.randn(2, 64, 480, device=DEV)
+    w = torch.randn(64, 64, 3, device=DEV)
+    cache = {}
+    y = F.conv1d(x, w, None, 1, 1, cache=cache)
+    assert 'w' not in cache
+    assert rel_err(y.cpu().double(), _conv_ref(x.cpu(), w.cpu(), None, 1)) < TOL32
+    x = torch.randn(2, 64, 64, device=DEV)
+    packed, chunk = F.conv1d_tap_packed(w)
+    with a2m.gemm_precision('bf16'):
+        rc = N.lib.a2m_conv1d_tap_fwd_f32(x.data_ptr(), 64 * 64, 64, 2, 64, 64, packed.data_ptr(),
+                                          chunk, None, 64, 3, 1, None, None, None, None, 1e-5, 0,
+                                          0.2, y.data_ptr(), 64 * 64, 64, 1, None, 0, None)
+    assert rc == N.A2M_EINVAL and 'chunk' in N.last_error()
+
+
+@pytest.mark.parametrize('M,N,K', [(256, 4096, 768), (300, 1000, 500), (1024, 2048, 6144)])
+def test_bf16x6_gemm_fp32_class(M, N, K):
+    """bf16x6 against fp64 on unrounded fp32 operands: within fp32 accumulation error."""
+    import a2m
+    from a2m import functional as F
+    g = torch.Generator().manual_seed(M * 3 + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    ref = A.double() @ B.double().t()
+    C = torch.empty(M, N, device=DEV)
+    with a2m.gemm_precision('bf16x6'):
+        F.gemm(M, N, K, A.to(DEV), K, 1, B.to(DEV), K, 1, C, N, 1)
+    assert rel_err(C.cpu().double(), ref) < TOL32
+
+
+def test_bf16x6_generator_eval_golden(g_state):
+    """G eval (B=2, T=64 reference fixture) with every GEMM in bf16x6: north_star's 1e-4."""
+    import a2m
+    from a2m.real_motion_model import SelfAttention_G
+    z = golden('g_eval_b2t64.npz')
+    g = SelfAttention_G(p=0.0)
+    g.load_state_dict(g_state, strict=False)
+    g = g.to(DEV).eval()
+    with torch.no_grad(), a2m.gemm_precision('bf16x6'):
+        pose, _ = g(torch.from_numpy(z['audio']).to(DEV))
+    e = rel_err(pose.cpu(), z["pose"])
+    assert e < 1e-4, e

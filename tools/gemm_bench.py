@@ -18,6 +18,9 @@ SHAPES = [(256, 4096, 768), (512, 4096, 3072), (2048, 1024, 3072), (1024, 2048, 
 if len(sys.argv) > 1:
     SHAPES = [tuple(int(v) for v in a.split(',')) for a in sys.argv[1:]]
 from a2m import _native as NN  # noqa: E402
+import a2m  # noqa: E402
+
+PRECS = os.environ.get('PREC', 'fp32').split(',')
 
 
 def one(M, N, K, tile, split):
@@ -30,6 +33,12 @@ def one(M, N, K, tile, split):
     torch.cuda.synchronize()
     ref = (A.double() @ B.double().t()).float()
     err = ((C - ref).abs().max() / ref.abs().max()).item()
+    if os.environ.get('NOGRAPH'):   # plain launches (PMC passes): 10 back to back
+        for _ in range(10):
+            run()
+        torch.cuda.synchronize()
+        print(f'gemm {M}x{N}x{K} rel err {err:.1e} (no timing)', flush=True)
+        return
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     iters = 20
@@ -47,10 +56,16 @@ def one(M, N, K, tile, split):
     e1.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / (3 * iters)
     tag = f'tile {tile} split {split}' if tile or split else 'planner'
+    tag = f'{CUR[0]:6s} ' + tag
     print(f'gemm {M}x{N}x{K} {tag:18s}: {us:8.1f} us  {2.0 * M * N * K / us / 1e6:6.1f} TF  rel err {err:.1e}', flush=True)
 
 
+CUR = ['fp32']
 for M, N, K in SHAPES:
-    for tile, split in PLANS:
-        one(M, N, K, tile, split)
+    for prec in PRECS:
+        CUR[0] = prec
+        a2m.set_gemm_precision(prec)
+        for tile, split in PLANS:
+            one(M, N, K, tile, split)
+a2m.set_gemm_precision('fp32')
 NN.lib.a2m_gemm_plan_override(0, 0)

@@ -50,6 +50,9 @@ def main():
         r = subprocess.run([sys.executable, __file__, '--child', mode], env=env, capture_output=True,
                            text=True, timeout=300)
         print(r.stdout.strip())
+        os.makedirs(os.path.join(REPO, 'gpurun_out'), exist_ok=True)
+        with open(os.path.join(REPO, 'gpurun_out', f'gemm_times_{mode}.err'), 'w') as f:
+            f.write(r.stderr)
         if r.returncode != 0:
             print(r.stderr[-3000:])
             sys.exit(r.returncode)

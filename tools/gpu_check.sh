@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 TAG=${1:-r1}
 SKIP_TESTS=${2:-}
 if [ "$SKIP_TESTS" != "--skip-tests" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -x --durations=15 > gpurun_out/pytest_gpu_$TAG.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread --durations=15 > gpurun_out/pytest_gpu_$TAG.log 2>&1
   rc=$?
   tail -5 gpurun_out/pytest_gpu_$TAG.log
   if [ $rc -ne 0 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
