@@ -331,6 +331,35 @@ def graph_layer(x, J, kind, nbr_ptr, nbr_idx, w0, w1, att_src, att_dst, bias, ln
     return out
 
 
+def graph_att_proj(w0, att_src, att_dst, cache=None):
+    """[8][64] GAT attention projections (a2m_graph_att_proj_f32), cached per weight version."""
+    key = _wkey((w0, att_src, att_dst))
+    if cache is not None and cache.get('key') == key:
+        return cache['U']
+    U = torch.empty(8, 64, device=w0.device)
+    N.check(N.lib.a2m_graph_att_proj_f32(_p(w0), _p(att_src), _p(att_dst), _p(U), _stream()))
+    if cache is not None:
+        cache.update(key=key, U=U)
+    return U
+
+
+def graph_stack(x, J, nbr_ptr, nbr_idx, layers, slope=0.2, out=None):
+    """Fused eval stack of graph layers (a2m_graph_stack_fwd_f32).  x: [F*J, 64] contiguous;
+    layers: list of (kind, w0, w1, U, bias, ln_w, ln_b) with U from graph_att_proj for GAT."""
+    _check_dev(x, out)
+    assert x.is_contiguous() and x.shape[1] == 64 and x.shape[0] % J == 0 and 0 < len(layers) <= 8
+    F = x.shape[0] // J
+    if out is None:
+        out = torch.empty_like(x)
+    n = len(layers)
+    ptrs = lambda i: (ctypes.c_void_p * n)(*[_p(L[i]) for L in layers])  # noqa: E731
+    kinds = (ctypes.c_int32 * n)(*[L[0] for L in layers])
+    N.check(N.lib.a2m_graph_stack_fwd_f32(_p(x), F, J, _p(nbr_ptr), _p(nbr_idx), n, kinds,
+                                          ptrs(1), ptrs(2), ptrs(3), ptrs(4), ptrs(5), ptrs(6),
+                                          slope, _p(out), _stream()))
+    return out
+
+
 # ------------------------------------------------------------------------- losses
 ANGLE_W = (0.7, 0.3)   # compute_comprehensive_angle_loss (real_motion_model.py:449-461)
 

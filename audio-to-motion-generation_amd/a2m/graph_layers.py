@@ -25,6 +25,7 @@ class GATConv(nn.Module):
         self.att_src = nn.Parameter(torch.empty(1, heads, out_channels))
         self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
         self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
+        self._U = {}   # attention projections for the fused eval stack (functional.graph_att_proj)
         self.reset_parameters()
 
     def reset_parameters(self):

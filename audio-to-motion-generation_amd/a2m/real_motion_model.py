@@ -103,15 +103,27 @@ class SelfAttention_G(_GraphTopology):
         a, b = h.view(B * T * nj, 64), torch.empty(B * T * nj, 64, device=x.device)
         ptr, idx = self.topology(part)
         lns = getattr(self, f'{part}_layer_norms')
-        for L in range(5):
-            g = getattr(self, f'{part}_gcn{L + 1}')
-            if L % 2 == 0:
-                F.graph_layer(a, nj, 0, ptr, idx, g.lin.weight, None, g.att_src, g.att_dst, g.bias,
-                              lns[L].weight, lns[L].bias, out=b)
-            else:
-                F.graph_layer(a, nj, 1, ptr, idx, g.lin_rel.weight, g.lin_root.weight, None, None,
-                              g.lin_rel.bias, lns[L].weight, lns[L].bias, out=b)
-            a, b = b, a
+        if _FUSED_STACK:
+            layers = []
+            for L in range(5):
+                g = getattr(self, f'{part}_gcn{L + 1}')
+                if L % 2 == 0:
+                    U = F.graph_att_proj(g.lin.weight, g.att_src, g.att_dst, cache=g._U)
+                    layers.append((0, g.lin.weight, None, U, g.bias, lns[L].weight, lns[L].bias))
+                else:
+                    layers.append((1, g.lin_rel.weight, g.lin_root.weight, None, g.lin_rel.bias,
+                                   lns[L].weight, lns[L].bias))
+            a = F.graph_stack(a, nj, ptr, idx, layers, out=b)
+        else:
+            for L in range(5):
+                g = getattr(self, f'{part}_gcn{L + 1}')
+                if L % 2 == 0:
+                    F.graph_layer(a, nj, 0, ptr, idx, g.lin.weight, None, g.att_src, g.att_dst, g.bias,
+                                  lns[L].weight, lns[L].bias, out=b)
+                else:
+                    F.graph_layer(a, nj, 1, ptr, idx, g.lin_rel.weight, g.lin_root.weight, None, None,
+                                  g.lin_rel.bias, lns[L].weight, lns[L].bias, out=b)
+                a, b = b, a
         rows = torch.empty(B, T, C, device=x.device)
         F.conv1d(a.view(B, T, nj * 64).permute(0, 2, 1), pout.weight, pout.bias, out=rows.permute(0, 2, 1))
         nrm = getattr(self, f'{part}_norm')
@@ -182,6 +194,7 @@ class SelfAttention_G(_GraphTopology):
 
 
 _BRANCH_STREAMS = os.environ.get('A2M_BRANCH_STREAMS', '1') != '0'
+_FUSED_STACK = os.environ.get('A2M_GRAPH_STACK', '1') != '0'   # one launch for the 5 graph layers
 _SIDE_STREAMS = {}
 
 

@@ -169,6 +169,9 @@ struct Plan {
 // fp32 accumulation: fp32-class accuracy at 16/6 of the f32 MFMA rate; BK 32).
 // (BK = 16 measured slower end to end.)
 static int g_gemm_prec = 0;
+// (fp32 at BK = 64 -- fewer barriers per MFMA -- measured 10-20 % slower on every G shape:
+// the k-loop's non-MFMA cost scales with the staged bytes, not with the barrier count;
+// profiles/r02_gemm_ablation.txt)
 static int gemm_bk(int prec) { return prec == 1 ? 64 : 32; }
 int gemm_k_tile() { return gemm_bk(g_gemm_prec); }
 

@@ -16,6 +16,13 @@
 #pragma once
 #include "a2m_internal.h"
 
+// Diagnostic builds only (tools/gemm_ablate.sh; never the shipped library): A2M_ABLATE = 1 drops
+// the k-loop MFMAs, 2 its global loads after the prologue, 3 its barriers (results wrong; the
+// timing of what remains tells which part holds the loop).
+#ifndef A2M_ABLATE
+#define A2M_ABLATE 0
+#endif
+
 namespace a2m {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -574,24 +581,24 @@ __device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int
 // The next tile's first fragments are read while this tile's second half is on the matrix
 // pipe, so no LDS latency sits between k-steps.  LDS[(i+1)&1] is free at the start of step i:
 // its last reads (tile i-1, half 1) preceded step i-1's barrier.
-template <int TM, int TN, int P>
+template <int TM, int TN, int P, int NS = 1>
 struct Frags;
-template <int TM, int TN>
-struct Frags<TM, TN, 0> {  // fp32: 16 k per half, 8 per lane
-  float a[TM][8], b[TN][8];
+template <int TM, int TN, int NS>
+struct Frags<TM, TN, 0, NS> {  // fp32: 16 NS k per half (BK = 32 NS), 8 NS per lane
+  float a[TM][8 * NS], b[TN][8 * NS];
 };
 template <int TM, int TN>
-struct Frags<TM, TN, 1> {   // bf16: 32 k per half = two K16 chunks, 8 per lane each
+struct Frags<TM, TN, 1, 1> {   // bf16: 32 k per half = two K16 chunks, 8 per lane each
   bf16x8 a[TM][2], b[TN][2];
 };
 template <int TM, int TN>
-struct Frags<TM, TN, 2> {   // bf16x6: 16 k per half (one K16 chunk), the three planes
+struct Frags<TM, TN, 2, 1> {   // bf16x6: 16 k per half (one K16 chunk), the three planes
   bf16x8 a[TM][3], b[TN][3];
 };
 
-template <int BM, int BN, int TM, int TN, int P, class LA, class LB>
+template <int BM, int BN, int TM, int TN, int P, int NS, class LA, class LB>
 __device__ __forceinline__ void read_frags(const float* As, const float* Bs, int half, int wm, int wn,
-                                           int li, int lh, Frags<TM, TN, P>& f) {
+                                           int li, int lh, Frags<TM, TN, P, NS>& f) {
   if constexpr (P == 2) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -610,9 +617,12 @@ __device__ __forceinline__ void read_frags(const float* As, const float* Bs, int
     }
   } else {
 #pragma unroll
-    for (int t = 0; t < TM; ++t) LA::frag(As, wm * (BM / 2) + t * 32 + li, half, lh, f.a[t]);
+    for (int sub = 0; sub < NS; ++sub) {
 #pragma unroll
-    for (int u = 0; u < TN; ++u) LB::frag(Bs, wn * (BN / 2) + u * 32 + li, half, lh, f.b[u]);
+      for (int t = 0; t < TM; ++t) LA::frag(As, wm * (BM / 2) + t * 32 + li, half * NS + sub, lh, &f.a[t][8 * sub]);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) LB::frag(Bs, wn * (BN / 2) + u * 32 + li, half * NS + sub, lh, &f.b[u][8 * sub]);
+    }
   }
 }
 
@@ -622,7 +632,7 @@ __device__ __forceinline__ void read_frags(const float* As, const float* Bs, int
 __device__ __forceinline__ constexpr int x6_ia(int j) { return j == 0 ? 2 : j == 1 ? 1 : j == 2 ? 0 : j == 3 ? 1 : j == 4 ? 0 : 0; }
 __device__ __forceinline__ constexpr int x6_ib(int j) { return j == 0 ? 0 : j == 1 ? 1 : j == 2 ? 2 : j == 3 ? 0 : j == 4 ? 1 : 0; }
 template <int S0, int S1, int TM, int TN>
-__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 2>& f, floatx16 (&acc)[TM][TN]) {
+__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 2, 1>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
   for (int j = S0; j < S1; ++j)
 #pragma unroll
@@ -632,12 +642,12 @@ __device__ __forceinline__ void mfma_part(const Frags<TM, TN, 2>& f, floatx16 (&
         acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][x6_ia(j)], f.b[u][x6_ib(j)], acc[t][u], 0, 0, 0);
 }
 template <int TM, int TN>
-__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 2>& f, floatx16 (&acc)[TM][TN]) {
+__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 2, 1>& f, floatx16 (&acc)[TM][TN]) {
   mfma_part<0, 6>(f, acc);
 }
 
-template <int S0, int S1, int TM, int TN>
-__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 0>& f, floatx16 (&acc)[TM][TN]) {
+template <int S0, int S1, int TM, int TN, int NS>
+__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 0, NS>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
   for (int s = S0; s < S1; ++s)
 #pragma unroll
@@ -647,7 +657,7 @@ __device__ __forceinline__ void mfma_part(const Frags<TM, TN, 0>& f, floatx16 (&
         acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[t][s], f.b[u][s], acc[t][u], 0, 0, 0);
 }
 template <int S0, int S1, int TM, int TN>
-__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 1>& f, floatx16 (&acc)[TM][TN]) {
+__device__ __forceinline__ void mfma_part(const Frags<TM, TN, 1, 1>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
   for (int c = S0; c < S1; ++c)
 #pragma unroll
@@ -657,10 +667,10 @@ __device__ __forceinline__ void mfma_part(const Frags<TM, TN, 1>& f, floatx16 (&
         acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][c], f.b[u][c], acc[t][u], 0, 0, 0);
 }
 
-template <int TM, int TN>
-__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 0>& f, floatx16 (&acc)[TM][TN]) {
+template <int TM, int TN, int NS>
+__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 0, NS>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
-  for (int s = 0; s < 8; ++s)
+  for (int s = 0; s < 8 * NS; ++s)
 #pragma unroll
     for (int t = 0; t < TM; ++t)
 #pragma unroll
@@ -669,7 +679,7 @@ __device__ __forceinline__ void mfma_half(const Frags<TM, TN, 0>& f, floatx16 (&
 }
 
 template <int TM, int TN>
-__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 1>& f, floatx16 (&acc)[TM][TN]) {
+__device__ __forceinline__ void mfma_half(const Frags<TM, TN, 1, 1>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -677,6 +687,14 @@ __device__ __forceinline__ void mfma_half(const Frags<TM, TN, 1>& f, floatx16 (&
 #pragma unroll
       for (int u = 0; u < TN; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][c], f.b[u][c], acc[t][u], 0, 0, 0);
+}
+
+// A2M_ABLATE = 1: keep the fragments live with one VALU op instead of the MFMAs
+template <class FR, int TM, int TN>
+__device__ __forceinline__ void ablate_touch(const FR& f, floatx16 (&acc)[TM][TN]) {
+  if constexpr (sizeof(f.a[0][0]) == 4)
+    acc[0][0][0] += __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, f.a[0][0]) ^
+                                                  __builtin_bit_cast(uint32_t, f.b[0][0])) * 1e-30f;
 }
 
 // H = false: fp32 operands, v_mfma_f32_32x32x2_f32, BK = 32 (two 16-k halves).
@@ -689,7 +707,9 @@ __device__ __forceinline__ void mfma_half(const Frags<TM, TN, 1>& f, floatx16 (&
 // different order than KS = 1: results agree to fp32 rounding, not bitwise.)
 template <int BM, int BN, int BK, int MA, int MB, int P, int KS = 1>
 __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
-  static_assert(BK == (P == 1 ? 64 : 32), "the k-step pipeline assumes two halves per k-tile");
+  static_assert(P == 0 ? (BK == 32 || BK == 64) : BK == (P == 1 ? 64 : 32),
+                "the k-step pipeline assumes two halves per k-tile");
+  constexpr int NS = P == 0 ? BK / 32 : 1;   // fp32: 16-k fragment chunks per half
   static_assert(KS == 1 || P == 0, "two wave groups: fp32 tiles only");
   constexpr int TM = BM / 64, TN = BN / 64;
   using LA = TileLoader<BM, BK, MA, P>;
@@ -745,7 +765,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
 
   const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
   if constexpr (KS == 1) {
-    Frags<TM, TN, P> f0, f1;
+    Frags<TM, TN, P, NS> f0, f1;
     if (nk > 0) {
       la.load(kbeg);
       lb.load(kbeg);
@@ -757,7 +777,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       }
     }
     __syncthreads();
-    if (nk > 0) read_frags<BM, BN, TM, TN, P, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
+    if (nk > 0) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
     for (int i = 0; i < nk; ++i) {
       const float* cur = lds + (i & 1) * STAGE;
       float* nxt = lds + ((i + 1) & 1) * STAGE;
@@ -766,12 +786,13 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
         lb.store(nxt + LA::TILE);
       }
       __builtin_amdgcn_sched_barrier(0);  // the tile stores stay ahead of the fragment reads
-      if (i + 2 < nk) {
+      if (A2M_ABLATE != 2 && i + 2 < nk) {
         la.load(kbeg + (i + 2) * BK);
         lb.load(kbeg + (i + 2) * BK);
       }
-      read_frags<BM, BN, TM, TN, P, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
-      mfma_half(f0, acc);
+      read_frags<BM, BN, TM, TN, P, NS, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
+      if (A2M_ABLATE != 1) mfma_half(f0, acc);
+      else ablate_touch(f0, acc);
       // The step's barrier, pinned after the first half's MFMAs (left to itself the compiler
       // hoists it above them, and __syncthreads' fence would also wait for the second half's
       // fragment reads).  Only this wave's tile stores must have landed: LDS ops retire in
@@ -779,26 +800,28 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       // second half's MFMAs wait for them where they are used).  s_waitcnt simm16 on gfx950:
       // vmcnt / expcnt at their maxima (no wait), lgkmcnt in bits 11:8.
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(0xC07F | ((2 * (TM + TN)) << 8));
-      __builtin_amdgcn_s_barrier();
+      constexpr int RD = P == 0 ? 2 * NS * (TM + TN) : 2 * (TM + TN);   // fragment reads after the stores
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((RD < 15 ? RD : 15) << 8));
+      if (A2M_ABLATE != 3) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       // the next tile's first fragments are read behind the first MFMAs of this second half
       // (issued right after the barrier they would be waited for before any MFMA: the compiler
       // cannot tell them apart from the second half's own reads in the LDS counter)
       constexpr int SPLIT = P == 1 ? 1 : 2;
-      constexpr int NSUB = P == 0 ? 8 : (P == 1 ? 2 : 6);
-      mfma_part<0, SPLIT>(f1, acc);
+      constexpr int NSUB = P == 0 ? 8 * NS : (P == 1 ? 2 : 6);
+      if (A2M_ABLATE != 1) mfma_part<0, SPLIT>(f1, acc);
       __builtin_amdgcn_sched_barrier(0);
-      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
+      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
       __builtin_amdgcn_sched_barrier(0);
-      mfma_part<SPLIT, NSUB>(f1, acc);
+      if (A2M_ABLATE != 1) mfma_part<SPLIT, NSUB>(f1, acc);
+      else ablate_touch(f1, acc);
     }
     __syncthreads();  // the m-contiguous epilogue reuses the stages
   } else {
     // The groups take turns staging: group j % 2 loads k-tile j three steps ahead and stores it
     // one step ahead, so a tile's global loads have two k-steps to land (one with a single
     // staging group) at no extra registers.
-    Frags<TM, TN, P> f;
+    Frags<TM, TN, P, NS> f;
     if (nk > 0) {
       if (grp == 0) {
         la.load(kbeg);
@@ -815,7 +838,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       }
     }
     __syncthreads();
-    if (nk > 0) read_frags<BM, BN, TM, TN, P, LA, LB>(lds, lds + LA::TILE, grp, wm, wn, li, lh, f);
+    if (nk > 0) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(lds, lds + LA::TILE, grp, wm, wn, li, lh, f);
     for (int i = 0; i < nk; ++i) {
       float* nxt = lds + ((i + 1) & 1) * STAGE;
       if (grp == ((i + 1) & 1)) {
@@ -823,14 +846,15 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
           la.store(nxt);
           lb.store(nxt + LA::TILE);
         }
-        if (i + 3 < nk) {
+        if (A2M_ABLATE != 2 && i + 3 < nk) {
           la.load(kbeg + (i + 3) * BK);
           lb.load(kbeg + (i + 3) * BK);
         }
       }
-      mfma_half(f, acc);
-      __syncthreads();
-      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, LA, LB>(nxt, nxt + LA::TILE, grp, wm, wn, li, lh, f);
+      if (A2M_ABLATE != 1) mfma_half(f, acc);
+      else ablate_touch(f, acc);
+      if (A2M_ABLATE != 3) __syncthreads();
+      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, grp, wm, wn, li, lh, f);
     }
     // sum the two groups' partial accumulators (group 1 -> LDS -> group 0)
     __syncthreads();

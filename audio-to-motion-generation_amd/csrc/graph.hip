@@ -263,9 +263,282 @@ __global__ __launch_bounds__(256, 3) void graph_layer_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused eval graph stack: the decoders' five {GAT | GraphConv} + LN64 + LeakyReLU + residual
+// layers (real_motion_model.py:173-201 body, :225-253 hand; eval: dropout = identity) in ONE
+// launch.  A workgroup keeps its frames' node tile in LDS for the whole stack -- each layer's
+// output overwrites it in place (every lane rewrites only the elements it alone reads) -- so
+// HBM sees the stack input once and its output once instead of five times each, the neighbour
+// lists are built once, and the per-layer launches / attention-projection launches disappear
+// (the GAT projections U = W_h^T att come precomputed, cached per weight version).
+constexpr int GMAXL = 8;
+struct GraphStack {
+  int nlayers;
+  int kind[GMAXL];
+  const float* w0[GMAXL];
+  const float* w1[GMAXL];
+  const float* U[GMAXL];
+  const float* bias[GMAXL];
+  const float* ln_w[GMAXL];
+  const float* ln_b[GMAXL];
+  float slope;
+};
+
+__global__ __launch_bounds__(256, 3) void graph_stack_kernel(
+    const float* __restrict__ x, int F, int J, const int* __restrict__ nbr_ptr,
+    const int* __restrict__ nbr_idx, GraphStack S, float* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) float xs[GMAXN * ZP];
+  __shared__ __attribute__((aligned(16))) float Uk[GF][2 * GHEADS];
+  __shared__ float al[2 * GHEADS][GMAXN];
+  __shared__ __attribute__((aligned(8))) unsigned char nbl[GMAXN][GMAXDEG];
+  __shared__ unsigned char ndeg[GMAXN];
+  __shared__ int csr[2 * GMAXN];
+
+  const int fpb = GMAXN / J;
+  const int NBmax = fpb * J;
+  const int64_t node0 = (int64_t)blockIdx.x * NBmax;
+  const int NB = (int)min<int64_t>(NBmax, (int64_t)F * J - node0);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+
+  const int ne = min(nbr_ptr[J], 2 * GMAXN - (J + 1));
+  {
+    constexpr int NL = GMAXN * (GF / 4) / 256;
+    float4 v[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * 256, n = i / (GF / 4), q = i % (GF / 4);
+      v[j] = n < NB ? *reinterpret_cast<const float4*>(x + (node0 + n) * GF + q * 4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * 256, n = i / (GF / 4), q = i % (GF / 4);
+      *reinterpret_cast<float4*>(xs + n * ZP + q * 4) = v[j];
+    }
+  }
+  for (int i = tid; i < J + 1 + ne; i += blockDim.x) csr[i] = i <= J ? nbr_ptr[i] : nbr_idx[i - (J + 1)];
+  __syncthreads();
+  // block-local in-neighbour lists (edge order; the GAT self loop is appended per layer)
+  for (int n = tid; n < GMAXN; n += blockDim.x) {
+    int d = 0;
+    if (n < NB) {
+      const int f0 = (n / J) * J, ln = n % J;
+      for (int e = csr[ln]; e < csr[ln + 1] && d < GMAXDEG - 1; ++e) nbl[n][d++] = f0 + csr[J + 1 + e];
+    }
+    for (int q = d; q < GMAXDEG; ++q) nbl[n][q] = 0;
+    ndeg[n] = d;
+  }
+  __syncthreads();
+  const int row = wave * 32 + li;
+  const int d0 = ndeg[row];
+  int ids[GMAXDEG];
+  {
+    const uint2 nb = *reinterpret_cast<const uint2*>(&nbl[row][0]);
+#pragma unroll
+    for (int q = 0; q < GMAXDEG; ++q) ids[q] = ((q < 4 ? nb.x : nb.y) >> (8 * (q & 3))) & 0xff;
+  }
+  int idg[GMAXDEG];   // GAT: neighbours + self loop at position d0
+#pragma unroll
+  for (int q = 0; q < GMAXDEG; ++q) idg[q] = q < d0 ? ids[q] : (q == d0 ? row : 0);
+
+  for (int L = 0; L < S.nlayers; ++L) {
+    const int kind = S.kind[L];
+    const int d = kind == 0 ? d0 + 1 : d0;
+    if (kind == 0) {
+      const float* U = S.U[L];
+      for (int i = tid; i < 2 * GHEADS * GF; i += blockDim.x) Uk[i % GF][i / GF] = U[i];
+      __syncthreads();
+      for (int n = tid; n < NB; n += blockDim.x) {
+        const float* xr = xs + n * ZP;
+        float sacc[2 * GHEADS];
+#pragma unroll
+        for (int q = 0; q < 2 * GHEADS; ++q) sacc[q] = 0.f;
+#pragma unroll 4
+        for (int k = 0; k < GF; k += 4) {
+          const float4 xv = *reinterpret_cast<const float4*>(xr + k);
+          const float xk[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float4 u0 = *reinterpret_cast<const float4*>(&Uk[k + j][0]);
+            const float4 u1 = *reinterpret_cast<const float4*>(&Uk[k + j][4]);
+            sacc[0] += xk[j] * u0.x; sacc[1] += xk[j] * u0.y; sacc[2] += xk[j] * u0.z; sacc[3] += xk[j] * u0.w;
+            sacc[4] += xk[j] * u1.x; sacc[5] += xk[j] * u1.y; sacc[6] += xk[j] * u1.z; sacc[7] += xk[j] * u1.w;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 2 * GHEADS; ++q) al[q][n] = sacc[q];
+      }
+      __syncthreads();
+    }
+
+    floatx16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+    const int nseg = kind == 0 ? GHEADS : 2;
+    const float* W0 = S.w0[L];
+    const float* W1 = S.w1[L];
+    auto wseg = [&](int sg) { return kind == 0 ? W0 + (int64_t)sg * GF * GF : (sg == 0 ? W0 : W1); };
+    auto load_b = [&](int sg, int kc, float4 (&bw)[2][2]) {
+      const float* W = wseg(sg);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float* p = W + (t * 32 + li) * GF + kc * 16 + lh * 8;
+        bw[t][0] = *reinterpret_cast<const float4*>(p);
+        bw[t][1] = *reinterpret_cast<const float4*>(p + 4);
+      }
+    };
+    float4 bcur[2][2], bnxt[2][2];
+    load_b(0, 0, bcur);
+    for (int seg = 0; seg < nseg; ++seg) {
+      const bool agg = kind == 0 || seg == 0;
+      float wq[GMAXDEG];
+      int id[GMAXDEG];
+#pragma unroll
+      for (int q = 0; q < GMAXDEG; ++q) id[q] = kind == 0 ? idg[q] : ids[q];
+      if (kind == 0) {
+        const float ad = al[GHEADS + seg][row];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < GMAXDEG; ++q) {
+          const float sv = al[seg][id[q]] + ad;
+          wq[q] = sv > 0.f ? sv : sv * 0.2f;
+          if (q < d) mx = fmaxf(mx, wq[q]);
+        }
+        float den = 0.f;
+#pragma unroll
+        for (int q = 0; q < GMAXDEG; ++q) {
+          wq[q] = q < d ? expf(wq[q] - mx) : 0.f;
+          den += wq[q];
+        }
+        const float inv = 1.f / (den + 1e-16f);
+#pragma unroll
+        for (int q = 0; q < GMAXDEG; ++q) wq[q] *= inv;
+      } else {
+#pragma unroll
+        for (int q = 0; q < GMAXDEG; ++q) wq[q] = q < d ? 1.f : 0.f;
+      }
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc) {
+        if (kc < 3) load_b(seg, kc + 1, bnxt);
+        else if (seg + 1 < nseg) load_b(seg + 1, 0, bnxt);
+        float af[8];
+        if (agg) {
+          float4 v[GMAXDEG][2];
+#pragma unroll
+          for (int q = 0; q < GMAXDEG; ++q) {
+            const float* p = xs + id[q] * ZP + kc * 16 + lh * 8;
+            v[q][0] = *reinterpret_cast<const float4*>(p);
+            v[q][1] = *reinterpret_cast<const float4*>(p + 4);
+          }
+#pragma unroll
+          for (int s8 = 0; s8 < 8; ++s8) af[s8] = 0.f;
+#pragma unroll
+          for (int q = 0; q < GMAXDEG; ++q) {
+            const float w = wq[q];
+            af[0] += w * v[q][0].x; af[1] += w * v[q][0].y; af[2] += w * v[q][0].z; af[3] += w * v[q][0].w;
+            af[4] += w * v[q][1].x; af[5] += w * v[q][1].y; af[6] += w * v[q][1].z; af[7] += w * v[q][1].w;
+          }
+        } else {
+          const float* p = xs + row * ZP + kc * 16 + lh * 8;
+          const float4 v0 = *reinterpret_cast<const float4*>(p);
+          const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
+          af[0] = v0.x; af[1] = v0.y; af[2] = v0.z; af[3] = v0.w;
+          af[4] = v1.x; af[5] = v1.y; af[6] = v1.z; af[7] = v1.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float bf[8] = {bcur[t][0].x, bcur[t][0].y, bcur[t][0].z, bcur[t][0].w,
+                               bcur[t][1].x, bcur[t][1].y, bcur[t][1].z, bcur[t][1].w};
+#pragma unroll
+          for (int s = 0; s < 8; ++s)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          bcur[t][0] = bnxt[t][0];
+          bcur[t][1] = bnxt[t][1];
+        }
+      }
+    }
+    __syncthreads();   // every gather of this layer has read the tile
+
+    // epilogue: out = LReLU(LN(acc * scale + bias)) + x, in place (or to y after the last layer)
+    const float scale = kind == 0 ? 1.f / GHEADS : 1.f;
+    const float* bias = S.bias[L];
+    const float b0 = bias[li], b1 = bias[32 + li];
+    const float lw0 = S.ln_w[L][li], lw1 = S.ln_w[L][32 + li];
+    const float lb0 = S.ln_b[L][li], lb1 = S.ln_b[L][32 + li];
+    const bool last = L + 1 == S.nlayers;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+      const float o0 = acc[0][q] * scale + b0, o1 = acc[1][q] * scale + b1;
+      const float mean = half32_sum(o0 + o1) * (1.f / GF);
+      const float sv = half32_sum((o0 - mean) * (o0 - mean) + (o1 - mean) * (o1 - mean));
+      const float rstd = 1.f / sqrtf(sv * (1.f / GF) + 1e-5f);
+      if (r >= NB) continue;
+      float u0 = (o0 - mean) * rstd * lw0 + lb0, u1 = (o1 - mean) * rstd * lw1 + lb1;
+      u0 = (u0 > 0.f ? u0 : u0 * S.slope) + xs[r * ZP + li];
+      u1 = (u1 > 0.f ? u1 : u1 * S.slope) + xs[r * ZP + 32 + li];
+      if (last) {
+        float* yr = y + (node0 + r) * GF;
+        yr[li] = u0;
+        yr[32 + li] = u1;
+      } else {
+        xs[r * ZP + li] = u0;
+        xs[r * ZP + 32 + li] = u1;
+      }
+    }
+    if (!last) __syncthreads();   // the layer's output is the next layer's tile
+  }
+}
+
 }  // namespace a2m
 
 using namespace a2m;
+
+extern "C" int a2m_graph_att_proj_f32(const float* w0, const float* att_src, const float* att_dst,
+                                      float* U, void* stream) {
+  A2M_CHECK_ARG(w0 && att_src && att_dst && U, "graph_att_proj: null pointer");
+  hipLaunchKernelGGL(graph_att_proj_kernel, dim3(1), dim3(2 * GHEADS * GF), 0, as_stream(stream),
+                     w0, att_src, att_dst, U);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+extern "C" int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
+                                       const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
+                                       const float* const* w0, const float* const* w1,
+                                       const float* const* U, const float* const* bias,
+                                       const float* const* ln_w, const float* const* ln_b,
+                                       float slope, float* y, void* stream) {
+  A2M_CHECK_ARG(x && y && nbr_ptr && nbr_idx && kinds && w0 && w1 && U && bias && ln_w && ln_b,
+                "graph_stack: null pointer");
+  A2M_CHECK_ARG(J > 0 && J <= GMAXN && F >= 0, "graph_stack: bad J=%d", J);
+  A2M_CHECK_ARG(nlayers > 0 && nlayers <= GMAXL, "graph_stack: %d layers (1..%d)", nlayers, GMAXL);
+  A2M_CHECK_ARG(x != y, "graph_stack: in-place not supported");
+  GraphStack S{};
+  S.nlayers = nlayers;
+  S.slope = slope;
+  for (int L = 0; L < nlayers; ++L) {
+    A2M_CHECK_ARG(kinds[L] == 0 || kinds[L] == 1, "graph_stack: layer %d kind %d", L, kinds[L]);
+    A2M_CHECK_ARG(w0[L] && bias[L] && ln_w[L] && ln_b[L] && (kinds[L] == 0 ? U[L] != nullptr : w1[L] != nullptr),
+                  "graph_stack: layer %d parameters missing", L);
+    S.kind[L] = kinds[L];
+    S.w0[L] = w0[L]; S.w1[L] = w1[L]; S.U[L] = U[L];
+    S.bias[L] = bias[L]; S.ln_w[L] = ln_w[L]; S.ln_b[L] = ln_b[L];
+  }
+  if (F == 0) return A2M_OK;
+  const int fpb = GMAXN / J;
+  hipLaunchKernelGGL(graph_stack_kernel, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
+                     x, F, J, nbr_ptr, nbr_idx, S, y);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
 
 extern "C" int a2m_graph_layer_fwd_f32(const float* x, int32_t F, int32_t J, int32_t kind,
                                        int32_t norm_res, const int32_t* nbr_ptr, const int32_t* nbr_idx,

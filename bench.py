@@ -373,6 +373,9 @@ def main():
     ap.add_argument('--batch', type=int, default=64)
     ap.add_argument('--frames', type=int, default=64)
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--branch-graphs', action='store_true',
+                    help='replay a2m.inference.GraphedGenerator (one graph per decoder branch, '
+                         'two streams) instead of one graph with the branches forked inside')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--mode', choices=('infer', 'train'), default='infer')
     ap.add_argument('--sync-bn', action='store_true',
@@ -424,8 +427,18 @@ def main():
 
     step = infer_step(g, wave)
     with torch.no_grad():
-        graph, static_out = capture_step(dev, step) if not args.no_graph else (None, None)
-        run = graph.replay if graph is not None else step
+        graph, static_out = None, None
+        if args.no_graph:
+            run = step
+        elif args.branch_graphs:
+            from a2m.inference import GraphedGenerator
+            from a2m.mel_features import log_mel_batch
+            graph = GraphedGenerator(g, lambda: log_mel_batch(wave))
+            static_out = graph.static['out']
+            run = graph
+        else:
+            graph, static_out = capture_step(dev, step)
+            run = graph.replay
         for _ in range(args.warmup):
             run()
         torch.cuda.synchronize()
@@ -469,7 +482,7 @@ def main():
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32' if args.dtype == 'fp32' else 'bf16',
         'data': 'synthetic 16 kHz speech-like audio, random-init weights',
         'config': {'workload': workload, 'global_batch': B * world, 'seq_len': T,
-                   'parallelism': f'replicas{world}', 'hip_graph': graph is not None},
+                   'parallelism': f'replicas{world}', 'hip_graph': 'none' if graph is None else ('per-branch graphs, two streams' if args.branch_graphs else 'one graph')},
         'roofline': roofline_entry(gt, peak),
         'mel_roofline': {'bound': 'hbm', 'achieved': round(mel_bytes / (mel_ms * 1e-3) / 1e9, 1),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',

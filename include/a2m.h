@@ -184,6 +184,22 @@ int a2m_layernorm_fwd_f32(const float* x, int32_t R, int32_t D, const float* w, 
                           float eps, float* y, int32_t T, int64_t ys_b, int64_t ys_d,
                           int64_t ys_t, float* mean_out, float* rstd_out, void* stream);
 
+/* GAT attention projections U[q][k] = sum_c W_h[c][k] att_q[c] (q < 4: att_src of head q,
+ * q >= 4: att_dst of head q-4) of one GATConv(64, 64, heads=4): the logits a[n][q] = x_n . U[q]
+ * without projecting x.  U: [8][64] device buffer; cache it per weight version. */
+int a2m_graph_att_proj_f32(const float* w0, const float* att_src, const float* att_dst, float* U,
+                           void* stream);
+/* Fused eval graph stack (real_motion_model.py:173-201 body / :225-253 hand, eval mode):
+ * nlayers x { y = LeakyReLU(LayerNorm64(L(x))) + x } with L = GATConv(64,64,heads=4,concat=False)
+ * (kinds[l] = 0: w0 = lin.weight [256][64], U from a2m_graph_att_proj_f32, bias) or GraphConv
+ * (kinds[l] = 1: w0 = lin_rel.weight, w1 = lin_root.weight, bias = lin_rel.bias).  The
+ * per-layer arrays are host arrays of device pointers.  One launch; each workgroup keeps its
+ * frames' node tile in LDS across the layers.  x, y: [F*J][64], distinct. */
+int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
+                            const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
+                            const float* const* w0, const float* const* w1, const float* const* U,
+                            const float* const* bias, const float* const* ln_w,
+                            const float* const* ln_b, float slope, float* y, void* stream);
 /* ---------------------------------------------------------------- skeleton graph layers
  * One fused GNN step of the body / hand decoders (real_motion_model.py:173-201, 225-253):
  *   y = LeakyReLU(LayerNorm64(L(x))) + x

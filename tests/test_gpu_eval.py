@@ -122,3 +122,26 @@ def test_window_batches_match_reference_getitem():
         assert np.array_equal(b['audio/log_mel_512'][k].cpu().numpy(), z[f'c0_item{k}_audio'])
     assert np.allclose(clip.meta(picks), np.stack([z[f'c0_item{k}_meta'] for k in range(len(picks))]),
                        rtol=0, atol=1e-12)
+
+
+def test_graphed_generator_matches_eager(g_state):
+    """a2m.inference.GraphedGenerator (trunk / body / hand / losses graphs on two streams)
+    replays exactly the eager eval forward: same kernels, same order per output -> bitwise."""
+    import torch
+    from a2m.inference import GraphedGenerator
+    from a2m.real_motion_model import SelfAttention_G
+    g = SelfAttention_G(p=0.0)
+    g.load_state_dict(g_state, strict=False)
+    g = g.to('cuda').eval()
+    torch.manual_seed(0)
+    audio = torch.randn(4, 64, 128, device='cuda')
+    with torch.no_grad():
+        ref, ref_losses = g(audio)
+        src = torch.empty_like(audio)
+        runner = GraphedGenerator(g, lambda: src)
+        for seed in (1, 2):
+            src.copy_(audio if seed == 1 else audio.flip(0))
+            out, losses = runner()
+            want, want_l = (ref, ref_losses) if seed == 1 else g(audio.flip(0))
+            assert torch.equal(out, want)
+            assert torch.equal(losses[0], want_l[0])

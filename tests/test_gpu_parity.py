@@ -316,6 +316,42 @@ def test_graph_layers_vs_oracle(part, J, lo):
     assert rel_err(out.cpu(), ref) < TOL
 
 
+@pytest.mark.parametrize('part,J,lo', [('body', 10, 0), ('hand', 42, 10)])
+def test_graph_stack_vs_oracle(part, J, lo):
+    """The fused 5-layer eval stack (a2m_graph_stack_fwd_f32: GAT, GraphConv, GAT, GraphConv,
+    GAT, each + LN64 + LeakyReLU + residual, node tile resident in LDS) against the oracle's
+    layer-by-layer PyG restatement, on a frame count that leaves a partial last workgroup."""
+    from a2m import functional as F
+    from a2m import skeleton as S
+    from oracle import model as OM
+    Fr = 29
+    x = _rand(Fr * J, 64, seed=80)
+    ei = S.edge_index(lo, J)
+    edges = OM.expand_edges(ei, J, Fr)
+    ptr, idx = S.in_neighbour_csr(ei, J)
+    dv = lambda t: t.to(DEV)  # noqa: E731
+    ref, layers = x, []
+    for L in range(5):
+        lnw, lnb = _rand(64, seed=90 + L).abs() + .5, _rand(64, seed=95 + L, scale=0.1)
+        if L % 2 == 0:
+            lw, asrc, adst, bias = _rand(256, 64, seed=100 + L, scale=0.15), \
+                _rand(1, 4, 64, seed=110 + L, scale=0.3), _rand(1, 4, 64, seed=120 + L, scale=0.3), \
+                _rand(64, seed=130 + L, scale=0.1)
+            g = OM._gat_fn(ref, edges, lw, asrc, adst, bias, 4)
+            U = F.graph_att_proj(dv(lw), dv(asrc), dv(adst))
+            layers.append((0, dv(lw), None, U, dv(bias), dv(lnw), dv(lnb)))
+        else:
+            wr, br, wo = _rand(64, 64, seed=140 + L, scale=0.12), _rand(64, seed=150 + L, scale=0.1), \
+                _rand(64, 64, seed=160 + L, scale=0.12)
+            g = OM.graph_conv(OM.Ctx({'g.lin_rel.weight': wr, 'g.lin_rel.bias': br,
+                                      'g.lin_root.weight': wo}), 'g', ref, edges)
+            layers.append((1, dv(wr), dv(wo), None, dv(br), dv(lnw), dv(lnb)))
+        ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(g, (64,), lnw, lnb), 0.2) + ref
+    out = F.graph_stack(dv(x), J, dv(ptr), dv(idx), layers)
+    e = rel_err(out.cpu(), ref)
+    assert e < TOL, e
+
+
 def test_pose_losses_vs_reference():
     from a2m import functional as F
     z = golden('losses.npz')
