@@ -190,6 +190,39 @@ def conv2d(x, w, b=None, stride=1, pad=(0, 0), bn=None, act=ACT_NONE, slope=0.2,
     return out
 
 
+def conv2d_nhwc_packed(w, cache=None):
+    """[Co][kh][kw][Ci] conv2d weights (a2m_conv2d_pack_nhwc_f32), cached per weight version."""
+    key = _wkey((w,))
+    if cache is not None and cache.get('key') == key:
+        return cache['w']
+    Co, Ci, kh, kw = w.shape
+    packed = torch.empty(Co * kh * kw * Ci, device=w.device)
+    N.check(N.lib.a2m_conv2d_pack_nhwc_f32(_p(w), Co, Ci, kh, kw, _p(packed), _stream()))
+    if cache is not None:
+        cache.update(key=key, w=packed)
+    return packed
+
+
+def conv2d_nhwc(x, w, b=None, stride=1, pad=(0, 0), bn=None, act=ACT_NONE, slope=0.2, cols=None,
+                out_nhwc=True, cache=None):
+    """Channels-last conv2d: x contiguous NHWC [B, H, W, Ci], w [Co, Ci, kh, kw] (packed and
+    cached in `cache`); returns NHWC [B, Ho, Wo, Co] (or NCHW with out_nhwc=False) with only
+    the output columns cols = (lo, hi) computed."""
+    _check_dev(x, w, b)
+    assert x.is_contiguous() and w.is_contiguous()
+    B, H, W, Ci = x.shape
+    Co, _, kh, kw = w.shape
+    ph, pw = pad
+    Ho, Wo = (H + 2 * ph - kh) // stride + 1, (W + 2 * pw - kw) // stride + 1
+    lo, hi = cols if cols is not None else (0, Wo)
+    packed = conv2d_nhwc_packed(w, cache)
+    out = torch.empty((B, Ho, Wo, Co) if out_nhwc else (B, Co, Ho, Wo), device=x.device, dtype=x.dtype)
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_conv2d_nhwc_fwd_f32(
+        _p(x), B, Ci, H, W, _p(packed), _p(b), Co, kh, kw, stride, ph, pw, *_bn_args(bn), act,
+        slope, _p(out), int(out_nhwc), Ho, Wo, lo, hi, wp, wn, _stream()))
+    return out
+
+
 def interp_time(x, T, out=None):
     _check_dev(x)
     assert x.is_contiguous()

@@ -87,6 +87,7 @@ class ConvNormRelu(nn.Module):
         self.leaky = leaky
         self.p = p
         self._tap = {}   # tap-chunked weights for the eval path (functional.conv1d_tap_packed)
+        self._nhwc = {}  # [Co][kh][kw][Ci] weights for the channels-last encoder chain
         if type == '1d':
             self.conv = nn.Conv1d(in_channels, out_channels, kernel_size, stride, padding)
             self.norm = nn.BatchNorm1d(out_channels)
@@ -192,6 +193,9 @@ class ConvTranspose1D(nn.Module):
                          act=F.ACT_RELU, out=out, cache=self._pack)
 
 
+_ENC_NHWC = __import__('os').environ.get('A2M_ENC_NHWC', '1') != '0'
+
+
 class AudioEncoder(nn.Module):
     def __init__(self, output_feats=64, input_channels=1, kernel_size=None, stride=None, p=0, groups=1):
         super().__init__()
@@ -233,11 +237,27 @@ class AudioEncoder(nn.Module):
             time_steps = x.shape[-2]
         if _grad_path(self, x):
             return _autograd().audio_encoder(self, x, time_steps)
-        h = x.contiguous().unsqueeze(1)
         cols = self.live_columns(x.shape[-1])
-        for layer, c in zip(self.conv, cols):
-            h = layer(h, cols=c)
+        nhwc = [_ENC_NHWC and self._nhwc_layer(i) for i in range(len(self.conv))]
+        # the mel [B, T, F] is NHWC with C = 1 and NCHW with the channel unsqueezed, for free
+        h = x.contiguous().unsqueeze(-1 if nhwc[0] else 1)
+        for i, (layer, c) in enumerate(zip(self.conv, cols)):
+            if nhwc[i]:
+                k, s, p = layer.geometry()
+                out_nhwc = i + 1 < len(self.conv) and nhwc[i + 1]
+                h = F.conv2d_nhwc(h, layer.conv.weight, layer.conv.bias, s, tuple(p),
+                                  bn=layer.bn_eval(), act=layer.act, cols=c, out_nhwc=out_nhwc,
+                                  cache=layer._nhwc)
+            else:
+                h = layer(h, cols=c)
         return F.interp_time(h, time_steps)
+
+    def _nhwc_layer(self, i):
+        """Channels-last where the NCHW path would gather its operand element by element
+        (K < 2048: conv0, conv1; tools/enc_layers.py: conv1 115 -> 89 us); the deeper layers
+        keep im2col + dense GEMM, which measured faster than the mode-4 runs there."""
+        w = self.conv[i].conv.weight
+        return w.shape[1] * w.shape[2] * w.shape[3] < 2048 and (w.shape[1] * w.shape[3]) % 4 == 0
 
 
 class UNet1D(nn.Module):

@@ -173,8 +173,8 @@ struct TileLoader {
   const Gather* g;
   const float* base;
   int K;
-  RowInfo ri[MODE == 2 || MODE >= 3 ? 1 : NPASS];
-  int lrow[MODE == 2 || MODE >= 3 ? 1 : NPASS];
+  RowInfo ri[MODE == 2 || MODE == 3 || MODE == 5 ? 1 : NPASS];
+  int lrow[MODE == 2 || MODE == 3 || MODE == 5 ? 1 : NPASS];
   int kq;  // k offset of this thread inside the tile
   int nrow;  // mode 3: rows of this group that exist (0..4)
   int rdim;   // mode 3: 0 rows via r0, 1 rows along h, 2 rows along w

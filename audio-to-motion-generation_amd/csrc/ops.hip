@@ -618,6 +618,20 @@ __global__ __launch_bounds__(256) void im2col2d_kernel(const float* __restrict__
   }
 }
 
+// Conv2d weights [Co][Ci][kh][kw] -> [Co][kh][kw][Ci] (the k order of the NHWC operand)
+__global__ void conv2d_pack_nhwc_kernel(const float* w, int Co, int Ci, int kh, int kw, float* out) {
+  const int64_t total = (int64_t)Co * Ci * kh * kw;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(i % kw);
+    int64_t t = i / kw;
+    const int r = (int)(t % kh);
+    t /= kh;
+    const int ci = (int)(t % Ci), co = (int)(t / Ci);
+    out[(((int64_t)co * kh + r) * kw + j) * Ci + ci] = w[i];
+  }
+}
+
 int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
                        const float* w, const float* bias, int32_t Co, int32_t kh, int32_t kw,
                        int32_t stride, int32_t pad_h, int32_t pad_w, const float* bn_w,
@@ -664,6 +678,57 @@ int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t
   Bg.sh = W; Bg.sw = 1; Bg.kcontig = 0;
   Epilogue E = epi_bn(y + w_lo, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
   E.N1 = Hout; E.N2 = Wn; E.so0 = Co * Hout * Wout; E.so1 = Wout; E.so2 = 1; E.som = Hout * Wout;
+  return gemm(A, Bg, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, as_stream(stream));
+}
+
+int a2m_conv2d_pack_nhwc_f32(const float* w, int32_t Co, int32_t Ci, int32_t kh, int32_t kw,
+                             float* packed, void* stream) {
+  A2M_CHECK_ARG(w && packed && Co > 0 && Ci > 0 && kh > 0 && kw > 0, "conv2d_pack_nhwc: bad args");
+  A2M_CHECK_ARG(fits32((int64_t)Co * Ci * kh * kw), "conv2d_pack_nhwc: too large");
+  hipLaunchKernelGGL(conv2d_pack_nhwc_kernel,
+                     dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Co * Ci * kh * kw, 256), 8192)),
+                     dim3(256), 0, as_stream(stream), w, Co, Ci, kh, kw, packed);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
+                            const float* packed, const float* bias, int32_t Co, int32_t kh,
+                            int32_t kw, int32_t stride, int32_t pad_h, int32_t pad_w,
+                            const float* bn_w, const float* bn_b, const float* bn_rm,
+                            const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
+                            int32_t y_nhwc, int32_t Hout, int32_t Wout, int32_t w_lo, int32_t w_hi,
+                            void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && packed && y, "conv2d_nhwc: null pointer");
+  A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && kh > 0 && kw > 0 && stride > 0,
+                "conv2d_nhwc: bad shape");
+  A2M_CHECK_ARG(Hout == (H + 2 * pad_h - kh) / stride + 1 && Wout == (W + 2 * pad_w - kw) / stride + 1,
+                "conv2d_nhwc: output geometry mismatch");
+  A2M_CHECK_ARG(0 <= w_lo && w_lo < w_hi && w_hi <= Wout, "conv2d_nhwc: bad column range [%d,%d)",
+                w_lo, w_hi);
+  A2M_CHECK_ARG((kw * Ci) % 4 == 0 && (reinterpret_cast<uintptr_t>(x) % 4) == 0,
+                "conv2d_nhwc: kw * Ci = %d must be a multiple of 4", kw * Ci);
+  A2M_CHECK_ARG(fits32((int64_t)B * Ci * H * W) && fits32((int64_t)B * Co * Hout * Wout),
+                "conv2d_nhwc: too large");
+  const int Wn = w_hi - w_lo;
+  Gather A = dense_rk(packed, Ci * kh * kw);
+  // rows n = (b, ho, wo - w_lo), k = (i, j, ci): the input element x[b][ho*s - ph + i]
+  // [(w_lo + wo)*s - pw + j][ci] sits at w' = win * Ci + ci along the fused (w, c) axis, so the
+  // inner k digit (j, ci) is a unit-stride run of kw * Ci floats (loader mode 4, float4 loads)
+  Gather Bg{};
+  Bg.base = x; Bg.bstride = 0; Bg.sr0 = H * W * Ci;
+  Bg.R1 = Hout; Bg.R2 = Wn; Bg.ar1 = stride; Bg.ar2 = stride * Ci;
+  Bg.sk0 = 0; Bg.K1 = kh; Bg.K2 = kw * Ci; Bg.bk1 = 1; Bg.bk2 = 1;
+  Bg.ch = -pad_h; Bg.cw = (w_lo * stride - pad_w) * Ci; Bg.divh = Bg.divw = 1;
+  Bg.Lh = H; Bg.Lw = W * Ci; Bg.sh = W * Ci; Bg.sw = 1; Bg.kcontig = 1;
+  Epilogue E;
+  if (y_nhwc) {
+    E = epi_bn(y + (int64_t)w_lo * Co, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+    E.N1 = Hout; E.N2 = Wn; E.so0 = Hout * Wout * Co; E.so1 = Wout * Co; E.so2 = Co; E.som = 1;
+  } else {
+    E = epi_bn(y + w_lo, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+    E.N1 = Hout; E.N2 = Wn; E.so0 = Co * Hout * Wout; E.so1 = Wout; E.so2 = 1; E.som = Hout * Wout;
+  }
   return gemm(A, Bg, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, as_stream(stream));
 }
 

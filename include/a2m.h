@@ -112,6 +112,21 @@ int a2m_convt1d_packed_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32
                                const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
                                int64_t ys_b, int64_t ys_c, void* ws, size_t ws_bytes, void* stream);
 
+/* Channels-last conv2d for the AudioEncoder eval chain (model_layers.py:219-280,
+ * ConvNormRelu(type='2d') layers): x NHWC [B][H][W][Ci] (the mel [B][T][F] is already NHWC with
+ * Ci = 1), weights packed once by a2m_conv2d_pack_nhwc_f32 as [Co][kh][kw][Ci], output NHWC
+ * [B][Hout][Wout][Co] (y_nhwc = 1) or NCHW (0), only columns [w_lo, w_hi) computed.  The GEMM's
+ * activation operand is a unit-stride run of kw*Ci floats per (row, kernel row) -- float4 loads,
+ * no im2col matrix and no transposed staging.  Requires (kw * Ci) % 4 == 0. */
+int a2m_conv2d_pack_nhwc_f32(const float* w, int32_t Co, int32_t Ci, int32_t kh, int32_t kw,
+                             float* packed, void* stream);
+int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
+                            const float* packed, const float* bias, int32_t Co, int32_t kh,
+                            int32_t kw, int32_t stride, int32_t pad_h, int32_t pad_w,
+                            const float* bn_w, const float* bn_b, const float* bn_rm,
+                            const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
+                            int32_t y_nhwc, int32_t Hout, int32_t Wout, int32_t w_lo, int32_t w_hi,
+                            void* ws, size_t ws_bytes, void* stream);
 /* AudioEncoder's Conv2d ConvNormRelu layers (model_layers.py:219-276) on contiguous
  * [B][Ci][H][W] -> [B][Co][Hout][Wout].  Only output columns [w_lo, w_hi) are computed
  * (the encoder's dead-column pruning); the rest of y is untouched. */

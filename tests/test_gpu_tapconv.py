@@ -125,3 +125,27 @@ def test_bf16x6_generator_eval_golden(g_state):
         pose, _ = g(torch.from_numpy(z['audio']).to(DEV))
     e = rel_err(pose.cpu(), z["pose"])
     assert e < 1e-4, e
+
+
+@pytest.mark.parametrize('B,Ci,Co,H,W,k,s,p,cols', [
+    (4, 1, 64, 64, 128, (4, 4), 2, (1, 1), (9, 55)),      # encoder conv0 (mel, Ci = 1)
+    (3, 64, 128, 32, 64, (4, 4), 2, (1, 1), (5, 27)),     # conv1
+    (2, 256, 512, 8, 16, (3, 3), 1, (1, 1), (4, 12)),     # conv3
+    (2, 512, 256, 8, 8, (3, 8), 1, (1, 0), (0, 1)),       # conv4 (3 x 8 kernel, W_out = 1)
+    (2, 12, 20, 9, 11, (3, 3), 2, (1, 1), None)])
+@pytest.mark.parametrize('out_nhwc', [True, False])
+def test_conv2d_nhwc_matches_fp64(B, Ci, Co, H, W, k, s, p, cols, out_nhwc):
+    """Channels-last conv2d (a2m_conv2d_nhwc_fwd_f32: activation operand as unit-stride runs of
+    kw*Ci floats, loader mode 4) against an fp64 convolution, on the computed column range."""
+    from a2m import functional as F
+    g = torch.Generator().manual_seed(B + Ci + Co + H)
+    x = torch.randn(B, Ci, H, W, generator=g)
+    w = torch.randn(Co, Ci, *k, generator=g) / np.sqrt(Ci * k[0] * k[1])
+    b = torch.randn(Co, generator=g)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride=s, padding=p)
+    lo, hi = cols if cols is not None else (0, ref.shape[-1])
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    y = F.conv2d_nhwc(xn, w.to(DEV), b.to(DEV), s, p, cols=cols, out_nhwc=out_nhwc, cache={})
+    y = (y.permute(0, 3, 1, 2) if out_nhwc else y).cpu().double()
+    e = rel_err(y[..., lo:hi], ref[..., lo:hi])
+    assert e < TOL32, e

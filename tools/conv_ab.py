@@ -39,19 +39,24 @@ def graph_time(fn, iters=20, reps=3):
     return e0.elapsed_time(e1) * 1e3 / (reps * iters)
 
 
-for B, Ci, Co, T in SHAPES:
-    x = torch.randn(B, Ci, T, device=dev)
-    w = torch.randn(Co, Ci, 3, device=dev) / (3 * Ci) ** 0.5
-    b = torch.randn(Co, device=dev)
-    y = torch.empty(B, Co, T, device=dev)
-    ref = torch.nn.functional.conv1d(x.double().cpu(), w.double().cpu(), b.double().cpu(), padding=1)
-    flops = 2.0 * B * T * Co * Ci * 3
-    for prec in PRECS:
-        a2m.set_gemm_precision(prec)
-        for name, cache in (('im2col', None), ('tap', {})):
-            us = graph_time(lambda: F.conv1d(x, w, b, 1, 1, act=F.ACT_LRELU, out=y, cache=cache))
-            F.conv1d(x, w, b, 1, 1, out=y, cache=cache)
-            err = ((y.double().cpu() - ref).abs().max() / ref.abs().max()).item()
-            print(f'conv B={B} Ci={Ci} Co={Co} T={T} {prec:6s} {name:6s}: {us:7.1f} us '
-                  f'{flops / us / 1e6:6.1f} TF  rel err {err:.1e}', flush=True)
-a2m.set_gemm_precision('fp32')
+def main():
+    for B, Ci, Co, T in SHAPES:
+        x = torch.randn(B, Ci, T, device=dev)
+        w = torch.randn(Co, Ci, 3, device=dev) / (3 * Ci) ** 0.5
+        b = torch.randn(Co, device=dev)
+        y = torch.empty(B, Co, T, device=dev)
+        ref = torch.nn.functional.conv1d(x.double().cpu(), w.double().cpu(), b.double().cpu(), padding=1)
+        flops = 2.0 * B * T * Co * Ci * 3
+        for prec in PRECS:
+            a2m.set_gemm_precision(prec)
+            for name, cache in (('im2col', None), ('tap', {})):
+                us = graph_time(lambda: F.conv1d(x, w, b, 1, 1, act=F.ACT_LRELU, out=y, cache=cache))
+                F.conv1d(x, w, b, 1, 1, out=y, cache=cache)
+                err = ((y.double().cpu() - ref).abs().max() / ref.abs().max()).item()
+                print(f'conv B={B} Ci={Ci} Co={Co} T={T} {prec:6s} {name:6s}: {us:7.1f} us '
+                      f'{flops / us / 1e6:6.1f} TF  rel err {err:.1e}', flush=True)
+    a2m.set_gemm_precision('fp32')
+
+
+if __name__ == '__main__':
+    main()
