@@ -97,32 +97,44 @@ def bn_cancelled(name):
         re.fullmatch(r'conv[123](\.\d)?\.(0|4|9)\.bias', name) is not None
 
 
-def test_train_step_oracle(g_state, d_state):
-    """One G-step + D-step in train mode (BN batch stats, p=0): losses and grads."""
+@pytest.mark.parametrize('fixture', ['train_step_b16t64', 'train_step_b2t64'])
+def test_train_step_oracle(fixture, g_state, d_state):
+    """One G-step in train mode (BN batch stats, p=0, version5_model_train.py:350-390): the
+    oracle's outputs against the reference's, its gradients against the exact (fp64) gradient
+    at the fixture's sampled indices, bounded by the reference's own fp32 error there.  The
+    step is ill-conditioned in fp32: two fp32 runs with different summation
+    orders (another CPU's BLAS kernels, another thread count) differ by ~0.5 % on some
+    gradients, so the reference's fp32 values are not a fixed target, the exact gradient is."""
     from oracle import model
-    z = golden('g_eval_b2t64.npz')
-    t = golden('train_step_b2t64.npz')
+    t = golden(fixture + '.npz')
+    f64 = golden(fixture + '_f64.npz')
+    z = t if 'audio' in t.files else golden('g_eval_b2t64.npz')
     gs = {k: v.clone().requires_grad_(v.is_floating_point() and 'running' not in k) for k, v in g_state.items()}
     ds = {k: v.clone().requires_grad_(v.is_floating_point() and 'running' not in k) for k, v in d_state.items()}
     audio, pose = torch.from_numpy(z['audio']), torch.from_numpy(z['real_pose'])
+    B = audio.shape[0]
     fake, internal = model.generator(gs, audio, real_pose=pose, train=True)
     fd = model.discriminator(ds, torch.diff(fake, dim=1), train=True)
     l1, sm, jk = model.motion_terms(pose, fake)
-    adv = torch.nn.functional.mse_loss(fd, torch.full((2, 4), 0.93))
+    adv = torch.nn.functional.mse_loss(fd, torch.full((B, 4), 0.93))
     loss = l1 + adv + 0.1 * sm + 0.05 * jk + internal[0] + internal[1]
     assert rel_err(fake.detach(), t['fake_pose']) < 1e-4
     assert rel_err(loss.detach(), t['G_loss']) < 1e-5
     loss.backward()
-    names = list(t['gG_names'])
-    for i, n in enumerate(names):
+    e, r = [], []
+    for i, n in enumerate(t['gG_names']):
         if bn_cancelled(n):
             continue
         g = gs[n].grad.double().reshape(-1).numpy()
         ix = t['gG_idx'][i]
         ok = ix >= 0
-        ref = t['gG_val'][i][ok]
-        scale = max(np.sqrt(t['gG_sumsq'][i] / max(g.size, 1)), np.abs(ref).max(), 1e-12)
-        assert np.abs(g[ix[ok]] - ref).max() / scale < 2e-3, n
+        exact = f64['gG_val'][i][ok]
+        scale = max(np.abs(exact).max(), 1e-30)
+        e.append(np.abs(g[ix[ok]] - exact).max() / scale)
+        r.append(np.abs(t['gG_val'][i][ok] - exact).max() / scale)
+    e, r = np.array(e), np.array(r)
+    assert np.median(e) <= 2.0 * np.median(r), (np.median(e), np.median(r))
+    assert np.all(e <= np.maximum(0.05, 8.0 * r)), e.max()
 
 
 def test_eval_norm_oracle_vs_reference():
