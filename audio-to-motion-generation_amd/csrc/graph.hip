@@ -271,6 +271,16 @@ __global__ __launch_bounds__(256, 3) void graph_layer_kernel(
 // HBM sees the stack input once and its output once instead of five times each, the neighbour
 // lists are built once, and the per-layer launches / attention-projection launches disappear
 // (the GAT projections U = W_h^T att come precomputed, cached per weight version).
+//
+// Work layout (differs from graph_layer_kernel):
+//  * MFMA rows are the block's nodes sorted by in-degree, the 32 heaviest (hand wrists: 5 in-edges
+//    + self loop) in one wave, rotated over the four waves by block so each SIMD gets its share;
+//    every wave gathers only up to its own rows' maximum degree (wave-uniform bound), not the
+//    GMAXDEG slots of the skeleton-wide maximum (hand: 2.9 gathers a row on average, not 8);
+//  * one gather of a neighbour's k-slice feeds all heads: the four GAT heads' edge softmaxes
+//    are held in registers and each gathered float4 is weighted four times, so the LDS gather
+//    traffic of a GAT layer is a quarter of the per-head loop's;
+//  * the logits x . U are computed by all 256 threads (two per node, four logits each).
 constexpr int GMAXL = 8;
 struct GraphStack {
   int nlayers;
@@ -284,14 +294,121 @@ struct GraphStack {
   float slope;
 };
 
-__global__ __launch_bounds__(256, 3) void graph_stack_kernel(
+// The k loop of one layer for a wave whose rows have at most DL gather slots (compile-time, so
+// the gathered slices and edge weights stay in registers): 8 steps of k = 8 (4 per lane half);
+// each gathered float4 is weighted for every segment, then 8 MFMAs per segment.  B fragments
+// (64 output channels) come from L2 one step ahead.
+__device__ __forceinline__ void stack_load_b(const float* W0, const float* W1, bool gat, int st, int li,
+                                             int lh, float4 (&bw)[GHEADS][2]) {
+  const int off = (st >> 1) * 16 + lh * 8 + (st & 1) * 4;
+#pragma unroll
+  for (int h = 0; h < GHEADS; ++h) {
+    if (!gat && h >= 2) break;
+    const float* W = gat ? W0 + (int64_t)h * GF * GF : (h == 0 ? W0 : W1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) bw[h][t] = *reinterpret_cast<const float4*>(W + (t * 32 + li) * GF + off);
+  }
+}
+
+__device__ __forceinline__ void stack_mfma4(const float (&af)[4], const float4 (&b)[2], floatx16 (&acc)[2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const float bf[4] = {b[t].x, b[t].y, b[t].z, b[t].w};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
+  }
+}
+
+template <int DL, bool GAT>
+__device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)[GMAXN], const int (&id)[GMAXDEG],
+                                              int node, int d0, const float* W0, const float* W1, int li,
+                                              int lh, floatx16 (&acc)[2]) {
+  constexpr int NS = GAT ? GHEADS : 1;   // aggregated segments (GraphConv: + the root term)
+  float wq[NS][DL];
+  if (GAT) {  // edge softmax per head over the in-edges + self loop (slot d0; PyG: LeakyReLU 0.2)
+    const int d = d0 + 1;
+#pragma unroll
+    for (int h = 0; h < NS; ++h) {
+      const float ad = al[GHEADS + h][node];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < DL; ++q) {
+        const float sv = al[h][id[q]] + ad;
+        wq[h][q] = sv > 0.f ? sv : sv * 0.2f;
+        if (q < d) mx = fmaxf(mx, wq[h][q]);
+      }
+      float den = 0.f;
+#pragma unroll
+      for (int q = 0; q < DL; ++q) {
+        wq[h][q] = q < d ? expf(wq[h][q] - mx) : 0.f;
+        den += wq[h][q];
+      }
+      const float inv = 1.f / (den + 1e-16f);
+#pragma unroll
+      for (int q = 0; q < DL; ++q) wq[h][q] *= inv;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < DL; ++q) wq[0][q] = q < d0 ? 1.f : 0.f;
+  }
+  float4 bc[GHEADS][2], bn[GHEADS][2];
+  stack_load_b(W0, W1, GAT, 0, li, lh, bc);
+#pragma unroll 1
+  for (int st = 0; st < 8; ++st) {
+    if (st < 7) stack_load_b(W0, W1, GAT, st + 1, li, lh, bn);
+    const int off = (st >> 1) * 16 + lh * 8 + (st & 1) * 4;
+    float af[NS][4];
+#pragma unroll
+    for (int h = 0; h < NS; ++h) af[h][0] = af[h][1] = af[h][2] = af[h][3] = 0.f;
+#pragma unroll
+    for (int q = 0; q < DL; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(xs + id[q] * ZP + off);
+#pragma unroll
+      for (int h = 0; h < NS; ++h) {
+        const float w = wq[h][q];
+        af[h][0] += w * v.x; af[h][1] += w * v.y; af[h][2] += w * v.z; af[h][3] += w * v.w;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < NS; ++h) stack_mfma4(af[h], bc[h], acc);
+    if (!GAT) {
+      const float4 o = *reinterpret_cast<const float4*>(xs + node * ZP + off);   // root term
+      const float ao[4] = {o.x, o.y, o.z, o.w};
+      stack_mfma4(ao, bc[1], acc);
+    }
+#pragma unroll
+    for (int h = 0; h < GHEADS; ++h) {
+      bc[h][0] = bn[h][0];
+      bc[h][1] = bn[h][1];
+    }
+  }
+}
+
+template <bool GAT>
+__device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, const float (*al)[GMAXN],
+                                                     const int (&id)[GMAXDEG], int node, int d0, const float* W0,
+                                                     const float* W1, int li, int lh, floatx16 (&acc)[2]) {
+  switch (dl) {
+    case 1: stack_layer_k<1, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 2: stack_layer_k<2, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 3: stack_layer_k<3, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 4: stack_layer_k<4, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 5: stack_layer_k<5, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 6: stack_layer_k<6, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 7: stack_layer_k<7, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    default: stack_layer_k<8, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void graph_stack_kernel(
     const float* __restrict__ x, int F, int J, const int* __restrict__ nbr_ptr,
     const int* __restrict__ nbr_idx, GraphStack S, float* __restrict__ y) {
-  __shared__ __attribute__((aligned(16))) float xs[GMAXN * ZP];
+  __shared__ __attribute__((aligned(16))) float xs[GMAXN * ZP];        // node-indexed tile
   __shared__ __attribute__((aligned(16))) float Uk[GF][2 * GHEADS];
-  __shared__ float al[2 * GHEADS][GMAXN];
+  __shared__ float al[2 * GHEADS][GMAXN];                              // node-indexed logits
   __shared__ __attribute__((aligned(8))) unsigned char nbl[GMAXN][GMAXDEG];
   __shared__ unsigned char ndeg[GMAXN];
+  __shared__ unsigned char rown[GMAXN];                                // MFMA row -> node (0xff: none)
   __shared__ int csr[2 * GMAXN];
 
   const int fpb = GMAXN / J;
@@ -320,7 +437,7 @@ __global__ __launch_bounds__(256, 3) void graph_stack_kernel(
   }
   for (int i = tid; i < J + 1 + ne; i += blockDim.x) csr[i] = i <= J ? nbr_ptr[i] : nbr_idx[i - (J + 1)];
   __syncthreads();
-  // block-local in-neighbour lists (edge order; the GAT self loop is appended per layer)
+  // block-local in-neighbour lists (edge order; the GAT self loop is added per layer)
   for (int n = tid; n < GMAXN; n += blockDim.x) {
     int d = 0;
     if (n < NB) {
@@ -329,48 +446,81 @@ __global__ __launch_bounds__(256, 3) void graph_stack_kernel(
     }
     for (int q = d; q < GMAXDEG; ++q) nbl[n][q] = 0;
     ndeg[n] = d;
+    rown[n] = 0xff;
   }
   __syncthreads();
-  const int row = wave * 32 + li;
-  const int d0 = ndeg[row];
+  // rows sorted by degree (descending; stable), the heaviest 32 in wave blockIdx & 3
+  for (int n = tid; n < NB; n += blockDim.x) {
+    const int d = ndeg[n];
+    int pos = 0;
+    for (int m = 0; m < NB; ++m) {
+      const int dm = ndeg[m];
+      pos += (dm > d) || (dm == d && m < n);
+    }
+    rown[((((pos >> 5) + blockIdx.x) & 3) << 5) | (pos & 31)] = (unsigned char)n;
+  }
+  __syncthreads();
+  const int rn = rown[wave * 32 + li];
+  const bool live = rn != 0xff;
+  const int node = live ? rn : 0;
+  const int d0 = live ? ndeg[node] : 0;
   int ids[GMAXDEG];
   {
-    const uint2 nb = *reinterpret_cast<const uint2*>(&nbl[row][0]);
+    const uint2 nb = *reinterpret_cast<const uint2*>(&nbl[node][0]);
 #pragma unroll
-    for (int q = 0; q < GMAXDEG; ++q) ids[q] = ((q < 4 ? nb.x : nb.y) >> (8 * (q & 3))) & 0xff;
+    for (int q = 0; q < GMAXDEG; ++q) ids[q] = live ? ((q < 4 ? nb.x : nb.y) >> (8 * (q & 3))) & 0xff : 0;
   }
-  int idg[GMAXDEG];   // GAT: neighbours + self loop at position d0
+  int idg[GMAXDEG];   // in-neighbours, then the GAT self loop at slot d0 (weight 0 in GraphConv)
 #pragma unroll
-  for (int q = 0; q < GMAXDEG; ++q) idg[q] = q < d0 ? ids[q] : (q == d0 ? row : 0);
+  for (int q = 0; q < GMAXDEG; ++q) idg[q] = q < d0 ? ids[q] : (q == d0 ? node : 0);
+  // wave-uniform gather bound: the largest in-degree among this wave's rows
+  int dw = d0;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) dw = max(dw, __shfl_xor(dw, o));
+  dw = __builtin_amdgcn_readfirstlane(dw);
+  // epilogue rows r = 32 wave + (q & 3) + 8 (q >> 2) + 4 lh  ->  their nodes, one byte each
+  unsigned en[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    en[j] = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int q = 4 * j + b;
+      en[j] |= (unsigned)rown[wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh] << (8 * b);
+    }
+  }
 
   for (int L = 0; L < S.nlayers; ++L) {
     const int kind = S.kind[L];
-    const int d = kind == 0 ? d0 + 1 : d0;
-    if (kind == 0) {
+    const bool gat = kind == 0;
+    int dl;                      // wave-uniform number of gather slots this layer
+    if (gat) {
       const float* U = S.U[L];
       for (int i = tid; i < 2 * GHEADS * GF; i += blockDim.x) Uk[i % GF][i / GF] = U[i];
       __syncthreads();
-      for (int n = tid; n < NB; n += blockDim.x) {
-        const float* xr = xs + n * ZP;
-        float sacc[2 * GHEADS];
-#pragma unroll
-        for (int q = 0; q < 2 * GHEADS; ++q) sacc[q] = 0.f;
+      {  // logits al[q][n] = x_n . U[q]: two threads per node, four logits each
+        const int n = tid >> 1, qh = (tid & 1) * 4;
+        if (n < NB) {
+          const float* xr = xs + n * ZP;
+          float s4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int k = 0; k < GF; k += 4) {
-          const float4 xv = *reinterpret_cast<const float4*>(xr + k);
-          const float xk[4] = {xv.x, xv.y, xv.z, xv.w};
+          for (int k = 0; k < GF; k += 4) {
+            const float4 xv = *reinterpret_cast<const float4*>(xr + k);
+            const float xk[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float4 u0 = *reinterpret_cast<const float4*>(&Uk[k + j][0]);
-            const float4 u1 = *reinterpret_cast<const float4*>(&Uk[k + j][4]);
-            sacc[0] += xk[j] * u0.x; sacc[1] += xk[j] * u0.y; sacc[2] += xk[j] * u0.z; sacc[3] += xk[j] * u0.w;
-            sacc[4] += xk[j] * u1.x; sacc[5] += xk[j] * u1.y; sacc[6] += xk[j] * u1.z; sacc[7] += xk[j] * u1.w;
+            for (int j = 0; j < 4; ++j) {
+              const float4 u = *reinterpret_cast<const float4*>(&Uk[k + j][qh]);
+              s4[0] += xk[j] * u.x; s4[1] += xk[j] * u.y; s4[2] += xk[j] * u.z; s4[3] += xk[j] * u.w;
+            }
           }
-        }
 #pragma unroll
-        for (int q = 0; q < 2 * GHEADS; ++q) al[q][n] = sacc[q];
+          for (int j = 0; j < 4; ++j) al[qh + j][n] = s4[j];
+        }
       }
       __syncthreads();
+      dl = dw + 1;
+    } else {
+      dl = dw;
     }
 
     floatx16 acc[2];
@@ -378,96 +528,13 @@ __global__ __launch_bounds__(256, 3) void graph_stack_kernel(
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
-    const int nseg = kind == 0 ? GHEADS : 2;
-    const float* W0 = S.w0[L];
-    const float* W1 = S.w1[L];
-    auto wseg = [&](int sg) { return kind == 0 ? W0 + (int64_t)sg * GF * GF : (sg == 0 ? W0 : W1); };
-    auto load_b = [&](int sg, int kc, float4 (&bw)[2][2]) {
-      const float* W = wseg(sg);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const float* p = W + (t * 32 + li) * GF + kc * 16 + lh * 8;
-        bw[t][0] = *reinterpret_cast<const float4*>(p);
-        bw[t][1] = *reinterpret_cast<const float4*>(p + 4);
-      }
-    };
-    float4 bcur[2][2], bnxt[2][2];
-    load_b(0, 0, bcur);
-    for (int seg = 0; seg < nseg; ++seg) {
-      const bool agg = kind == 0 || seg == 0;
-      float wq[GMAXDEG];
-      int id[GMAXDEG];
-#pragma unroll
-      for (int q = 0; q < GMAXDEG; ++q) id[q] = kind == 0 ? idg[q] : ids[q];
-      if (kind == 0) {
-        const float ad = al[GHEADS + seg][row];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int q = 0; q < GMAXDEG; ++q) {
-          const float sv = al[seg][id[q]] + ad;
-          wq[q] = sv > 0.f ? sv : sv * 0.2f;
-          if (q < d) mx = fmaxf(mx, wq[q]);
-        }
-        float den = 0.f;
-#pragma unroll
-        for (int q = 0; q < GMAXDEG; ++q) {
-          wq[q] = q < d ? expf(wq[q] - mx) : 0.f;
-          den += wq[q];
-        }
-        const float inv = 1.f / (den + 1e-16f);
-#pragma unroll
-        for (int q = 0; q < GMAXDEG; ++q) wq[q] *= inv;
-      } else {
-#pragma unroll
-        for (int q = 0; q < GMAXDEG; ++q) wq[q] = q < d ? 1.f : 0.f;
-      }
-#pragma unroll
-      for (int kc = 0; kc < 4; ++kc) {
-        if (kc < 3) load_b(seg, kc + 1, bnxt);
-        else if (seg + 1 < nseg) load_b(seg + 1, 0, bnxt);
-        float af[8];
-        if (agg) {
-          float4 v[GMAXDEG][2];
-#pragma unroll
-          for (int q = 0; q < GMAXDEG; ++q) {
-            const float* p = xs + id[q] * ZP + kc * 16 + lh * 8;
-            v[q][0] = *reinterpret_cast<const float4*>(p);
-            v[q][1] = *reinterpret_cast<const float4*>(p + 4);
-          }
-#pragma unroll
-          for (int s8 = 0; s8 < 8; ++s8) af[s8] = 0.f;
-#pragma unroll
-          for (int q = 0; q < GMAXDEG; ++q) {
-            const float w = wq[q];
-            af[0] += w * v[q][0].x; af[1] += w * v[q][0].y; af[2] += w * v[q][0].z; af[3] += w * v[q][0].w;
-            af[4] += w * v[q][1].x; af[5] += w * v[q][1].y; af[6] += w * v[q][1].z; af[7] += w * v[q][1].w;
-          }
-        } else {
-          const float* p = xs + row * ZP + kc * 16 + lh * 8;
-          const float4 v0 = *reinterpret_cast<const float4*>(p);
-          const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
-          af[0] = v0.x; af[1] = v0.y; af[2] = v0.z; af[3] = v0.w;
-          af[4] = v1.x; af[5] = v1.y; af[6] = v1.z; af[7] = v1.w;
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const float bf[8] = {bcur[t][0].x, bcur[t][0].y, bcur[t][0].z, bcur[t][0].w,
-                               bcur[t][1].x, bcur[t][1].y, bcur[t][1].z, bcur[t][1].w};
-#pragma unroll
-          for (int s = 0; s < 8; ++s)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          bcur[t][0] = bnxt[t][0];
-          bcur[t][1] = bnxt[t][1];
-        }
-      }
-    }
+    dl = __builtin_amdgcn_readfirstlane(dl);
+    if (gat) stack_layer_dispatch<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
+    else stack_layer_dispatch<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
     __syncthreads();   // every gather of this layer has read the tile
 
     // epilogue: out = LReLU(LN(acc * scale + bias)) + x, in place (or to y after the last layer)
-    const float scale = kind == 0 ? 1.f / GHEADS : 1.f;
+    const float scale = gat ? 1.f / GHEADS : 1.f;
     const float* bias = S.bias[L];
     const float b0 = bias[li], b1 = bias[32 + li];
     const float lw0 = S.ln_w[L][li], lw1 = S.ln_w[L][32 + li];
@@ -475,22 +542,22 @@ __global__ __launch_bounds__(256, 3) void graph_stack_kernel(
     const bool last = L + 1 == S.nlayers;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int r = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+      const int nd = (en[q >> 2] >> (8 * (q & 3))) & 0xff;
       const float o0 = acc[0][q] * scale + b0, o1 = acc[1][q] * scale + b1;
       const float mean = half32_sum(o0 + o1) * (1.f / GF);
       const float sv = half32_sum((o0 - mean) * (o0 - mean) + (o1 - mean) * (o1 - mean));
       const float rstd = 1.f / sqrtf(sv * (1.f / GF) + 1e-5f);
-      if (r >= NB) continue;
+      if (nd == 0xff) continue;
       float u0 = (o0 - mean) * rstd * lw0 + lb0, u1 = (o1 - mean) * rstd * lw1 + lb1;
-      u0 = (u0 > 0.f ? u0 : u0 * S.slope) + xs[r * ZP + li];
-      u1 = (u1 > 0.f ? u1 : u1 * S.slope) + xs[r * ZP + 32 + li];
+      u0 = (u0 > 0.f ? u0 : u0 * S.slope) + xs[nd * ZP + li];
+      u1 = (u1 > 0.f ? u1 : u1 * S.slope) + xs[nd * ZP + 32 + li];
       if (last) {
-        float* yr = y + (node0 + r) * GF;
+        float* yr = y + (node0 + nd) * GF;
         yr[li] = u0;
         yr[32 + li] = u1;
       } else {
-        xs[r * ZP + li] = u0;
-        xs[r * ZP + 32 + li] = u1;
+        xs[nd * ZP + li] = u0;
+        xs[nd * ZP + 32 + li] = u1;
       }
     }
     if (!last) __syncthreads();   // the layer's output is the next layer's tile
