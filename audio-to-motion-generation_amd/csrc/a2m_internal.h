@@ -166,14 +166,18 @@ __device__ __forceinline__ float row16_max(float v) {
   v = fmaxf(v, dpp_f<DPP_HALF_MIRROR>(v));
   return fmaxf(v, dpp_f<DPP_MIRROR>(v));
 }
-// sum over the 32 lanes of each wave half (lanes l and l^16 combined by one bpermute)
+// sum over the 32 lanes of each wave half: lanes l and l^16 combined by v_permlane16_swap (gfx950:
+// exchanges 16-lane rows 0<->1 and 2<->3 in VALU, no LDS round trip), so r[0] + r[1] is v_l + v_{l^16}
+// on every lane (the same two addends in either order: bit-identical to a shuffle)
 __device__ __forceinline__ float half32_sum(float v) {
   v = row16_sum(v);
-  return v + __shfl_xor(v, 16);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 __device__ __forceinline__ float wave64_sum(float v) {
   v = half32_sum(v);
-  return v + __shfl_xor(v, 32);
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 __device__ __forceinline__ float wave64_max(float v) {
   v = row16_max(v);

@@ -14,6 +14,11 @@
 namespace a2m {
 
 constexpr int GF = 64;          // joint feature dim
+// Diagnostic builds only (never the shipped library): STACK_ABL = 1 drops the stack's MFMAs,
+// 2 its neighbour gathers, 4 the weight-fragment loads (tools/stack_bench.py times them).
+#ifndef STACK_ABL
+#define STACK_ABL 0
+#endif
 constexpr int GHEADS = 4;
 constexpr int GMAXN = 128;      // node rows per workgroup (4 waves x 32 MFMA rows)
 constexpr int ZP = GF + 4;      // LDS row pitch (floats): 16-B aligned, conflict-free b128 reads
@@ -298,24 +303,15 @@ struct GraphStack {
 // the gathered slices and edge weights stay in registers): 8 steps of k = 8 (4 per lane half);
 // each gathered float4 is weighted for every segment, then 8 MFMAs per segment.  B fragments
 // (64 output channels) come from L2 one step ahead.
-__device__ __forceinline__ void stack_load_b(const float* W0, const float* W1, bool gat, int st, int li,
-                                             int lh, float4 (&bw)[GHEADS][2]) {
-  const int off = (st >> 1) * 16 + lh * 8 + (st & 1) * 4;
-#pragma unroll
-  for (int h = 0; h < GHEADS; ++h) {
-    if (!gat && h >= 2) break;
-    const float* W = gat ? W0 + (int64_t)h * GF * GF : (h == 0 ? W0 : W1);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) bw[h][t] = *reinterpret_cast<const float4*>(W + (t * 32 + li) * GF + off);
-  }
-}
-
 __device__ __forceinline__ void stack_mfma4(const float (&af)[4], const float4 (&b)[2], floatx16 (&acc)[2]) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const float bf[4] = {b[t].x, b[t].y, b[t].z, b[t].w};
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
+    for (int s = 0; s < 4; ++s) {
+      if (STACK_ABL == 1) acc[t][s] += af[s] * bf[s];
+      else acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
+    }
   }
 }
 
@@ -323,6 +319,7 @@ template <int DL, bool GAT>
 __device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)[GMAXN], const int (&id)[GMAXDEG],
                                               int node, int d0, const float* W0, const float* W1, int li,
                                               int lh, floatx16 (&acc)[2]) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
   constexpr int NS = GAT ? GHEADS : 1;   // aggregated segments (GraphConv: + the root term)
   float wq[NS][DL];
   if (GAT) {  // edge softmax per head over the in-edges + self loop (slot d0; PyG: LeakyReLU 0.2)
@@ -351,36 +348,51 @@ __device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)
 #pragma unroll
     for (int q = 0; q < DL; ++q) wq[0][q] = q < d0 ? 1.f : 0.f;
   }
-  float4 bc[GHEADS][2], bn[GHEADS][2];
-  stack_load_b(W0, W1, GAT, 0, li, lh, bc);
-#pragma unroll 1
-  for (int st = 0; st < 8; ++st) {
-    if (st < 7) stack_load_b(W0, W1, GAT, st + 1, li, lh, bn);
-    const int off = (st >> 1) * 16 + lh * 8 + (st & 1) * 4;
-    float af[NS][4];
+  // per-lane 32-bit offsets of the B rows (t*32 + li) at this lane half's k; segment h adds h*GF*GF
+  const uint32_t boff = (uint32_t)(li * GF + lh * 8);
+  auto load_b = [&](int st, float4 (&bw)[GHEADS][2]) {
+    const uint32_t off = boff + (st >> 1) * 16 + (st & 1) * 4;
 #pragma unroll
-    for (int h = 0; h < NS; ++h) af[h][0] = af[h][1] = af[h][2] = af[h][3] = 0.f;
+    for (int h = 0; h < (GAT ? GHEADS : 2); ++h) {
+      const float* W = GAT ? W0 + h * GF * GF : (h == 0 ? W0 : W1);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        bw[h][t] = STACK_ABL == 4 ? make_float4(W0[0] * st, 1.f, 0.5f, (float)h) : *reinterpret_cast<const float4*>(W + off + t * 32 * GF);
+    }
+  };
+  auto step = [&](int st, const float4 (&bc)[GHEADS][2]) {
+    const int off = (st >> 1) * 16 + lh * 8 + (st & 1) * 4;
+    f2 a01[NS], a23[NS];
+#pragma unroll
+    for (int h = 0; h < NS; ++h) a01[h] = a23[h] = f2{0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < DL; ++q) {
-      const float4 v = *reinterpret_cast<const float4*>(xs + id[q] * ZP + off);
+      const float4 v = *reinterpret_cast<const float4*>(xs + (STACK_ABL == 2 ? node : id[q]) * ZP + off);
 #pragma unroll
       for (int h = 0; h < NS; ++h) {
-        const float w = wq[h][q];
-        af[h][0] += w * v.x; af[h][1] += w * v.y; af[h][2] += w * v.z; af[h][3] += w * v.w;
+        a01[h].x += wq[h][q] * v.x; a01[h].y += wq[h][q] * v.y; a23[h].x += wq[h][q] * v.z; a23[h].y += wq[h][q] * v.w;
       }
     }
 #pragma unroll
-    for (int h = 0; h < NS; ++h) stack_mfma4(af[h], bc[h], acc);
+    for (int h = 0; h < NS; ++h) {
+      const float af[4] = {a01[h].x, a01[h].y, a23[h].x, a23[h].y};
+      stack_mfma4(af, bc[h], acc);
+    }
     if (!GAT) {
       const float4 o = *reinterpret_cast<const float4*>(xs + node * ZP + off);   // root term
       const float ao[4] = {o.x, o.y, o.z, o.w};
       stack_mfma4(ao, bc[1], acc);
     }
-#pragma unroll
-    for (int h = 0; h < GHEADS; ++h) {
-      bc[h][0] = bn[h][0];
-      bc[h][1] = bn[h][1];
-    }
+  };
+  // ping-pong B buffers: each step's fragments are loaded one step ahead, no register copies
+  float4 ba[GHEADS][2], bb[GHEADS][2];
+  load_b(0, ba);
+#pragma unroll 1
+  for (int st = 0; st < 8; st += 2) {
+    load_b(st + 1, bb);
+    step(st, ba);
+    if (st + 2 < 8) load_b(st + 2, ba);
+    step(st + 1, bb);
   }
 }
 
@@ -410,6 +422,8 @@ __global__ __launch_bounds__(256, 2) void graph_stack_kernel(
   __shared__ unsigned char ndeg[GMAXN];
   __shared__ unsigned char rown[GMAXN];                                // MFMA row -> node (0xff: none)
   __shared__ int csr[2 * GMAXN];
+  __shared__ __attribute__((aligned(16))) float osc[4][32 * ZP];        // per-wave epilogue scratch
+  __shared__ __attribute__((aligned(16))) float lnp[2 * GF];            // this layer's LN weight | bias
 
   const int fpb = GMAXN / J;
   const int NBmax = fpb * J;
@@ -478,18 +492,6 @@ __global__ __launch_bounds__(256, 2) void graph_stack_kernel(
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) dw = max(dw, __shfl_xor(dw, o));
   dw = __builtin_amdgcn_readfirstlane(dw);
-  // epilogue rows r = 32 wave + (q & 3) + 8 (q >> 2) + 4 lh  ->  their nodes, one byte each
-  unsigned en[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    en[j] = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int q = 4 * j + b;
-      en[j] |= (unsigned)rown[wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh] << (8 * b);
-    }
-  }
-
   for (int L = 0; L < S.nlayers; ++L) {
     const int kind = S.kind[L];
     const bool gat = kind == 0;
@@ -502,7 +504,8 @@ __global__ __launch_bounds__(256, 2) void graph_stack_kernel(
         const int n = tid >> 1, qh = (tid & 1) * 4;
         if (n < NB) {
           const float* xr = xs + n * ZP;
-          float s4[4] = {0.f, 0.f, 0.f, 0.f};
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          f2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
 #pragma unroll 4
           for (int k = 0; k < GF; k += 4) {
             const float4 xv = *reinterpret_cast<const float4*>(xr + k);
@@ -510,11 +513,12 @@ __global__ __launch_bounds__(256, 2) void graph_stack_kernel(
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const float4 u = *reinterpret_cast<const float4*>(&Uk[k + j][qh]);
-              s4[0] += xk[j] * u.x; s4[1] += xk[j] * u.y; s4[2] += xk[j] * u.z; s4[3] += xk[j] * u.w;
+              const f2 x2 = {xk[j], xk[j]};
+              s01 = __builtin_elementwise_fma(x2, f2{u.x, u.y}, s01);
+              s23 = __builtin_elementwise_fma(x2, f2{u.z, u.w}, s23);
             }
           }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) al[qh + j][n] = s4[j];
+          al[qh][n] = s01.x; al[qh + 1][n] = s01.y; al[qh + 2][n] = s23.x; al[qh + 3][n] = s23.y;
         }
       }
       __syncthreads();
@@ -531,35 +535,68 @@ __global__ __launch_bounds__(256, 2) void graph_stack_kernel(
     dl = __builtin_amdgcn_readfirstlane(dl);
     if (gat) stack_layer_dispatch<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
     else stack_layer_dispatch<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
-    __syncthreads();   // every gather of this layer has read the tile
-
-    // epilogue: out = LReLU(LN(acc * scale + bias)) + x, in place (or to y after the last layer)
+    // epilogue: out = LReLU(LN(acc * scale + bias)) + x, in place (or to y after the last layer).
+    // The wave's 32 x 64 result goes through its private LDS scratch so that each lane then owns
+    // half a row (32 contiguous features): the LayerNorm sums are 32-element register sums plus
+    // one lane-pair DPP add, instead of 32 cross-lane reductions over the MFMA layout.
     const float scale = gat ? 1.f / GHEADS : 1.f;
-    const float* bias = S.bias[L];
-    const float b0 = bias[li], b1 = bias[32 + li];
-    const float lw0 = S.ln_w[L][li], lw1 = S.ln_w[L][32 + li];
-    const float lb0 = S.ln_b[L][li], lb1 = S.ln_b[L][32 + li];
-    const bool last = L + 1 == S.nlayers;
+    {
+      const float* bias = S.bias[L];
+      const float b0 = bias[li], b1 = bias[32 + li];
+      float* o = osc[wave];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int nd = (en[q >> 2] >> (8 * (q & 3))) & 0xff;
-      const float o0 = acc[0][q] * scale + b0, o1 = acc[1][q] * scale + b1;
-      const float mean = half32_sum(o0 + o1) * (1.f / GF);
-      const float sv = half32_sum((o0 - mean) * (o0 - mean) + (o1 - mean) * (o1 - mean));
-      const float rstd = 1.f / sqrtf(sv * (1.f / GF) + 1e-5f);
-      if (nd == 0xff) continue;
-      float u0 = (o0 - mean) * rstd * lw0 + lb0, u1 = (o1 - mean) * rstd * lw1 + lb1;
-      u0 = (u0 > 0.f ? u0 : u0 * S.slope) + xs[nd * ZP + li];
-      u1 = (u1 > 0.f ? u1 : u1 * S.slope) + xs[nd * ZP + 32 + li];
-      if (last) {
-        float* yr = y + (node0 + nd) * GF;
-        yr[li] = u0;
-        yr[32 + li] = u1;
-      } else {
-        xs[nd * ZP + li] = u0;
-        xs[nd * ZP + 32 + li] = u1;
+      for (int q = 0; q < 16; ++q) {
+        const int rr = (q & 3) + 8 * (q >> 2) + 4 * lh;
+        o[rr * ZP + li] = acc[0][q] * scale + b0;
+        o[rr * ZP + 32 + li] = acc[1][q] * scale + b1;
       }
     }
+    if (tid < 2 * GF) lnp[tid] = tid < GF ? S.ln_w[L][tid] : S.ln_b[L][tid - GF];
+    __syncthreads();   // every gather of this layer has read the tile; scratch and LN params visible
+    {
+      const int rr = lane >> 1, hf = (lane & 1) * 32;
+      const int nd = rown[wave * 32 + rr];
+      const float* orow = osc[wave] + rr * ZP + hf;
+      float v[32];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 t = *reinterpret_cast<const float4*>(orow + 4 * j);
+        v[4 * j] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) sm += v[j];
+      sm += dpp_f<DPP_XOR1>(sm);
+      const float mean = sm * (1.f / GF);
+      float sq = 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) sq += (v[j] - mean) * (v[j] - mean);
+      sq += dpp_f<DPP_XOR1>(sq);
+      const float rstd = 1.f / sqrtf(sq * (1.f / GF) + 1e-5f);
+      if (nd != 0xff) {
+        float* xr = xs + nd * ZP + hf;
+        const bool last = L + 1 == S.nlayers;
+        float* yr = y + (node0 + nd) * GF + hf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 xv = *reinterpret_cast<const float4*>(xr + 4 * j);
+          const float4 w = *reinterpret_cast<const float4*>(lnp + hf + 4 * j);
+          const float4 bb = *reinterpret_cast<const float4*>(lnp + GF + hf + 4 * j);
+          float4 u;
+          u.x = (v[4 * j] - mean) * rstd * w.x + bb.x;
+          u.y = (v[4 * j + 1] - mean) * rstd * w.y + bb.y;
+          u.z = (v[4 * j + 2] - mean) * rstd * w.z + bb.z;
+          u.w = (v[4 * j + 3] - mean) * rstd * w.w + bb.w;
+          u.x = (u.x > 0.f ? u.x : u.x * S.slope) + xv.x;
+          u.y = (u.y > 0.f ? u.y : u.y * S.slope) + xv.y;
+          u.z = (u.z > 0.f ? u.z : u.z * S.slope) + xv.z;
+          u.w = (u.w > 0.f ? u.w : u.w * S.slope) + xv.w;
+          if (last) *reinterpret_cast<float4*>(yr + 4 * j) = u;
+          else *reinterpret_cast<float4*>(xr + 4 * j) = u;
+        }
+      }
+    }
+    const bool last = L + 1 == S.nlayers;
     if (!last) __syncthreads();   // the layer's output is the next layer's tile
   }
 }

@@ -692,6 +692,96 @@ int a2m_conv2d_pack_nhwc_f32(const float* w, int32_t Co, int32_t Ci, int32_t kh,
   return A2M_OK;
 }
 
+// Single-input-channel conv2d (the encoder's first layer, model_layers.py:262-263: 1 -> 64,
+// k 4x4, s 2 over the [B, T, F] mel) as a direct kernel: K = kh*kw = 16 is far too shallow for
+// the GEMM engine (its k loop never fills).  One workgroup per C1_ROWS output rows of one clip:
+// the input rows they read are staged in LDS once, each thread loads the taps of 4 output
+// channels into registers once and sweeps C1_ROWS rows x its output columns, writing float4
+// channel groups so a pixel's Co channels leave as one contiguous run (NHWC).  Bias, BN-eval
+// affine and the activation are fused as in the GEMM epilogue (gemm_kernel.h epi_value).
+constexpr int C1_K = 4, C1_ROWS = 4, C1_MAXW = 512;
+constexpr int C1_IN_ROWS = (C1_ROWS - 1) * 2 + C1_K;   // stride <= 2
+__global__ __launch_bounds__(256) void conv2d_c1_kernel(
+    const float* __restrict__ x, int H, int W, const float* __restrict__ packed, const float* __restrict__ bias,
+    int Co, int stride, int ph, int pw, const float* __restrict__ bn_w,
+    const float* __restrict__ bn_b, const float* __restrict__ bn_rm, const float* __restrict__ bn_rv,
+    float bn_eps, int act, float slope, float* __restrict__ y, int y_nhwc, int Hout, int Wout, int w_lo, int w_hi) {
+  constexpr int kh = C1_K, kw = C1_K;
+  __shared__ float rows[C1_IN_ROWS][C1_MAXW];
+  const int rb = (Hout + C1_ROWS - 1) / C1_ROWS;
+  const int b = blockIdx.x / rb, ho0 = (blockIdx.x % rb) * C1_ROWS;
+  const int nr = min(C1_ROWS, Hout - ho0);
+  const int tid = threadIdx.x;
+  // input rows ho0*s - ph + i and the columns the live outputs read, zero outside the image
+  const int c0 = w_lo * stride - pw, nc = (w_hi - 1 - w_lo) * stride + kw;
+  const int nin = (nr - 1) * stride + kh;
+  for (int idx = tid; idx < nin * nc; idx += blockDim.x) {
+    const int i = idx / nc, c = idx % nc;
+    const int hi = ho0 * stride - ph + i, wi = c0 + c;
+    rows[i][c] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? x[((int64_t)b * H + hi) * W + wi] : 0.f;
+  }
+  const int ng = Co / 4;                 // float4 channel groups
+  const int wpp = blockDim.x / ng;       // output columns per pass
+  const int g = tid % ng, wsub = tid / ng;
+  float wt[4][kh * kw];
+  float sc[4], sh[4], bo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = 4 * g + j;
+    const float4* wp = reinterpret_cast<const float4*>(packed + co * kh * kw);
+#pragma unroll
+    for (int t = 0; t < kh * kw / 4; ++t) {
+      const float4 v = wp[t];
+      wt[j][4 * t] = v.x; wt[j][4 * t + 1] = v.y; wt[j][4 * t + 2] = v.z; wt[j][4 * t + 3] = v.w;
+    }
+    // epi_value order: + bias, then (v - rm) * (w / sqrt(rv + eps)) + b
+    const float bb = bias ? bias[co] : 0.f;
+    if (bn_w) {
+      sc[j] = bn_w[co] / sqrtf(bn_rv[co] + bn_eps);
+      sh[j] = bb - bn_rm[co];
+      bo[j] = bn_b[co];
+    } else {
+      sc[j] = 1.f;
+      sh[j] = bb;
+      bo[j] = 0.f;
+    }
+  }
+  __syncthreads();
+  if (wsub >= wpp) return;
+  for (int r = 0; r < nr; ++r) {
+    const int ho = ho0 + r;
+    for (int wo = w_lo + wsub; wo < w_hi; wo += wpp) {
+      const int cb = (wo - w_lo) * stride;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < kh; ++i) {
+#pragma unroll
+        for (int j = 0; j < kw; ++j) {
+          const float xv = rows[r * stride + i][cb + j];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[c] = fmaf(wt[c][i * kw + j], xv, acc[c]);
+        }
+      }
+      float o[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float v = (acc[c] + sh[c]) * sc[c] + bo[c];
+        if (act == ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (act == ACT_LRELU) v = v > 0.f ? v : v * slope;
+        else if (act == ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+        o[c] = v;
+      }
+      if (y_nhwc) {
+        *reinterpret_cast<float4*>(y + (((int64_t)b * Hout + ho) * Wout + wo) * Co + 4 * g) =
+            make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) y[(((int64_t)b * Co + 4 * g + c) * Hout + ho) * Wout + wo] = o[c];
+      }
+    }
+  }
+}
+
 int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
                             const float* packed, const float* bias, int32_t Co, int32_t kh,
                             int32_t kw, int32_t stride, int32_t pad_h, int32_t pad_w,
@@ -710,6 +800,16 @@ int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, in
                 "conv2d_nhwc: kw * Ci = %d must be a multiple of 4", kw * Ci);
   A2M_CHECK_ARG(fits32((int64_t)B * Ci * H * W) && fits32((int64_t)B * Co * Hout * Wout),
                 "conv2d_nhwc: too large");
+  if (Ci == 1 && kh == C1_K && kw == C1_K && stride <= 2 && Co % 4 == 0 && Co <= 1024 &&
+      (w_hi - 1 - w_lo) * stride + kw <= C1_MAXW && reinterpret_cast<uintptr_t>(packed) % 16 == 0 &&
+      (!y_nhwc || reinterpret_cast<uintptr_t>(y) % 16 == 0)) {
+    hipLaunchKernelGGL(conv2d_c1_kernel, dim3((unsigned)(B * cdiv(Hout, C1_ROWS))), dim3(256), 0,
+                       as_stream(stream), x, H, W,
+                       packed, bias, Co, stride, pad_h, pad_w, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act,
+                       slope, y, y_nhwc, Hout, Wout, w_lo, w_hi);
+    A2M_LAUNCH_CHECK();
+    return A2M_OK;
+  }
   const int Wn = w_hi - w_lo;
   Gather A = dense_rk(packed, Ci * kh * kw);
   // rows n = (b, ho, wo - w_lo), k = (i, j, ci): the input element x[b][ho*s - ph + i]

@@ -1,0 +1,50 @@
+"""Times the fused eval graph stack (a2m_graph_stack_fwd_f32: GAT, GraphConv, GAT, GraphConv,
+GAT) at the bench shapes: hand (J=42) and body (J=10) over B*T = 4096 frames.
+    python tools/stack_bench.py [hand|body] [iters]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'audio-to-motion-generation_amd'))
+import torch  # noqa: E402
+
+from a2m import functional as F  # noqa: E402
+from a2m import skeleton as S  # noqa: E402
+
+dev = torch.device('cuda')
+FR = 4096
+which = sys.argv[1] if len(sys.argv) > 1 else 'both'
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+g = torch.Generator(device='cpu').manual_seed(0)
+
+
+def rnd(*s, scale=1.0):
+    return (torch.randn(*s, generator=g) * scale).to(dev)
+
+
+for name, J, lo in (('hand', 42, 10), ('body', 10, 0)):
+    if which not in ('both', name):
+        continue
+    ptr, idx = [t.to(dev) for t in S.in_neighbour_csr(S.edge_index(lo, J), J)]
+    x = rnd(FR * J, 64)
+    layers = []
+    for L in range(5):
+        lnw, lnb = rnd(64).abs() + .5, rnd(64, scale=0.1)
+        if L % 2 == 0:
+            lw = rnd(256, 64, scale=0.15)
+            U = F.graph_att_proj(lw, rnd(1, 4, 64, scale=0.3), rnd(1, 4, 64, scale=0.3))
+            layers.append((0, lw, None, U, rnd(64, scale=0.1), lnw, lnb))
+        else:
+            layers.append((1, rnd(64, 64, scale=0.12), rnd(64, 64, scale=0.12), None, rnd(64, scale=0.1), lnw, lnb))
+    out = torch.empty_like(x)
+    for _ in range(3):
+        F.graph_stack(x, J, ptr, idx, layers, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        F.graph_stack(x, J, ptr, idx, layers, out=out)
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / iters
+    gf = FR * J * 64 * 64 * 2 * (3 * 4 + 2 * 2) / 1e9
+    print(f'{name} stack: {us:.1f} us/launch, {gf:.2f} GFLOP of MFMA work, {gf / us * 1e-3:.1f} TF', flush=True)
