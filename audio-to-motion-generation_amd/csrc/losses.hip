@@ -53,14 +53,15 @@ __global__ __launch_bounds__(256) void pose_loss_partial_kernel(const float* gen
   __shared__ float red[4];
   const int b = blockIdx.x;
   float* pb = part + (int64_t)b * kPart;
-  // bone lengths averaged over time (one thread per bone and pose)
-  for (int i = threadIdx.x; i < 2 * kBones; i += blockDim.x) {
+  // bone lengths averaged over time (one thread per bone and pose); without a real pose the
+  // bone loss is 0 and the generated lengths are not needed (the eval / inference path)
+  for (int i = threadIdx.x; real != nullptr && i < 2 * kBones; i += blockDim.x) {
     const bool is_real = i >= kBones;
-    if (is_real && real == nullptr) continue;
     const int jb = (i % kBones) + 1, pj = kParents[jb];
     const float* base = is_real ? real + b * rs_b : gen + b * gs_b;
     const int64_t st = is_real ? rs_t : gs_t;
     float s = 0.f;
+#pragma unroll 8
     for (int t = 0; t < T; ++t) {
       const float* p = base + t * st;
       const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(256) void pose_loss_final_kernel(const float* part,
                                                               float body_w, float* out) {
   __shared__ float red[4];
   float bone = 0.f, hs = 0.f, bs = 0.f;
-  for (int i = threadIdx.x; i < B * kBones; i += blockDim.x) {
+  for (int i = threadIdx.x; has_real && i < B * kBones; i += blockDim.x) {
     const float* pb = part + (int64_t)(i / kBones) * kPart;
     const int k = i % kBones;
     const float d = pb[k] - pb[kBones + k];
