@@ -19,12 +19,26 @@ constexpr int GF = 64;          // joint feature dim
 #ifndef STACK_ABL
 #define STACK_ABL 0
 #endif
+#ifndef STACK_PINGPONG
+#define STACK_PINGPONG 0
+#endif
+#ifndef STACK_WG_PER_CU
+#define STACK_WG_PER_CU 3
+#endif
 constexpr int GHEADS = 4;
 constexpr int GMAXN = 128;      // node rows per workgroup (4 waves x 32 MFMA rows)
 constexpr int ZP = GF + 4;      // LDS row pitch (floats): 16-B aligned, conflict-free b128 reads
 constexpr int GMAXDEG = 8;      // max in-degree (+ self loop) of a skeleton node (hand roots: 5 + 1)
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// LDS ordering between the lanes of ONE wave (its private scratch): a wavefront-scope fence pair
+// around a wave barrier.
+__device__ __forceinline__ void stack_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Layer math, restructured "aggregate, then transform" so the 256-wide GAT projection is
 // never materialised:
@@ -384,6 +398,7 @@ __device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)
       stack_mfma4(ao, bc[1], acc);
     }
   };
+#if STACK_PINGPONG
   // ping-pong B buffers: each step's fragments are loaded one step ahead, no register copies
   float4 ba[GHEADS][2], bb[GHEADS][2];
   load_b(0, ba);
@@ -394,6 +409,16 @@ __device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)
     if (st + 2 < 8) load_b(st + 2, ba);
     step(st + 1, bb);
   }
+#else
+  // single-buffered B (registers for three workgroups per CU): a step's fragments are requested
+  // before its gathers and FMAs, which cover part of the L2 latency; co-resident waves the rest
+#pragma unroll 1
+  for (int st = 0; st < 8; ++st) {
+    float4 bc[GHEADS][2];
+    load_b(st, bc);
+    step(st, bc);
+  }
+#endif
 }
 
 template <bool GAT>
@@ -412,7 +437,7 @@ __device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, co
   }
 }
 
-__global__ __launch_bounds__(256, 2) void graph_stack_kernel(
+__global__ __launch_bounds__(256, STACK_WG_PER_CU) void graph_stack_kernel(
     const float* __restrict__ x, int F, int J, const int* __restrict__ nbr_ptr,
     const int* __restrict__ nbr_idx, GraphStack S, float* __restrict__ y) {
   __shared__ __attribute__((aligned(16))) float xs[GMAXN * ZP];        // node-indexed tile
@@ -422,7 +447,7 @@ __global__ __launch_bounds__(256, 2) void graph_stack_kernel(
   __shared__ unsigned char ndeg[GMAXN];
   __shared__ unsigned char rown[GMAXN];                                // MFMA row -> node (0xff: none)
   __shared__ int csr[2 * GMAXN];
-  __shared__ __attribute__((aligned(16))) float osc[4][32 * ZP];        // per-wave epilogue scratch
+  __shared__ __attribute__((aligned(16))) float osc[4][8 * ZP];         // per-wave epilogue scratch (8 rows)
   __shared__ __attribute__((aligned(16))) float lnp[2 * GF];            // this layer's LN weight | bias
 
   const int fpb = GMAXN / J;
@@ -536,63 +561,66 @@ __global__ __launch_bounds__(256, 2) void graph_stack_kernel(
     if (gat) stack_layer_dispatch<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
     else stack_layer_dispatch<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
     // epilogue: out = LReLU(LN(acc * scale + bias)) + x, in place (or to y after the last layer).
-    // The wave's 32 x 64 result goes through its private LDS scratch so that each lane then owns
-    // half a row (32 contiguous features): the LayerNorm sums are 32-element register sums plus
-    // one lane-pair DPP add, instead of 32 cross-lane reductions over the MFMA layout.
+    // The wave's 32 x 64 result goes through its private LDS scratch, 8 rows at a time (rows
+    // 8p..8p+7 are exactly accumulator entries q = 4p..4p+3), so that each lane then owns 8
+    // contiguous features of a row: the LayerNorm sums are 8-element register sums plus two
+    // DPP adds over the row's 8 lanes, instead of cross-lane reductions in the MFMA layout.
     const float scale = gat ? 1.f / GHEADS : 1.f;
+    if (tid < 2 * GF) lnp[tid] = tid < GF ? S.ln_w[L][tid] : S.ln_b[L][tid - GF];
+    __syncthreads();   // every gather of this layer has read the tile; LN params visible
     {
       const float* bias = S.bias[L];
       const float b0 = bias[li], b1 = bias[32 + li];
+      const bool last_l = L + 1 == S.nlayers;
       float* o = osc[wave];
+      const int r8 = lane >> 3, seg = (lane & 7) * 8;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int rr = (q & 3) + 8 * (q >> 2) + 4 * lh;
-        o[rr * ZP + li] = acc[0][q] * scale + b0;
-        o[rr * ZP + 32 + li] = acc[1][q] * scale + b1;
-      }
-    }
-    if (tid < 2 * GF) lnp[tid] = tid < GF ? S.ln_w[L][tid] : S.ln_b[L][tid - GF];
-    __syncthreads();   // every gather of this layer has read the tile; scratch and LN params visible
-    {
-      const int rr = lane >> 1, hf = (lane & 1) * 32;
-      const int nd = rown[wave * 32 + rr];
-      const float* orow = osc[wave] + rr * ZP + hf;
-      float v[32];
+      for (int p = 0; p < 4; ++p) {
+        if (p > 0) stack_wave_sync();   // the previous pass's scratch reads of this wave
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float4 t = *reinterpret_cast<const float4*>(orow + 4 * j);
-        v[4 * j] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
-      }
-      float sm = 0.f;
+        for (int qq = 0; qq < 4; ++qq) {
+          const int q = 4 * p + qq;
+          const int rr = (q & 3) + 4 * lh;
+          o[rr * ZP + li] = acc[0][q] * scale + b0;
+          o[rr * ZP + 32 + li] = acc[1][q] * scale + b1;
+        }
+        stack_wave_sync();
+        const int nd = rown[wave * 32 + 8 * p + r8];
+        const float4 v0 = *reinterpret_cast<const float4*>(o + r8 * ZP + seg);
+        const float4 v1 = *reinterpret_cast<const float4*>(o + r8 * ZP + seg + 4);
+        const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        float sm = 0.f;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) sm += v[j];
-      sm += dpp_f<DPP_XOR1>(sm);
-      const float mean = sm * (1.f / GF);
-      float sq = 0.f;
+        for (int j = 0; j < 8; ++j) sm += v[j];
+        sm = quad_sum(sm);
+        sm += dpp_f<DPP_HALF_MIRROR>(sm);
+        const float mean = sm * (1.f / GF);
+        float sq = 0.f;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) sq += (v[j] - mean) * (v[j] - mean);
-      sq += dpp_f<DPP_XOR1>(sq);
-      const float rstd = 1.f / sqrtf(sq * (1.f / GF) + 1e-5f);
-      if (nd != 0xff) {
-        float* xr = xs + nd * ZP + hf;
-        const bool last = L + 1 == S.nlayers;
-        float* yr = y + (node0 + nd) * GF + hf;
+        for (int j = 0; j < 8; ++j) sq += (v[j] - mean) * (v[j] - mean);
+        sq = quad_sum(sq);
+        sq += dpp_f<DPP_HALF_MIRROR>(sq);
+        const float rstd = 1.f / sqrtf(sq * (1.f / GF) + 1e-5f);
+        if (nd != 0xff) {
+          float* xr = xs + nd * ZP + seg;
+          float* yr = y + (node0 + nd) * GF + seg;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float4 xv = *reinterpret_cast<const float4*>(xr + 4 * j);
-          const float4 w = *reinterpret_cast<const float4*>(lnp + hf + 4 * j);
-          const float4 bb = *reinterpret_cast<const float4*>(lnp + GF + hf + 4 * j);
-          float4 u;
-          u.x = (v[4 * j] - mean) * rstd * w.x + bb.x;
-          u.y = (v[4 * j + 1] - mean) * rstd * w.y + bb.y;
-          u.z = (v[4 * j + 2] - mean) * rstd * w.z + bb.z;
-          u.w = (v[4 * j + 3] - mean) * rstd * w.w + bb.w;
-          u.x = (u.x > 0.f ? u.x : u.x * S.slope) + xv.x;
-          u.y = (u.y > 0.f ? u.y : u.y * S.slope) + xv.y;
-          u.z = (u.z > 0.f ? u.z : u.z * S.slope) + xv.z;
-          u.w = (u.w > 0.f ? u.w : u.w * S.slope) + xv.w;
-          if (last) *reinterpret_cast<float4*>(yr + 4 * j) = u;
-          else *reinterpret_cast<float4*>(xr + 4 * j) = u;
+          for (int j = 0; j < 2; ++j) {
+            const float4 xv = *reinterpret_cast<const float4*>(xr + 4 * j);
+            const float4 w = *reinterpret_cast<const float4*>(lnp + seg + 4 * j);
+            const float4 bb = *reinterpret_cast<const float4*>(lnp + GF + seg + 4 * j);
+            float4 u;
+            u.x = (v[4 * j] - mean) * rstd * w.x + bb.x;
+            u.y = (v[4 * j + 1] - mean) * rstd * w.y + bb.y;
+            u.z = (v[4 * j + 2] - mean) * rstd * w.z + bb.z;
+            u.w = (v[4 * j + 3] - mean) * rstd * w.w + bb.w;
+            u.x = (u.x > 0.f ? u.x : u.x * S.slope) + xv.x;
+            u.y = (u.y > 0.f ? u.y : u.y * S.slope) + xv.y;
+            u.z = (u.z > 0.f ? u.z : u.z * S.slope) + xv.z;
+            u.w = (u.w > 0.f ? u.w : u.w * S.slope) + xv.w;
+            if (last_l) *reinterpret_cast<float4*>(yr + 4 * j) = u;
+            else *reinterpret_cast<float4*>(xr + 4 * j) = u;
+          }
         }
       }
     }
