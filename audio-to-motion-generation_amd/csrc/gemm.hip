@@ -176,7 +176,7 @@ static int gemm_bk(int prec) { return prec == 1 ? 64 : 32; }
 int gemm_k_tile() { return gemm_bk(g_gemm_prec); }
 
 static int gemm_xcd_group() {
-  static const int g = env_int("A2M_GEMM_XCD", 0);
+  static const int g = env_int("A2M_GEMM_XCD", 8);
   return g < 0 ? 0 : g;
 }
 

@@ -487,7 +487,11 @@ def main():
         'mel_roofline': {'bound': 'hbm', 'achieved': round(mel_bytes / (mel_ms * 1e-3) / 1e9, 1),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(mel_bytes / (mel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         'ms_per_launch': round(mel_ms, 4)},
+                         'ms_per_launch': round(mel_ms, 4),
+                         'algorithmic_bytes': int(mel_bytes),
+                         'traffic': (load_traffic('logmel2048_kernel') or {}).get('bytes_per_launch')
+                         if (B, T) == (64, 64) else None,
+                         'note': 'VALU-issue bound (DESIGN.md 4): ~732 VALU instructions per frame-wave'},
         'mel_encoder_roofline': mel_enc,
         'path_roofline': {'bound': 'mfma', 'achieved': round(path_tf, 2), 'peak': peak,
                           'unit': 'TFLOP/s', 'frac': round(path_tf / peak, 4),

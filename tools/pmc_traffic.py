@@ -17,8 +17,10 @@ import json
 import os
 from collections import defaultdict
 
-FAMILIES = ('gemm_kernel', 'splitk_reduce_kernel', 'logmel_kernel', 'graph_layer_kernel',
-            'graph_att_proj_kernel', 'channel_attention_kernel', 'softmax_rows_kernel', 'layernorm_kernel')
+FAMILIES = ('gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'logmel_kernel',
+            'graph_stack_kernel', 'graph_layer_kernel', 'graph_att_proj_kernel', 'attn_fused_eval_kernel',
+            'attn_core_wide_kernel', 'conv2d_c1_kernel', 'im2col2d_kernel', 'im2col1d_kernel',
+            'channel_attention_kernel', 'softmax_rows_kernel', 'layernorm_kernel')
 
 
 def read_counter(d, name):
