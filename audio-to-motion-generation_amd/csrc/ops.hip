@@ -377,6 +377,25 @@ int softmax_rows(float* x, int rows, int n, hipStream_t st) {
 
 using namespace a2m;
 
+// [B][C][T] (batch stride xs_b) -> [B*T][C]: the k-contiguous (dense) operand layout of a 1x1
+// conv's GEMM.  One workgroup per (clip, 64 channels): the 64 x T tile is read along t and
+// written along c through LDS (pitch T + 1).
+constexpr int TR_C = 64, TR_MAXT = 64;
+__global__ __launch_bounds__(256) void bct_to_btc_kernel(const float* __restrict__ x, int64_t xs_b, int C,
+                                                         int T, float* __restrict__ xt) {
+  __shared__ float tile[TR_C][TR_MAXT + 1];
+  const int b = blockIdx.y, c0 = blockIdx.x * TR_C;
+  const float* src = x + b * xs_b + (int64_t)c0 * T;
+  const int nc = min(TR_C, C - c0);
+  for (int i = threadIdx.x; i < nc * T; i += blockDim.x) tile[i / T][i % T] = src[i];
+  __syncthreads();
+  float* dst = xt + (int64_t)b * T * C + c0;
+  for (int i = threadIdx.x; i < nc * T; i += blockDim.x) {
+    const int t = i / nc, c = i % nc;
+    dst[(int64_t)t * C + c] = tile[c][t];
+  }
+}
+
 extern "C" {
 
 int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t, int32_t B,
@@ -896,9 +915,33 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
   const int Cq = C / 8, Cqkv = C / 4 + C;
   const int64_t qs_b = (int64_t)Cqkv * T;
   // q, k, v as ONE 1x1 convolution with the stacked weights: qkv[b][0:Cq | Cq:2Cq | 2Cq:][t]
-  int rc = a2m_conv1d_fwd_f32(x, x_bs, T, 1, B, C, T, wqkv, bqkv, Cqkv, 1, 1, 0, nullptr, nullptr,
-                              nullptr, nullptr, 0.f, A2M_ACT_NONE, 0.f, qkv, qs_b, T, 1, ws,
-                              ws_bytes, stream);
+  int rc;
+  static const int btc_ok = std::getenv("A2M_ATTN_BTC") ? std::atoi(std::getenv("A2M_ATTN_BTC")) : 1;
+  if (btc_ok && C >= 1024 && T <= TR_MAXT) {
+    // wide channels (the UNet's SelfAttention(2048)): x is first copied to [B*T][C] so the
+    // projection GEMM reads both operands as dense k-contiguous rows instead of gathering x's
+    // t-runs (mode 3): 255 -> ~220 us for the up_attention projection at T = 32, for a copy of
+    // a few microseconds.  Same k order, so the same result bit for bit.
+    const size_t xt_bytes = (((size_t)B * T * C * sizeof(float)) + 255) & ~size_t(255);
+    const size_t need = xt_bytes + gemm_ws_bytes(Cqkv, B * T, C, 1);
+    if (!ws || ws_bytes < need) {
+      set_error("self_attention: workspace too small (%zu < %zu bytes)", ws_bytes, need);
+      return A2M_EWS;
+    }
+    float* xt = static_cast<float*>(ws);
+    hipLaunchKernelGGL(bct_to_btc_kernel, dim3((unsigned)cdiv(C, TR_C), (unsigned)B), dim3(256), 0, st,
+                       x, x_bs, C, T, xt);
+    A2M_LAUNCH_CHECK();
+    Gather A = dense_rk(wqkv, C);
+    Gather Bx = dense_rk(xt, C);
+    Epilogue E = epi_bn(qkv, bqkv, nullptr, nullptr, nullptr, nullptr, 1e-5f, A2M_ACT_NONE, 0.f);
+    E.N1 = 1; E.N2 = T; E.so0 = (int)qs_b; E.so1 = 0; E.so2 = 1; E.som = T;
+    rc = gemm(A, Bx, E, Cqkv, B * T, C, 1, static_cast<char*>(ws) + xt_bytes, ws_bytes - xt_bytes, st);
+  } else {
+    rc = a2m_conv1d_fwd_f32(x, x_bs, T, 1, B, C, T, wqkv, bqkv, Cqkv, 1, 1, 0, nullptr, nullptr,
+                            nullptr, nullptr, 0.f, A2M_ACT_NONE, 0.f, qkv, qs_b, T, 1, ws,
+                            ws_bytes, stream);
+  }
   if (rc) return rc;
   static const int fused_ok = std::getenv("A2M_ATTN_FUSED") ? std::atoi(std::getenv("A2M_ATTN_FUSED")) : 1;
   if (fused_ok && attn_core_fits(C, T))
