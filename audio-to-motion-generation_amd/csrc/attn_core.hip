@@ -197,7 +197,6 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   // float4 per thread, transposed writes conflict-free (32 lanes = 32 consecutive c).
   // w tile [col][c]: stacked rows Q 0..Cq-1 -> cols 0.., K Cq.. -> 32.., V 2Cq + c0.. -> 64..;
   // two float4 per thread along c.
-  float4 xr[1], wr[2];
   int wrow[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -205,13 +204,14 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
     wrow[u] = col < 32 ? (col < Cq ? col : -1)
                        : col < 64 ? (col - 32 < Cq ? Cq + col - 32 : -1) : 2 * Cq + c0 + col - 64;
   }
-  auto load_tile = [&](int kt) {
+  // two register sets, so a tile's global loads are issued two k-steps before its LDS store
+  // (one step of MFMAs, ~1k cycles, does not cover an L2 / HBM round trip)
+  auto load_tile = [&](int kt, float4& xr, float4 (&wr)[2]) {
     const int cb = kt * FK;
-#pragma unroll
-    for (int u = 0; u < 1; ++u) {
-      const int e = tid + u * 512, c = e & 31, tq = e >> 5;
-      xr[u] = 4 * tq < T ? *reinterpret_cast<const float4*>(xb + (int64_t)(cb + c) * T + 4 * tq)
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    {
+      const int c = tid & 31, tq = tid >> 5;
+      xr = 4 * tq < T ? *reinterpret_cast<const float4*>(xb + (int64_t)(cb + c) * T + 4 * tq)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -220,16 +220,15 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store_tile = [&](float* st) {
+  auto store_tile = [&](float* st, const float4& xr, const float4 (&wr)[2]) {
     float* xs = st;
     float* ws = st + XT;
-#pragma unroll
-    for (int u = 0; u < 1; ++u) {
-      const int e = tid + u * 512, c = e & 31, t = 4 * (e >> 5);
-      xs[(t + 0) * FKP + c] = xr[u].x;
-      xs[(t + 1) * FKP + c] = xr[u].y;
-      xs[(t + 2) * FKP + c] = xr[u].z;
-      xs[(t + 3) * FKP + c] = xr[u].w;
+    {
+      const int c = tid & 31, t = 4 * (tid >> 5);
+      xs[(t + 0) * FKP + c] = xr.x;
+      xs[(t + 1) * FKP + c] = xr.y;
+      xs[(t + 2) * FKP + c] = xr.z;
+      xs[(t + 3) * FKP + c] = xr.w;
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -241,13 +240,7 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int nk = C / FK;
-  load_tile(0);
-  store_tile(lds);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const float* cur = lds + (kt & 1) * STG;
-    if (kt + 1 < nk) load_tile(kt + 1);
+  auto mma_tile = [&](const float* cur) {
     float af[2][8], bf[2][8];
 #pragma unroll
     for (int half = 0; half < 2; ++half) {  // both halves' fragments first
@@ -263,8 +256,25 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
 #pragma unroll
     for (int half = 0; half < 2; ++half)
 #pragma unroll
-      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[half][s], bf[half][s], acc, 0, 0, 0);
-    if (kt + 1 < nk) store_tile(lds + ((kt + 1) & 1) * STG);
+      for (int s2 = 0; s2 < 8; ++s2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[half][s2], bf[half][s2], acc, 0, 0, 0);
+  };
+  const int nk = C / FK;   // even (C in {128, 256})
+  float4 xa, wa[2], xb2, wb2[2];
+  load_tile(0, xa, wa);
+  store_tile(lds, xa, wa);
+  if (nk > 1) load_tile(1, xa, wa);          // set A: tile 1
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    // step kt (stage 0): tile kt+1 waits in set A, tile kt+2 loads into set B
+    if (kt + 2 < nk) load_tile(kt + 2, xb2, wb2);
+    mma_tile(lds);
+    if (kt + 1 < nk) store_tile(lds + STG, xa, wa);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    // step kt+1 (stage 1): tile kt+2 waits in set B, tile kt+3 loads into set A
+    if (kt + 3 < nk) load_tile(kt + 3, xa, wa);
+    mma_tile(lds + STG);
+    if (kt + 2 < nk) store_tile(lds, xb2, wb2);
     __syncthreads();
   }
 
