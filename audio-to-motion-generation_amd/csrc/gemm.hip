@@ -341,7 +341,16 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
   } else {
     static const int ks2 = env_int("A2M_GEMM_KS2", 1);
+    static const int ks3 = env_int("A2M_GEMM_KS3", 1);
+    // few-block launches (one 64x64 block per CU or less) with a tap-chunked or row-gathered B:
+    // two wave groups split the k range (KS = 3), so each SIMD runs two independent k pipelines
+    const int nt = (int)cdiv(K, p.bk);
+    const int kq = mb == 5 ? B.tapconv : 1;
+    const int64_t blocks = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
+    const bool use_ks3 = ks3 && p.bm == 64 && p.splits == 1 && ma == 0 && (mb == 5 || mb == 3) &&
+                         blocks <= 256 && nt % (2 * kq) == 0 && nt >= 8;
     if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
+    else if (use_ks3) launch_tile<64, 64, 32, 0, 3>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
     // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end
     else if (ks2 && ma == 0 && mb == 0) launch_tile<64, 64, 32, 0, 2>(a, ma, mb, batch, stream);

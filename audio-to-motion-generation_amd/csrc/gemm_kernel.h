@@ -705,8 +705,14 @@ __device__ __forceinline__ void ablate_touch(const FR& f, floatx16 (&acc)[TM][TN
 // other's issue gaps at one block per CU); the groups stage alternate k-tiles, the partial
 // accumulators are summed through LDS before the epilogue.  (The k-halves of one k-tile are added in a
 // different order than KS = 1: results agree to fp32 rounding, not bitwise.)
+// KS = 3 (64x64 fp32 tile, any operand modes): 512 threads, two wave groups that each run the
+// whole KS = 1 pipeline (own LDS stages) over one half of the k range, in lockstep barriers;
+// the partial accumulators are summed through LDS as for KS = 2.  For launches with few blocks
+// (one per CU), where a single wave per SIMD leaves the MFMA pipe idle between its own LDS /
+// barrier waits.  The host splits the k range on whole k-tile groups (mode 5: whole channel
+// chunks, all taps).
 template <int BM, int BN, int BK, int MA, int MB, int P, int KS = 1>
-__global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
+__global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs args) {
   static_assert(P == 0 ? (BK == 32 || BK == 64) : BK == (P == 1 ? 64 : 32),
                 "the k-step pipeline assumes two halves per k-tile");
   constexpr int NS = P == 0 ? BK / 32 : 1;   // fp32: 16-k fragment chunks per half
@@ -715,9 +721,10 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
   using LA = TileLoader<BM, BK, MA, P>;
   using LB = TileLoader<BN, BK, MB, P>;
   constexpr int STAGE = LA::TILE + LB::TILE;
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) float lds_all[(KS == 3 ? 4 : 2) * STAGE];
   static_assert(KS == 1 || (TM * TN * 16 * 256 <= 2 * STAGE), "KS = 2 partials must fit the stages");
   const int grp = KS == 1 ? 0 : (int)(threadIdx.x >> 8);
+  float* lds = KS == 3 ? lds_all + grp * 2 * STAGE : lds_all;
   const int tid = threadIdx.x & 255;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -747,8 +754,14 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
   const int zz = bz;
   const int batch = zz / args.splits, split = zz % args.splits;
   const int m0 = by * BM, n0 = bx * BN;
-  const int kbeg = split * args.kchunk;
-  const int kend = min(args.K, kbeg + args.kchunk);
+  int kbeg = split * args.kchunk;
+  int kend = min(args.K, kbeg + args.kchunk);
+  if constexpr (KS == 3) {   // group g: k-tiles [g * nt / 2, (g + 1) * nt / 2) of the block's range
+    const int nt = (kend - kbeg + BK - 1) / BK;
+    const int mid = kbeg + (nt / 2) * BK;
+    if (grp == 0) kend = mid;
+    else kbeg = mid;
+  }
 
   LA la;
   LB lb;
@@ -764,7 +777,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 
   const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
-  if constexpr (KS == 1) {
+  if constexpr (KS == 1 || KS == 3) {
     Frags<TM, TN, P, NS> f0, f1;
     if (nk > 0) {
       la.load(kbeg);
@@ -817,6 +830,30 @@ __global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
       else ablate_touch(f1, acc);
     }
     __syncthreads();  // the m-contiguous epilogue reuses the stages
+    if constexpr (KS == 3) {   // group 1's partial accumulators -> LDS -> group 0
+      if (grp == 1) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+#pragma unroll
+          for (int u = 0; u < TN; ++u)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) lds_all[((t * TN + u) * 16 + q) * 256 + tid] = acc[t][u][q];
+      }
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int t = 0; t < TM; ++t)
+#pragma unroll
+          for (int u = 0; u < TN; ++u)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[t][u][q] += lds_all[((t * TN + u) * 16 + q) * 256 + tid];
+      }
+      __syncthreads();  // the partials region is free again
+      if (grp == 1) {
+        if (args.mcontig) __syncthreads();  // the epilogue's one barrier
+        return;
+      }
+    }
   } else {
     // The groups take turns staging: group j % 2 loads k-tile j three steps ahead and stores it
     // one step ahead, so a tile's global loads have two k-steps to land (one with a single
@@ -948,9 +985,13 @@ template <int BM, int BN, int BK, int P, int KS = 1>
 void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
-  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3(256 * KS), 0, st, a); return; }
+  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3(KS == 1 ? 256 : 512), 0, st, a); return; }
   if constexpr (KS == 2) {  // dense operands only (gemm.hip)
     A2M_L(0, 0)
+    return;
+  }
+  if constexpr (KS == 3) {  // dense / gathered weights x tap-chunked conv1d operands (gemm.hip)
+    A2M_L(0, 5) A2M_L(0, 3) A2M_L(0, 0)
     return;
   }
   A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3) A2M_L(0, 4)
@@ -964,6 +1005,7 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
 
 extern template void launch_tile<64, 64, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 32, 0, 2>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<64, 64, 32, 0, 3>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
