@@ -308,6 +308,21 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     p.splits = (int)cdiv(K, p.kchunk);
   }
   if (K == 0) { p.splits = 1; p.kchunk = p.bk; }
+  // few-block launches (one 64x64 block per CU or less) with a tap-chunked or row-gathered B
+  // split the k range across the block's two wave groups (KS = 3): each SIMD runs two
+  // independent k pipelines.  A2M_GEMM_KS3=2 also turns the planner's two-way split-K plans on
+  // such launches into KS = 3 (no partial-sum round trip or reduce launch); measured slower on
+  // every such launch of the bench step (the groups share every barrier; two independent
+  // blocks per CU do not), so off by default
+  static const int ks3 = env_int("A2M_GEMM_KS3", 1);
+  const int64_t blocks64 = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
+  const int nt_all = (int)cdiv(K, p.bk);
+  bool use_ks3 = prec == 0 && ks3 && p.bm == 64 && ma == 0 && blocks64 <= 256 &&
+                 nt_all % (2 * kquant) == 0 && nt_all >= 8 &&
+                 ((p.splits == 1 && (mb == 5 || mb == 3)) ||
+                  (ks3 >= 2 && p.splits == 2 && force_split <= 0 && g_override_split == 0 &&
+                   (mb == 0 || mb == 3 || mb == 5)));
+  if (use_ks3) { p.splits = 1; p.kchunk = nt_all * p.bk; }
   a.splits = p.splits;
   a.kchunk = p.kchunk;
   a.partial = nullptr;
@@ -341,14 +356,6 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
   } else {
     static const int ks2 = env_int("A2M_GEMM_KS2", 1);
-    static const int ks3 = env_int("A2M_GEMM_KS3", 1);
-    // few-block launches (one 64x64 block per CU or less) with a tap-chunked or row-gathered B:
-    // two wave groups split the k range (KS = 3), so each SIMD runs two independent k pipelines
-    const int nt = (int)cdiv(K, p.bk);
-    const int kq = mb == 5 ? B.tapconv : 1;
-    const int64_t blocks = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
-    const bool use_ks3 = ks3 && p.bm == 64 && p.splits == 1 && ma == 0 && (mb == 5 || mb == 3) &&
-                         blocks <= 256 && nt % (2 * kq) == 0 && nt >= 8;
     if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
     else if (use_ks3) launch_tile<64, 64, 32, 0, 3>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
