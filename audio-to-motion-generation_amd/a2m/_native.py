@@ -36,6 +36,9 @@ SIGNATURES = {
                                            P, P, P, P, F32, I32, F32, P, I64, I64, P, SZ, P]),
     'a2m_convt1d_pack_f32': (ctypes.c_int, [P, I32, I32, I32, I32, I32, P, P]),
     'a2m_conv1d_tap_chunk': (I32, []),
+    'a2m_convt1d_tap_pack_f32': (ctypes.c_int, [P, I32, I32, I32, I32, I32, I32, P, P]),
+    'a2m_convt1d_tap_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, I32, P, I32, I32, I32, I32,
+                                               I32, P, P, P, P, F32, I32, F32, P, I64, I64, P, SZ, P]),
     'a2m_conv2d_pack_nhwc_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P]),
     'a2m_conv2d_nhwc_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32,
                                                I32, P, P, P, P, F32, I32, F32, P, I32, I32, I32,

@@ -77,6 +77,7 @@ def _bn_args(bn):
 
 # ------------------------------------------------------------------------------ convs
 _TAP_CONV = __import__('os').environ.get('A2M_TAP_CONV', '1') != '0'
+_TAP_CONVT = __import__('os').environ.get('A2M_CONVT_TAP', '1') != '0'
 
 
 def _tap_eligible(x, ks, stride, pad, Ci):
@@ -154,9 +155,33 @@ def convt_packed(w, stride, pad, cache=None):
     return packed
 
 
+def convt_tap_packed(w, stride, pad, cache=None):
+    """Per-phase tap-chunked ConvTranspose1d weights for the engine's current k-tile
+    (a2m_convt1d_tap_pack_f32), cached in `cache` per weight version and chunk."""
+    chunk = N.lib.a2m_conv1d_tap_chunk()
+    key = _wkey((w,)) + (stride, pad, 'tap', chunk)
+    if cache is not None and cache.get('key') == key:
+        return cache['w'], chunk
+    Ci, Co, ks = w.shape
+    packed = torch.empty(Ci * Co * ks, device=w.device)
+    N.check(N.lib.a2m_convt1d_tap_pack_f32(_p(w), Ci, Co, ks, stride, pad, chunk, _p(packed), _stream()))
+    if cache is not None:
+        cache.update(key=key, w=packed)
+    return packed, chunk
+
+
+def _convt_tap_eligible(x, stride, Tout):
+    B, Ci, Tin = x.shape
+    return (_TAP_CONVT and Tout == stride * Tin and Tin % 4 == 0 and 64 % Tin == 0 and
+            Ci % N.lib.a2m_conv1d_tap_chunk() == 0 and x.data_ptr() % 16 == 0 and
+            x.stride(0) % 4 == 0 and x.stride(1) % 4 == 0)
+
+
 def convt1d(x, w, b=None, stride=2, pad=1, out_pad=1, bn=None, act=ACT_NONE, slope=0.2, out=None,
             cache=None):
-    """x: [B, Ci, Tin] (t contiguous), w: [Ci, Co, k]; `cache` keeps the packed weights."""
+    """x: [B, Ci, Tin] (t contiguous), w: [Ci, Co, k]; `cache` keeps the packed weights.
+    Clip lengths that tile the engine's 64 rows run each output phase as a tap-chunked conv1d
+    (a2m_convt1d_tap_fwd_f32), others the per-phase gathered GEMM (a2m_convt1d_packed_fwd_f32)."""
     _check_dev(x, w, b, out)
     B, Ci, Tin = x.shape
     assert x.stride(2) == 1 and w.is_contiguous() and w.shape[0] == Ci
@@ -165,6 +190,12 @@ def convt1d(x, w, b=None, stride=2, pad=1, out_pad=1, bn=None, act=ACT_NONE, slo
     if out is None:
         out = torch.empty(B, Co, Tout, device=x.device, dtype=x.dtype)
     assert tuple(out.shape) == (B, Co, Tout) and out.stride(2) == 1
+    if _convt_tap_eligible(x, stride, Tout):
+        packed, chunk = convt_tap_packed(w, stride, pad, cache)
+        _with_ws(x.device, lambda wp, wn: N.lib.a2m_convt1d_tap_fwd_f32(
+            _p(x), x.stride(0), x.stride(1), B, Ci, Tin, _p(packed), chunk, _p(b), Co, ks, stride, pad,
+            out_pad, *_bn_args(bn), act, slope, _p(out), out.stride(0), out.stride(1), wp, wn, _stream()))
+        return out
     packed = convt_packed(w, stride, pad, cache)
     _with_ws(x.device, lambda wp, wn: N.lib.a2m_convt1d_packed_fwd_f32(
         _p(x), x.stride(0), x.stride(1), B, Ci, Tin, _p(packed), _p(b), Co, ks, stride, pad, out_pad,

@@ -251,6 +251,29 @@ __global__ void convt_pack_kernel(const float* w, int Ci, int Co, int ks, int s,
   }
 }
 
+// ConvTranspose1d weights [Ci][Co][ks] -> per output phase r, tap-chunked for loader mode 5:
+// P_r[co][(cc*nt + j')*CH + cl] = W[cc*CH + cl][co][kk0 + (nt - 1 - j')*s].  Taps are reversed
+// (j' = nt - 1 - j) so that tap j' reads input u + (off0 - nt + 1) + j', an ascending shift
+// like a stride-1 conv1d's; phases back to back as in convt_pack_kernel.
+__global__ void convt_tap_pack_kernel(const float* w, int Ci, int Co, int ks, int s, int pad, int ch,
+                                      float* out) {
+  const int64_t total = (int64_t)Ci * Co * ks;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % ks);
+    const int64_t t = i / ks;
+    const int co = (int)(t % Co), ci = (int)(t / Co);
+    const int r = (((kk - pad) % s) + s) % s;
+    int64_t off = 0;
+    int kk0;
+    for (int rr = 0; rr < r; ++rr) off += (int64_t)Co * Ci * phase_taps(rr, ks, s, pad, &kk0);
+    const int nt = phase_taps(r, ks, s, pad, &kk0);
+    const int jr = nt - 1 - (kk - kk0) / s;
+    const int cc = ci / ch, cl = ci - cc * ch;
+    out[off + (int64_t)co * nt * Ci + ((int64_t)cc * nt + jr) * ch + cl] = w[i];
+  }
+}
+
 // Conv1d weights [Co][Ci][ks] -> tap-chunked [Co][Ci/CH][ks][CH] (the k order of loader mode 5)
 __global__ void conv1d_tap_pack_kernel(const float* w, int Co, int Ci, int ks, int ch, float* out) {
   const int64_t total = (int64_t)Co * Ci * ks;
@@ -570,6 +593,74 @@ int a2m_convt1d_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int
                      dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Ci * Co * ks, 256), 8192)),
                      dim3(256), 0, as_stream(stream), w, Ci, Co, ks, stride, pad, packed);
   A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_convt1d_tap_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int32_t stride,
+                             int32_t pad, int32_t chunk, float* packed, void* stream) {
+  A2M_CHECK_ARG(w && packed && Ci > 0 && Co > 0 && ks > 0 && stride > 0 && pad >= 0 &&
+                    (chunk == 32 || chunk == 64) && Ci % chunk == 0,
+                "convt1d_tap_pack: bad args Ci=%d Co=%d k=%d s=%d p=%d chunk=%d", Ci, Co, ks, stride,
+                pad, chunk);
+  A2M_CHECK_ARG(fits32((int64_t)Ci * Co * ks), "convt1d_tap_pack: too large");
+  hipLaunchKernelGGL(convt_tap_pack_kernel,
+                     dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Ci * Co * ks, 256), 8192)),
+                     dim3(256), 0, as_stream(stream), w, Ci, Co, ks, stride, pad, chunk, packed);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_convt1d_tap_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
+                            int32_t Tin, const float* packed, int32_t chunk, const float* bias,
+                            int32_t Co, int32_t ks, int32_t stride, int32_t pad, int32_t out_pad,
+                            const float* bn_w, const float* bn_b, const float* bn_rm,
+                            const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
+                            int64_t ys_b, int64_t ys_c, void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && packed && y, "convt1d_tap: null pointer");
+  const int Tout = (Tin - 1) * stride - 2 * pad + ks + out_pad;
+  A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && ks > 0 && stride > 0 && pad >= 0 && Tout == stride * Tin,
+                "convt1d_tap: bad shape B=%d Ci=%d T=%d Co=%d k=%d s=%d p=%d op=%d (every output "
+                "phase must hold Tin rows)", B, Ci, Tin, Co, ks, stride, pad, out_pad);
+  A2M_CHECK_ARG(chunk == gemm_k_tile() && Ci % chunk == 0,
+                "convt1d_tap: weights packed in %d-channel chunks, the engine's k-tile is %d (Ci=%d)",
+                chunk, gemm_k_tile(), Ci);
+  A2M_CHECK_ARG(Tin % 4 == 0 && 64 % Tin == 0,
+                "convt1d_tap: clip length %d must divide the 64-row tile and be a multiple of 4", Tin);
+  A2M_CHECK_ARG(fits32(xs_b) && fits32(xs_c) && fits32((int64_t)B * xs_b) &&
+                    fits32((int64_t)B * ys_b) && fits32(ys_c) && fits32((int64_t)Ci * Co * ks),
+                "convt1d_tap: tensor too large for 32-bit offsets");
+  A2M_CHECK_ARG((reinterpret_cast<uintptr_t>(x) % 16) == 0 && xs_b % 4 == 0 && xs_c % 4 == 0,
+                "convt1d_tap: x rows must be 16-byte aligned");
+  // Output phase r = the stride-1 conv1d (loader mode 5) of x with the phase's nt taps at input
+  // shifts off0 - nt + 1 .. off0 (a2m_convt1d_tap_pack_f32's reversed tap order), written to
+  // y[.., s*u + r]: the same phase decomposition as a2m_convt1d_packed_fwd_f32, with each
+  // chunk's x window loaded once for all of the phase's taps instead of gathered per tap.
+  hipStream_t st = as_stream(stream);
+  size_t off = 0;
+  for (int r = 0; r < stride; ++r) {
+    int kk0 = -1, ntap = 0;
+    for (int kk = 0; kk < ks; ++kk)
+      if ((((r + pad - kk) % stride) + stride) % stride == 0) { if (kk0 < 0) kk0 = kk; ++ntap; }
+    float* yr = y + r;
+    Epilogue E = epi_bn(yr, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+    E.N1 = 1; E.N2 = Tin; E.so0 = (int)ys_b; E.so1 = 0; E.so2 = stride; E.som = (int)ys_c;
+    if (ntap == 0) {  // this phase only gets the bias / BN / act of zero
+      int rc = gemm(dense_rk(packed, 1), dense_rk(x, 1), E, Co, B * Tin, 0, 1, nullptr, 0, st);
+      if (rc) return rc;
+      continue;
+    }
+    const int cw = (r + pad - kk0) / stride - ntap + 1;
+    A2M_CHECK_ARG(cw > -Tin && cw + ntap - 1 < Tin, "convt1d_tap: tap shift %d..%d outside the clip",
+                  cw, cw + ntap - 1);
+    Gather Bg{};
+    Bg.base = x; Bg.bstride = 0;
+    Bg.sr0 = (int)xs_b; Bg.R1 = 1; Bg.R2 = Tin; Bg.sk0 = (int)xs_c;
+    Bg.K1 = Bg.K2 = 1; Bg.divh = Bg.divw = 1; Bg.Lh = Bg.Lw = 1;
+    Bg.cw = cw; Bg.tapconv = ntap;
+    int rc = gemm(dense_rk(packed + off, ntap * Ci), Bg, E, Co, B * Tin, ntap * Ci, 1, ws, ws_bytes, st);
+    if (rc) return rc;
+    off += (size_t)Co * ntap * Ci;
+  }
   return A2M_OK;
 }
 

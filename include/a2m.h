@@ -111,6 +111,20 @@ int a2m_convt1d_packed_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32
                                const float* bn_w, const float* bn_b, const float* bn_rm,
                                const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
                                int64_t ys_b, int64_t ys_c, void* ws, size_t ws_bytes, void* stream);
+/* The same forward with each phase as a stride-1 tap-chunked conv1d (the GEMM engine's loader
+ * mode 5: a channel chunk's x window is loaded once for all of the phase's taps).  Weights
+ * packed per phase in `chunk`-channel chunks with reversed taps (chunk = a2m_conv1d_tap_chunk(),
+ * Ci % chunk == 0); every phase must hold Tin outputs (Tout = stride * Tin), Tin % 4 == 0 and
+ * 64 % Tin == 0, x rows 16-byte aligned.  Replaces nn.ConvTranspose1d.forward at the
+ * ConvTranspose1D shapes (model_layers.py:193-215, the UNet up path at :325). */
+int a2m_convt1d_tap_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int32_t stride,
+                             int32_t pad, int32_t chunk, float* packed, void* stream);
+int a2m_convt1d_tap_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t Ci,
+                            int32_t Tin, const float* packed, int32_t chunk, const float* bias,
+                            int32_t Co, int32_t ks, int32_t stride, int32_t pad, int32_t out_pad,
+                            const float* bn_w, const float* bn_b, const float* bn_rm,
+                            const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
+                            int64_t ys_b, int64_t ys_c, void* ws, size_t ws_bytes, void* stream);
 
 /* Channels-last conv2d for the AudioEncoder eval chain (model_layers.py:219-280,
  * ConvNormRelu(type='2d') layers): x NHWC [B][H][W][Ci] (the mel [B][T][F] is already NHWC with

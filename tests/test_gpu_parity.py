@@ -120,7 +120,8 @@ def test_conv1d_strided_views_and_linear():
     assert rel_err(out.cpu(), ref) < TOL
 
 
-@pytest.mark.parametrize('B,Ci,Co,T', [(2, 64, 32, 8), (3, 2048, 1024, 16), (2, 40, 24, 7)])
+@pytest.mark.parametrize('B,Ci,Co,T', [(2, 64, 32, 8), (3, 2048, 1024, 16), (2, 1024, 512, 32),
+                                        (2, 40, 24, 7)])
 def test_convt1d_bn_relu(B, Ci, Co, T):
     from a2m import functional as F
     x, w, b = _rand(B, Ci, T, seed=20), _rand(Ci, Co, 3, seed=21, scale=0.1), _rand(Co, seed=22)
@@ -130,6 +131,30 @@ def test_convt1d_bn_relu(B, Ci, Co, T):
     d = [t.to(DEV) for t in (x, w, b, bw, bb, rm, rv)]
     out = F.convt1d(d[0], d[1], d[2], bn=(d[3], d[4], d[5], d[6], 1e-5), act=F.ACT_RELU)
     assert out.shape == ref.shape and rel_err(out.cpu(), ref) < TOL
+
+
+@pytest.mark.parametrize('ks,stride,pad,op,T', [(3, 2, 1, 1, 16), (4, 2, 1, 0, 8), (5, 2, 2, 1, 32),
+                                                (3, 1, 1, 0, 16), (6, 4, 1, 0, 4), (2, 2, 0, 0, 64)])
+def test_convt1d_tap_path(ks, stride, pad, op, T):
+    """The tap-chunked ConvTranspose1d (a2m_convt1d_tap_fwd_f32, loader mode 5 per output
+    phase) against torch and against the gathered per-phase path on the same inputs."""
+    from a2m import functional as F
+    from a2m import _native as NN
+    B, Ci, Co = 3, 96, 40
+    x, w, b = _rand(B, Ci, T, seed=27), _rand(Ci, Co, ks, seed=28, scale=0.1), _rand(Co, seed=29)
+    ref = torch.nn.functional.conv_transpose1d(x, w, b, stride=stride, padding=pad, output_padding=op)
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    assert F._convt_tap_eligible(xd, stride, ref.shape[2])
+    out = F.convt1d(xd, wd, bd, stride, pad, op)
+    assert out.shape == ref.shape and rel_err(out.cpu(), ref) < TOL
+    Tout = ref.shape[2]
+    packed = F.convt_packed(wd, stride, pad)
+    gathered = torch.empty(B, Co, Tout, device=DEV)
+    F._with_ws(xd.device, lambda wp, wn: NN.lib.a2m_convt1d_packed_fwd_f32(
+        F._p(xd), xd.stride(0), xd.stride(1), B, Ci, T, F._p(packed), F._p(bd), Co, ks, stride, pad, op,
+        *F._bn_args(None), F.ACT_NONE, 0.2, F._p(gathered), gathered.stride(0), gathered.stride(1), wp, wn,
+        F._stream()))
+    assert rel_err(out.cpu(), gathered.cpu()) < TOL
 
 
 def test_conv2d_column_range():
