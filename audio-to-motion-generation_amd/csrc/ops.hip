@@ -691,17 +691,22 @@ int a2m_convt1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, i
 // (model_layers.py:60-118 at the AudioEncoder shapes).  Rows are written along k, four
 // consecutive k per thread (float4 stores); the input reads are L2 hits (each element is read
 // kh*kw / stride^2 times).
+constexpr int I2C2_QUADS = 256;   // k quads per workgroup (one per thread)
 __global__ __launch_bounds__(256) void im2col2d_kernel(const float* __restrict__ x, int Ci, int H, int W,
                                                        int kh, int kw, int stride, int ph, int pw,
                                                        int Hout, int Wn, int w_lo, int K,
                                                        float* __restrict__ col) {
-  // one workgroup per (b, ho): each thread decomposes its four k = (ci, i, j) once and then
-  // writes them for every live column wn (the k -> input-row arithmetic is amortised over Wn)
+  // workgroup (b, ho) x k-range: each thread decomposes its four k = (ci, i, j) once and then
+  // writes them for every live column wn (the k -> input-row arithmetic is amortised over Wn).
+  // With one live column the k range is split over blockIdx.y (one quad per thread): conv5's
+  // im2col 18.5 -> 14.7 us.  With several columns the split measured slower (27.0 -> 30.4 us at
+  // conv3), and so did staging the input patch in LDS (26.3 / 20.6 / 32.4 us at conv3 / 4 / 5):
+  // all of these run at 1.5-2 TB/s of columns, like the other copy kernels of the step.
   const int ho = blockIdx.x % Hout, b = blockIdx.x / Hout;
   const int hb = ho * stride - ph;
   const int khw = kh * kw;
-  float* rows = col + (int64_t)blockIdx.x * Wn * K;
-  for (int k0 = threadIdx.x * 4; k0 < K; k0 += blockDim.x * 4) {
+  for (int k0 = (blockIdx.y * I2C2_QUADS + threadIdx.x) * 4; k0 < K; k0 += gridDim.y * I2C2_QUADS * 4) {
+    float* rows = col + (int64_t)blockIdx.x * Wn * K + k0;
     const float* src[4];
     int jj[4];
     bool hv[4];
@@ -715,6 +720,7 @@ __global__ __launch_bounds__(256) void im2col2d_kernel(const float* __restrict__
       src[q] = x + ((int64_t)(b * Ci + ci) * H + (hv[q] ? h : 0)) * W;
       jj[q] = j;
     }
+#pragma unroll 2
     for (int wn = 0; wn < Wn; ++wn) {
       const int wb = (w_lo + wn) * stride - pw;
       float v[4];
@@ -723,7 +729,7 @@ __global__ __launch_bounds__(256) void im2col2d_kernel(const float* __restrict__
         const int w = wb + jj[q];
         v[q] = (hv[q] && w >= 0 && w < W) ? src[q][w] : 0.f;
       }
-      *reinterpret_cast<float4*>(rows + (int64_t)wn * K + k0) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(rows + (int64_t)wn * K) = make_float4(v[0], v[1], v[2], v[3]);
     }
   }
 }
@@ -772,8 +778,9 @@ int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t
     }
     float* col = static_cast<float*>(ws);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(im2col2d_kernel, dim3((unsigned)(B * Hout)), dim3(256), 0, st, x, Ci, H, W, kh,
-                       kw, stride, pad_h, pad_w, Hout, Wn, w_lo, (int)K, col);
+    const unsigned ksplit = Wn == 1 ? (unsigned)cdiv(K, 4 * I2C2_QUADS) : 1u;
+    hipLaunchKernelGGL(im2col2d_kernel, dim3((unsigned)(B * Hout), ksplit), dim3(256), 0, st, x, Ci, H,
+                       W, kh, kw, stride, pad_h, pad_w, Hout, Wn, w_lo, (int)K, col);
     A2M_LAUNCH_CHECK();
     Gather Bd = dense_rk(col, (int)K);
     Epilogue E = epi_bn(y + w_lo, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);

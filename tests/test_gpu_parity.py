@@ -157,6 +157,26 @@ def test_convt1d_tap_path(ks, stride, pad, op, T):
     assert rel_err(out.cpu(), gathered.cpu()) < TOL
 
 
+@pytest.mark.parametrize('Ci,Co,k,stride,pad,H,W,cols', [
+    (128, 128, (4, 4), 2, (1, 1), 16, 32, (3, 13)),    # AudioEncoder conv3 geometry, LDS patch
+    (256, 128, (3, 3), 1, (1, 1), 8, 16, (4, 12)),     # conv4 geometry
+    (256, 128, (3, 8), 1, (0, 0), 8, 16, (4, 5)),      # conv5 geometry (one live column)
+    (1024, 128, (4, 4), 1, (1, 1), 6, 12, (0, 13)),    # wide K, every column
+])
+def test_conv2d_im2col_paths(Ci, Co, k, stride, pad, H, W, cols):
+    """Column-range conv2d on the im2col + dense GEMM path (Co >= 128, K >= 2048; one live
+    column takes the k-split im2col grid) against torch on the live columns."""
+    from a2m import functional as F
+    x, w, b = _rand(2, Ci, H, W, seed=33), _rand(Co, Ci, *k, seed=34, scale=0.05), _rand(Co, seed=35)
+    assert Ci * k[0] * k[1] >= 2048
+    ref = torch.nn.functional.conv2d(x, w, b, stride=stride, padding=pad)
+    lo, hi = cols
+    hi = min(hi, ref.shape[3])
+    out = torch.full(ref.shape, float('nan'), device=DEV)
+    F.conv2d(x.to(DEV), w.to(DEV), b.to(DEV), stride, pad, cols=(lo, hi), out=out)
+    assert rel_err(out[..., lo:hi].cpu(), ref[..., lo:hi]) < TOL
+
+
 def test_conv2d_column_range():
     from a2m import functional as F
     x, w, b = _rand(2, 8, 16, 32, seed=30), _rand(12, 8, 4, 4, seed=31, scale=0.2), _rand(12, seed=32)
