@@ -45,3 +45,17 @@ for (Ci, Co, T) in [(2048, 1024, 16), (1024, 512, 32)]:
         print(f'convT {Ci}->{Co} T={T} tile {tile} split {split}: {us:6.1f} us '
               f'{2 * Co * Ci * 3 * 64 * T / us / 1e6:5.1f} TF', flush=True)
 NN.lib.a2m_gemm_plan_override(0, 0)
+
+# the encoder's conv1 (64 -> 128, 4x4 s2 p1) on the channels-last path (loader mode 4), the 22
+# live columns of the bench geometry
+if os.environ.get('PROBE_CONV1', '1') == '1':
+    x = torch.randn(64, 32, 64, 64, device=dev)
+    w = torch.randn(128, 64, 4, 4, device=dev) * 0.05
+    b = torch.randn(128, device=dev)
+    cache = {}
+    for tile, split in plans:
+        NN.lib.a2m_gemm_plan_override(tile, split)
+        us = t(lambda: F.conv2d_nhwc(x, w, b, 2, (1, 1), cols=(5, 27), cache=cache))
+        print(f'conv1 nhwc 64->128 cols 22 tile {tile} split {split}: {us:6.1f} us '
+              f'{2 * 128 * 1024 * 64 * 16 * 22 / us / 1e6:5.1f} TF', flush=True)
+    NN.lib.a2m_gemm_plan_override(0, 0)
