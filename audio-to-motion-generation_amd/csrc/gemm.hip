@@ -315,9 +315,10 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   // every such launch of the bench step (the groups share every barrier; two independent
   // blocks per CU do not), so off by default
   static const int ks3 = env_int("A2M_GEMM_KS3", 1);
+  static const int ks3_maxb = env_int("A2M_GEMM_KS3_MAXB", 256);
   const int64_t blocks64 = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
   const int nt_all = (int)cdiv(K, p.bk);
-  bool use_ks3 = prec == 0 && ks3 && p.bm == 64 && ma == 0 && blocks64 <= 256 &&
+  bool use_ks3 = prec == 0 && ks3 && p.bm == 64 && ma == 0 && blocks64 <= ks3_maxb &&
                  nt_all % (2 * kquant) == 0 && nt_all >= 8 &&
                  ((p.splits == 1 && (mb == 5 || mb == 3)) ||
                   (ks3 >= 2 && p.splits == 2 && force_split <= 0 && g_override_split == 0 &&
