@@ -332,6 +332,22 @@ def test_channel_attention_layernorm_mean_repeat():
     assert torch.equal(buf[:, 10:].cpu(), x[:, :10, :1].expand(3, 10, 4)) and buf[:, :10].abs().max() == 0
 
 
+@pytest.mark.parametrize('B,T,D', [(3, 64, 256), (2, 32, 200), (2, 20, 256), (1, 16, 512)])
+def test_layernorm_to_bct_paths(B, T, D):
+    """LayerNorm of [B*T][D] rows written as [B][D][T] (the decoders' permute), values and the
+    saved mean / rstd, against torch, for D up to the kernel's 512 and ragged D / T."""
+    from a2m import functional as F
+    rows = _rand(B * T, D, seed=68)
+    w, b = _rand(D, seed=69).abs() + .5, _rand(D, seed=70)
+    ref = torch.nn.functional.layer_norm(rows, (D,), w, b).view(B, T, D).permute(0, 2, 1)
+    stats = {}
+    out = F.layernorm_to_bct(rows.to(DEV), w.to(DEV), b.to(DEV), T, stats=stats)
+    assert out.shape == ref.shape and rel_err(out.cpu(), ref) < TOL
+    assert rel_err(stats['mean'].cpu(), rows.mean(1)) < TOL
+    var = rows.var(1, unbiased=False)
+    assert rel_err(stats['rstd'].cpu(), 1.0 / torch.sqrt(var + 1e-5)) < TOL
+
+
 @pytest.mark.parametrize('part,J,lo', [('body', 10, 0), ('hand', 42, 10)])
 def test_graph_layers_vs_oracle(part, J, lo):
     from a2m import functional as F
