@@ -437,6 +437,20 @@ __global__ __launch_bounds__(256, 2) void attn_core_wide_kernel(
       vf[m][kc][1] = j + 4 < T ? *reinterpret_cast<const float4*>(vr + j + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  // the epilogue's x (and residual) values, fetched now so their latency hides behind the
+  // score / softmax phases instead of following the PV MFMAs
+  float xv[2][16], rv[2][16];
+  if (li < T) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = c0 + wave * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int64_t o = (int64_t)blockIdx.y * x_bs + (int64_t)c * T + li;
+        xv[m][r] = x[o];
+        rv[m][r] = res ? res[o] : 0.f;
+      }
+  }
   // Q^T, K^T into LDS (float4 along t, written transposed); rows t >= T are zero
   {
     const int nq = Cq * (T / 4);
@@ -557,8 +571,8 @@ __global__ __launch_bounds__(256, 2) void attn_core_wide_kernel(
       for (int r = 0; r < 16; ++r) {
         const int c = c0 + wave * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         const int64_t o = (int64_t)b * x_bs + (int64_t)c * T + li;
-        float val = g * acc[r] + x[o];
-        if (res) val += res[o];
+        float val = g * acc[r] + xv[m][r];
+        if (res) val += rv[m][r];
         y[o] = val;
       }
     }
