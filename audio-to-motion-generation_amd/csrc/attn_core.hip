@@ -302,6 +302,19 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   }
   __syncthreads();
 
+  // waves 4-7 (PV + epilogue) fetch their x / residual values now, while waves 0-3 run the
+  // score product and the softmax, instead of after their PV MFMAs
+  float xv[16], rv[16];
+  if (wave >= 4 && wc * 32 + li < T) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = c0 + wt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int64_t o = (int64_t)b * x_bs + (int64_t)c * T + wc * 32 + li;
+      xv[r] = x[o];
+      rv[r] = res ? res[o] : 0.f;
+    }
+  }
+
   // S[i][j] = sum_c' Q^T[i][c'] K^T[j][c']: waves 0-3, wave (wt, wc) owns the 32 x 32 tile
   floatx16 sacc;
 #pragma unroll
@@ -386,8 +399,8 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
     for (int r = 0; r < 16; ++r) {
       const int c = c0 + wt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
       const int64_t o = (int64_t)b * x_bs + (int64_t)c * T + i;
-      float val = g * sacc[r] + x[o];
-      if (res) val += res[o];
+      float val = g * sacc[r] + xv[r];
+      if (res) val += rv[r];
       y[o] = val;
     }
   }
