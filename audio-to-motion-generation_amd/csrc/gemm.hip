@@ -203,7 +203,9 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   const double fixed = prec == 2 ? (tile == 128 ? 15.0 : 2.0)
                                  : (tile == 128 ? (gathered ? 16.0 : 10.0) : 3.0);
   double t = per_cu * block_flops / thr + cdiv(per_cu, occ) * fixed + 4.0;
-  if (splits > 1) t += (splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0;
+  // A2M_GEMM_SPLIT_COST (percent, experiments): scales the reduce term
+  static const double red_scale = env_int("A2M_GEMM_SPLIT_COST", 100) / 100.0;
+  if (splits > 1) t += red_scale * ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0);
   return t;
 }
 
