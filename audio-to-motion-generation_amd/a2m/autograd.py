@@ -431,9 +431,19 @@ class _PoseLosses(torch.autograd.Function):
         return dgen, None, None
 
 
+def _no_real_grad(real, what):
+    """The backward kernels produce d/d(generated pose) only.  The reference's losses are also
+    differentiable in the real pose, which its training loop never asks for (the real pose is
+    data); asking for it here is an error rather than a silently missing gradient."""
+    if torch.is_grad_enabled() and real is not None and real.requires_grad:
+        raise NotImplementedError(f'{what}: gradient with respect to the real pose is not '
+                                  f'implemented (detach it)')
+
+
 def pose_losses(gen, real=None, angle_w=F.ANGLE_W):
     """[bone, angle] with autograd when an input needs it (the plain HIP op otherwise)."""
-    if torch.is_grad_enabled() and (gen.requires_grad or (real is not None and real.requires_grad)):
+    _no_real_grad(real, 'pose_losses')
+    if torch.is_grad_enabled() and gen.requires_grad:
         return _PoseLosses.apply(gen, real, angle_w)
     return F.pose_losses(gen.contiguous(), real.contiguous() if real is not None else None, angle_w)
 
@@ -456,6 +466,7 @@ class _MotionTerms(torch.autograd.Function):
 
 
 def motion_terms(fake_pose, real_pose):
+    _no_real_grad(real_pose, 'motion_terms')
     return _MotionTerms.apply(fake_pose, real_pose)
 
 

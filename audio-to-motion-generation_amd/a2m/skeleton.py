@@ -54,15 +54,22 @@ def edge_index(lo, n):
 
 def in_neighbour_csr(ei, n):
     """CSR over targets: for node i the sources of edges into i, in edge order (the order a
-    PyG scatter visits them)."""
+    PyG scatter visits them).  Raises ValueError for topologies beyond the graph kernels'
+    limits (include/a2m.h): <= 128 nodes, in-degree <= 7 (8 with GAT's self loop), and
+    ptr + idx entries <= 256 (the block-local CSR the kernels stage in LDS)."""
     src, dst = ei[0].tolist(), ei[1].tolist()
+    if n > 128:
+        raise ValueError(f'graph of {n} nodes: the graph kernels support at most 128')
     ptr, idx = [0], []
     for i in range(n):
         idx += [s for s, d in zip(src, dst) if d == i]
         ptr.append(len(idx))
-        # the fused graph kernel keeps <= 8 in-neighbours (incl. GAT's self loop) per node
-        assert ptr[-1] - ptr[-2] <= 7, 'in-degree > 7 is not supported by the graph kernel'
-    assert n <= 128, 'graphs of more than 128 nodes are not supported by the graph kernel'
+        if ptr[-1] - ptr[-2] > 7:
+            raise ValueError(f'node {i} has in-degree {ptr[-1] - ptr[-2]}: the graph kernels '
+                             f'support at most 7 (+ the GAT self loop)')
+    if len(ptr) + len(idx) > 256:
+        raise ValueError(f'{len(idx)} edges over {n} nodes: the graph kernels hold at most '
+                         f'{256 - (n + 1)} edges for this node count')
     return torch.tensor(ptr, dtype=torch.int32), torch.tensor(idx, dtype=torch.int32)
 
 

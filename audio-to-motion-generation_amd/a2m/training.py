@@ -8,8 +8,8 @@ over clips with one process per GPU.
 
 Data parallelism: every rank runs the step on its shard of the batch.
 Gradients of the network being stepped are averaged by GradReducer: the optimiser's flat
-gradient buffer is cut into ~25 MB buckets in reverse parameter order (the order backward
-produces them), and each bucket's all-reduce (RCCL over xGMI on MI355X, gloo in CPU tests)
+gradient buffer is cut into buckets in reverse parameter order (the order backward produces
+them); a bucket closes once it holds at least bucket_mb (25 MB by default), and each bucket's all-reduce (RCCL over xGMI on MI355X, gloo in CPU tests)
 is launched from a post-accumulate-grad hook as soon as its last gradient lands, so it runs
 on the communication stream while the rest of the backward computes.  Buckets launch strictly
 in order, so every rank issues the same collective sequence.  Optionally the buckets travel
@@ -175,6 +175,7 @@ class GradReducer:
         self.handles = []
         self.active = False
         self.in_backward = 0       # buckets launched from hooks, i.e. overlapped with backward
+        self.error = None
 
     def begin(self):
         """Arm the hooks for one backward (call after zero_grad, before backward)."""
@@ -190,8 +191,12 @@ class GradReducer:
                 return
             b = self.bucket_of[i]
             if i not in self.expected or b < self.next:
-                raise RuntimeError(f'GradReducer: gradient of parameter {i} arrived after its bucket '
-                                   f'was reduced (the set of parameters with gradients changed)')
+                # not raised here: the other ranks would block in their next bucket's
+                # all-reduce.  finish() launches every bucket in order regardless, then all
+                # ranks agree on the error and raise together
+                self.error = (f'GradReducer: gradient of parameter {i} arrived after its bucket '
+                              f'was reduced (the set of parameters with gradients changed)')
+                return
             self.pending[b] -= 1
             while self.next < len(self.buckets) and self.pending[self.next] == 0:
                 self._launch(self.next)
@@ -234,12 +239,22 @@ class GradReducer:
             self.next += 1
         if self.expected is None:
             self.expected = set(self.arrived)
-        elif not self.arrived <= self.expected:
-            raise RuntimeError('GradReducer: parameters outside the learnt set received gradients')
+        elif self.error is None and not self.arrived <= self.expected:
+            self.error = 'GradReducer: parameters outside the learnt set received gradients'
         for sl, buf, work in self.handles:
             work.wait()
             if buf is not sl:
                 sl.copy_(buf)
+        # every rank has issued the same bucket sequence; now agree on whether any rank saw a
+        # gradient outside the plan (or learnt a different parameter set), and fail together
+        n = len(self.expected)
+        flag = torch.tensor([1.0 if self.error else 0.0, n, -n], dtype=torch.float64,
+                            device=self.opt.flat_grad.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        if flag[0].item() > 0 or flag[1].item() != -flag[2].item():
+            self.active = False
+            raise RuntimeError(self.error or 'GradReducer: another rank received gradients outside '
+                                             'the learnt parameter set')
         self.opt.flat_grad.div_(self.world)
         self.active = False
         return self.opt.flat_grad
@@ -250,7 +265,7 @@ class GANTrainer:
 
     def __init__(self, generator, discriminator, lr=10e-4, lambda_gan=1.0, lambda_d=1.0,
                  dynamic=None, fixed_labels=None, process_group=None, sync_bn=False,
-                 bucket_mb=25.0, grad_reduce_dtype=None, label_seed=0):
+                 bucket_mb=25.0, grad_reduce_dtype=None, label_seed=None):
         self.G, self.D = generator, discriminator
         self.opt_G = FlatAdam(generator.parameters(), lr=lr)
         self.opt_D = FlatAdam(discriminator.parameters(), lr=lr)
@@ -275,6 +290,20 @@ class GANTrainer:
             dist.all_reduce(t, group=self.pg)
             t.div_(self.world)
 
+    def _shared_label_seed(self, dev):
+        """label_seed, or (None) a seed that follows the user's torch.manual_seed like the
+        reference's global-RNG draw (version5_model_train.py:169,178): torch.initial_seed() of
+        rank 0, broadcast so every rank draws the same global-batch labels."""
+        if self.label_seed is not None:
+            return int(self.label_seed)
+        seed = torch.initial_seed() & ((1 << 62) - 1)
+        if self.world > 1:
+            t = torch.tensor([seed], dtype=torch.int64, device=dev)
+            dist.broadcast(t, src=dist.get_global_rank(self.pg, 0) if self.pg is not None else 0,
+                           group=self.pg)
+            seed = int(t.item())
+        return seed
+
     def _labels(self, epoch, B, dev):
         """Labels for this rank's shard: the global batch (B x world) is drawn from a generator
         seeded identically on every rank and sliced, so a DP run sees the labels of the
@@ -283,7 +312,7 @@ class GANTrainer:
             v, f = self.fixed_labels
             return torch.full((B, 4), v, device=dev), torch.full((B, 4), f, device=dev)
         if self._label_gen is None or self._label_gen.device != torch.device(dev):
-            self._label_gen = torch.Generator(device=dev).manual_seed(self.label_seed)
+            self._label_gen = torch.Generator(device=dev).manual_seed(self._shared_label_seed(dev))
         Bg, lo = B * self.world, B * self.rank
         real = self.dyn.get_smooth_labels(epoch, Bg, dev, True, generator=self._label_gen)
         fake = self.dyn.get_smooth_labels(epoch, Bg, dev, False, generator=self._label_gen)

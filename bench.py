@@ -202,8 +202,29 @@ def run_mel_kernel(dev, wave, iters=50):
     return ms, nbytes
 
 
+def cgroup_cpus():
+    """CPUs this job is granted by its cgroup's CPU quota (cgroup v2 cpu.max "quota period", or
+    v1 cfs_quota_us / cfs_period_us), as (cpus or None, the raw quota string)."""
+    for path in ('/sys/fs/cgroup/cpu.max',):
+        try:
+            with open(path) as f:
+                raw = f.read().strip()
+            q, per = raw.split()[:2]
+            return (None if q == 'max' else max(1, -(-int(q) // int(per)))), f'{path}: {raw}'
+        except (OSError, ValueError):
+            pass
+    try:
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as f:
+            q = int(f.read())
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as f:
+            per = int(f.read())
+        return (None if q <= 0 else max(1, -(-q // per))), f'cfs_quota_us {q} / cfs_period_us {per}'
+    except (OSError, ValueError):
+        return None, 'no cgroup CPU quota found'
+
+
 def host_cpu():
-    """CPU model and core counts of the host the baseline runs on."""
+    """CPU model, physical cores, CPUs in the affinity mask, and the cgroup-granted CPUs."""
     model = 'unknown'
     try:
         with open('/proc/cpuinfo') as f:
@@ -222,19 +243,23 @@ def host_cpu():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count()
-    return model, phys, avail
+    granted, quota = cgroup_cpus()
+    return model, phys, avail, granted, quota
 
 
 def cpu_baseline(B=64, T=64, max_s=40.0):
     """torch-CPU fp32 oracle port (numpy float64 mel + functional G) on the bench's own
-    workload shape (B clips x T frames), timed on this host's cores: one warm-up, then the
-    median of up to 5 runs within max_s."""
+    workload shape (B clips x T frames), timed on this host's cores (all the
+    cores the job may use -- the affinity mask capped by the cgroup CPU quota): two warm-up
+    runs, then the median of up to 5 runs within max_s."""
     sys.path.insert(0, REPO)
     import numpy as np
     from oracle import mel as omel, model as omodel, synth, weights
     from a2m.real_motion_model import SelfAttention_G
-    threads = torch.get_num_threads()
-    model_name, phys, avail = host_cpu()
+    model_name, phys, avail, granted, quota = host_cpu()
+    threads = min(avail, granted) if granted else avail
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     shapes = {k: tuple(v.shape) for k, v in SelfAttention_G(p=0.0).state_dict().items()}
     sd = weights.make_state_dict(shapes, seed=7)
     wav = synth.speech_like(B, synth.samples_for_frames(T), seed=1)
@@ -243,17 +268,23 @@ def cpu_baseline(B=64, T=64, max_s=40.0):
         mel = np.stack([omel.log_mel(w, **omel.BUILD_CFG) for w in wav]).astype(np.float32)
         with torch.no_grad():
             omodel.generator(sd, torch.from_numpy(mel))
-    step()
-    times, t_all = [], time.perf_counter()
-    while len(times) < 5 and time.perf_counter() - t_all < max_s:
-        t0 = time.perf_counter()
-        step()
-        times.append(time.perf_counter() - t0)
+    try:
+        for _ in range(2):
+            step()
+        times, t_all = [], time.perf_counter()
+        while len(times) < 5 and time.perf_counter() - t_all < max_s:
+            t0 = time.perf_counter()
+            step()
+            times.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev_threads)
     med = sorted(times)[len(times) // 2]
     return {'value': round(B * T / med, 1), 'unit': 'pose-frames/s', 'cores': threads, 'kind': 'port',
             'cpu_model': model_name, 'host_physical_cores': phys, 'host_cpus_available': avail,
+            'cgroup_cpus': granted, 'cgroup_quota': quota,
             'sample': f'{B} clips x {T} frames, the bench workload (numpy fp64 log-mel + torch-CPU fp32 '
-                      f'G forward), median of {len(times)} runs, {threads} torch threads'}
+                      f'G forward), 2 warm-up runs, median of {len(times)} runs, {threads} torch threads '
+                      f'(affinity {avail} CPUs, cgroup quota {granted or "none"})'}
 
 
 # dense FLOPs of one training iteration at T=64 measured with torch's
@@ -308,13 +339,13 @@ def run_train(args, world, rank, dev):
         'metric': 'pose-frames/sec (whole node), PATS 64-frame clips batch 64, training iteration',
         'value': round(Bg * T / (ms * 1e-3), 1), 'unit': 'pose-frames/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
-        'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32' if args.dtype == 'fp32' else 'bf16',
+        'scaling': 'strong', 'vs_baseline': None, 'dtype': dtype_label(args.dtype),
         'data': 'synthetic mel/pose tensors, random-init weights',
         'config': {'workload': cfg + ': version5_model_train.py iteration (G x3 + D x1, Adam, '
                                'smoothed noisy labels), DP over ranks',
                    'batchnorm': 'sync' if tr.sync_bn else 'per-rank statistics',
-                   'grad_allreduce': (f'{len(tr.red_G.buckets)} G / {len(tr.red_D.buckets)} D buckets of '
-                                      f'<= {args.bucket_mb:g} MB, overlapped with backward, '
+                   'grad_allreduce': (f'{len(tr.red_G.buckets)} G / {len(tr.red_D.buckets)} D buckets '
+                                      f'(each closed once >= {args.bucket_mb:g} MB), overlapped with backward, '
                                       f'{"bf16" if args.dtype == "bf16" else "fp32"} on the wire'),
                    'global_batch': Bg, 'seq_len': T, 'parallelism': f'dp{world}'},
         'path_roofline': {'bound': 'mfma', 'achieved': round(tf, 2), 'peak': peak,
@@ -328,6 +359,12 @@ def run_train(args, world, rank, dev):
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dtype_label(dtype):
+    """Arithmetic type of the GEMMs: f32; bf16 (bf16 operands, f32 accumulation); bf16x6 (f32
+    operands split exactly into three bf16 planes, six bf16 products: f32-class results)."""
+    return {'fp32': 'f32', 'bf16': 'bf16', 'bf16x6': 'bf16x6'}[dtype]
 
 
 def mfma_peak(dtype):
@@ -485,7 +522,7 @@ def main():
         'metric': 'pose-frames/sec (whole node), PATS 64-frame clips batch 64, 1/2/4/8 MI355X',
         'value': round(value, 1), 'unit': 'pose-frames/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32' if args.dtype == 'fp32' else 'bf16',
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': dtype_label(args.dtype),
         'data': 'synthetic 16 kHz speech-like audio, random-init weights',
         'config': {'workload': workload, 'global_batch': B * world, 'seq_len': T,
                    'parallelism': f'replicas{world}', 'hip_graph': 'none' if graph is None else ('per-branch graphs, two streams' if args.branch_graphs else 'one graph')},

@@ -223,7 +223,11 @@ int a2m_graph_att_proj_f32(const float* w0, const float* att_src, const float* a
  * (kinds[l] = 0: w0 = lin.weight [256][64], U from a2m_graph_att_proj_f32, bias) or GraphConv
  * (kinds[l] = 1: w0 = lin_rel.weight, w1 = lin_root.weight, bias = lin_rel.bias).  The
  * per-layer arrays are host arrays of device pointers.  One launch; each workgroup keeps its
- * frames' node tile in LDS across the layers.  x, y: [F*J][64], distinct. */
+ * frames' node tile in LDS across the layers.  x, y: [F*J][64], distinct.
+ * Topology limits (nbr_ptr / nbr_idx are device arrays, so they are NOT checked here; the
+ * Python host side validates them where the CSR is built, a2m/skeleton.py in_neighbour_csr):
+ * J <= 128, in-degree <= 7 per node, and (J + 1) + nbr_ptr[J] <= 256.  A topology beyond
+ * them gives wrong results. */
 int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
                             const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
                             const float* const* w0, const float* const* w1, const float* const* U,
@@ -238,7 +242,8 @@ int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t*
  *   kind 1: GraphConv(64,64): W_rel (sum_nbr x) + b_rel + W_root x
  * The topology is given as an in-neighbour CSR over one graph (nbr_ptr[J+1], nbr_idx,
  * source nodes of the edges into each target, in edge order) and is shared by all F
- * frames.  norm_res = 0 gives the bare layer y = L(x) (the discriminator's per-sample
+ * frames (limits as for a2m_graph_stack_fwd_f32: J <= 128, in-degree <= 7,
+ * (J + 1) + nbr_ptr[J] <= 256; not checked on the device arrays).  norm_res = 0 gives the bare layer y = L(x) (the discriminator's per-sample
  * GATConv, real_motion_model.py:602-616).  lin_out (GAT: x' [F*J][256]; GraphConv: aggregated x [F*J][64]) and
  * pre_ln [F*J][64] are saved for the backward pass when not NULL. */
 int a2m_graph_layer_fwd_f32(const float* x, int32_t F, int32_t J, int32_t kind,

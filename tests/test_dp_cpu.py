@@ -228,3 +228,93 @@ def test_syncbn_plumbing_two_ranks():
         assert sync_bn and seen and all(w == 2 for w in seen)   # every BN in the step sees 2 ranks
         assert after == 0                                       # per-rank statistics restored
         assert t == [[1.5 + 2.5, 2.0]]                          # SUM over the ranks, float64
+
+
+def _mismatch_worker(rank, world, port, q):
+    """Rank 1 sends a gradient through a parameter outside the learnt set on the second step:
+    both ranks must raise together (no rank left waiting in a bucket all-reduce)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from a2m.training import GANTrainer
+        _patch_ops()
+
+        class BranchG(TinyG):
+            use_extra = False
+
+            def __init__(self):
+                super().__init__()
+                self.extra = torch.nn.Linear(48, 48)
+
+            def forward(self, audio, real_pose=None):
+                if self.use_extra:
+                    audio = audio.clone()
+                    pose, internal = super().forward(audio, real_pose)
+                    return pose + self.extra.weight.sum() * 0, internal
+                return super().forward(audio, real_pose)
+
+        torch.manual_seed(11)
+        g = BranchG()
+        tr = GANTrainer(g, TinyD(), lr=1e-2, fixed_labels=(0.93, 0.07), bucket_mb=0.009)
+        audio, pose = _data()
+        tr.iteration(audio[rank::world], pose[rank::world], epoch=0, g_freq=1, d_freq=1)
+        g.use_extra = rank == 1
+        try:
+            tr.iteration(audio[rank::world], pose[rank::world], epoch=1, g_freq=1, d_freq=1)
+            q.put((rank, 'no error'))
+        except RuntimeError as e:
+            q.put((rank, 'raised: ' + str(e)[:60]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_grad_reducer_mismatch_raises_on_every_rank():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mismatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    assert all(v.startswith('raised: GradReducer') for v in res.values()), res
+
+
+def _seed_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from a2m.training import GANTrainer
+        _patch_ops()
+        torch.manual_seed(100 + rank)       # ranks differ; rank 0's seed must win
+        tr = GANTrainer(TinyG(), TinyD(), lr=1e-2)
+        real, fake = tr._labels(0, 4, torch.device('cpu'))
+        q.put((rank, (real.numpy(), fake.numpy())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_label_seed_follows_rank0_manual_seed():
+    """label_seed=None: the labels follow torch.manual_seed (the reference draws them from the
+    global RNG), and every rank slices the same global-batch draw (rank 0's seed)."""
+    from a2m.training import DynamicGANTraining
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    gen = torch.Generator().manual_seed(100)
+    dyn = DynamicGANTraining(g_lr=5e-3, d_lr=1e-2)
+    real = dyn.get_smooth_labels(0, 8, 'cpu', True, generator=gen).numpy()
+    fake = dyn.get_smooth_labels(0, 8, 'cpu', False, generator=gen).numpy()
+    for r in (0, 1):
+        assert (res[r][0] == real[4 * r:4 * r + 4]).all() and (res[r][1] == fake[4 * r:4 * r + 4]).all()
