@@ -4,8 +4,9 @@ version5_model_train.py:285-286), one fused HIP kernel per step.
 On construction the module's parameters are re-seated as views of one contiguous buffer.
 zero_grad() leaves .grad unset, so autograd's AccumulateGrad keeps each fresh gradient tensor
 as it is (no per-parameter add kernel), and collect_grads() gathers them into one contiguous
-gradient buffer with a few segment-gather launches; the data-parallel all-reduce is then a
-single collective over `flat_grad`, and the update is one launch over `flat`.  `param_groups[0]['lr']` may be changed between steps
+gradient buffer with a few segment-gather launches; the data-parallel all-reduce then runs
+over contiguous buckets of `flat_grad` (training.GradReducer), and the update is one launch
+over `flat`.  `param_groups[0]['lr']` may be changed between steps
 (DynamicGANTraining.adjust_learning_rates does).
 
 Every parameter starts on a 64-byte boundary of the buffer (ALIGN floats): the GEMM engine
