@@ -194,6 +194,7 @@ class ConvTranspose1D(nn.Module):
 
 
 _ENC_NHWC = __import__('os').environ.get('A2M_ENC_NHWC', '1') != '0'
+_ENC_NHWC_ALL = __import__('os').environ.get('A2M_ENC_NHWC_ALL', '1') != '0'
 
 
 class AudioEncoder(nn.Module):
@@ -253,11 +254,18 @@ class AudioEncoder(nn.Module):
         return F.interp_time(h, time_steps)
 
     def _nhwc_layer(self, i):
-        """Channels-last where the NCHW path would gather its operand element by element
-        (K < 2048: conv0, conv1; tools/enc_layers.py: conv1 115 -> 89 us); the deeper layers
-        keep im2col + dense GEMM, which measured faster than the mode-4 runs there."""
+        """Channels-last for every layer the GEMM engine can read as contiguous channel runs:
+        conv0 (Ci = 1, its direct kernel) and every layer with Ci a multiple of the k-tile
+        (loader mode 6: each k-tile is one tap's channel slice), so no layer needs an im2col
+        matrix (A2M_ENC_NHWC_ALL=0 restores the round-2 split: channels-last only below K =
+        2048, im2col + dense GEMM above)."""
         w = self.conv[i].conv.weight
-        return w.shape[1] * w.shape[2] * w.shape[3] < 2048 and (w.shape[1] * w.shape[3]) % 4 == 0
+        Ci, kw = w.shape[1], w.shape[3]
+        if (Ci * kw) % 4 != 0:
+            return False
+        if _ENC_NHWC_ALL and (Ci == 1 or Ci % 64 == 0):
+            return True
+        return Ci * w.shape[2] * kw < 2048
 
 
 class UNet1D(nn.Module):

@@ -60,6 +60,11 @@ struct Gather {
   int ar1, ar2, bk1, bk2, ch, cw;
   int divh, divw, Lh, Lw;
   int kcontig;  // 1: consecutive k are (usually) adjacent in memory -> k-major thread map
+  int nhwc;     // > 0: channels-last conv rows (loader mode 6), the channel count Ci (a multiple
+                // of the k-tile): rows n = (r0 = image, r1 = output row, r2 = live output
+                // column), k = (i, j, c) with K2 = kw taps per kernel row; pixel (r1*ar1 + ch + i,
+                // r2*ar2 + cw + j) of an Lh x Lw image, sr0 = the image stride; every k-tile is
+                // one tap's channel slice, a contiguous run
   int tapconv;  // > 0: stride-1 conv1d operand in tap-chunked k order (loader mode 5): k =
                 // (chunk, tap, ci) with BK-channel chunks, rows n = b*R2 + t; the chunk's
                 // x[b][c][t] window is loaded once and re-stored shifted for each of the

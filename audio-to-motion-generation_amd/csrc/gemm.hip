@@ -125,6 +125,7 @@ static int env_int(const char* name, int dflt) {
 
 static int operand_mode(const Gather& g, int K) {
   if (g.tapconv > 0) return 5;
+  if (g.nhwc > 0) return 6;
   if (!g.kcontig) {
     // rows 4-at-a-time contiguous: plain [K][R] (rows via r0, unit stride), or stride-1 im2col
     // rows along w (R2 % 4 == 0) or along h (R2 == 1, R1 % 4 == 0), unit element stride
@@ -147,15 +148,8 @@ static int operand_mode(const Gather& g, int K) {
 }
 
 struct Plan {
-  int bm, bn, bk, splits, kchunk;
+  int bm, bk, splits, kchunk;
 };
-
-// Tile codes of the planner / overrides: 64 = 64x64, 128 = 128x128, 12864 = 128 (M) x 64 (N),
-// 64128 = 64 x 128.
-static void tile_dims(int code, int& bm, int& bn) {
-  bm = code == 128 || code == 12864 ? 128 : 64;
-  bn = code == 128 || code == 64128 ? 128 : 64;
-}
 
 // Tile / split-K choice by a cost model fitted to measured sweeps of the engine on MI355X
 // (tools/gemm_tune.py; DESIGN.md "GEMM planner").  For each candidate (tile, splits):
@@ -189,25 +183,8 @@ static int gemm_xcd_group() {
 
 static int g_override_tile = 0, g_override_split = 0;   // a2m_gemm_plan_override (tuning)
 
-static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int code, int kchunk,
+static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int tile, int kchunk,
                            int splits, int prec) {
-  int bm, bn;
-  tile_dims(code, bm, bn);
-  if (bm != bn) {
-    // non-square fp32 tiles (128x64 / 64x128): LDS 55 KB -> 2 resident blocks per CU; per-CU
-    // throughput between the 64x64 and 128x128 tiles (provisional: tools/tile_probe.py)
-    static const double thrn[2] = {400e3, 470e3};
-    const int64_t tiles = cdiv(M, bm) * cdiv(N, bn) * (int64_t)batch;
-    const int64_t per_cu = cdiv(tiles * splits, 256);
-    const int c = (int)std::min<int64_t>(per_cu, 2);
-    double thr = thrn[c - 1];
-    if (gathered) thr *= 0.92;
-    const double block_flops = 2.0 * bm * bn * (double)kchunk;
-    double t = per_cu * block_flops / thr + cdiv(per_cu, 2) * 6.0 + 4.0;
-    if (splits > 1) t += (splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0;
-    return t;
-  }
-  const int tile = bm;
   static const double thr64[4] = {340e3, 428e3, 435e3, 440e3};   // flop / us per CU
   static const double thr128[2] = {464e3, 500e3};
   // bf16x6 (fitted to a plan sweep of the G forward's shapes, tools/sweep_summary.py): three
@@ -241,14 +218,10 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, in
   const int BK = gemm_bk(prec);
   const int KQ = BK * kquant;   // split boundaries on whole k-tile groups (mode 5: all taps of a chunk)
   static const int cand_splits[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256};
-  Plan p{64, 64, BK, 1, (int)(cdiv(std::max(K, 1), KQ) * KQ)};
+  Plan p{64, BK, 1, (int)(cdiv(std::max(K, 1), KQ) * KQ)};
   double best = 1e300;
-  // the non-square tiles join the search under A2M_GEMM_NSQ=1 (fp32 only) or when forced
-  static const int nsq = env_int("A2M_GEMM_NSQ", 0);
-  for (int tile : {64, 128, 12864, 64128}) {
+  for (int tile : {64, 128}) {
     if (force_tile && tile != force_tile) continue;
-    if (!force_tile && tile > 128 && (!nsq || prec != 0)) continue;
-    if (tile > 128 && prec != 0) continue;
     for (int s : cand_splits) {
       if (force_split && s != force_split) continue;
       const int kchunk = (int)(cdiv(cdiv(std::max(K, 1), s), KQ) * KQ);
@@ -258,14 +231,14 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, in
       const double t = plan_cost_us(M, N, K, batch, gathered, tile, kchunk, se, prec);
       if (t < best) {
         best = t;
-        tile_dims(tile, p.bm, p.bn);
+        p.bm = tile;
         p.kchunk = kchunk;
         p.splits = se;
       }
     }
   }
   if (force_split && best == 1e300) {   // a forced split outside the candidate list
-    tile_dims(force_tile ? force_tile : 64, p.bm, p.bn);
+    p.bm = force_tile ? force_tile : 64;
     p.kchunk = (int)(cdiv(cdiv(std::max(K, 1), force_split), KQ) * KQ);
     p.splits = (int)cdiv(std::max(K, 1), p.kchunk);
   }
@@ -332,7 +305,9 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   const int ma = operand_mode(A, K), mb = operand_mode(B, K);
   const int prec = g_gemm_prec;
   const int kquant = mb == 5 ? B.tapconv : 1;
-  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || mb >= 3, prec, kquant);
+  // gathered: row-vector staging (modes 2 / 3) or gathers; k-contiguous conv rows (mode 6) load
+  // like dense rows
+  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || (mb >= 3 && mb != 6), prec, kquant);
   if (force_split > 0) {
     p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk * kquant) * p.bk * kquant);
     p.splits = (int)cdiv(K, p.kchunk);
@@ -348,7 +323,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   static const int ks3_maxb = env_int("A2M_GEMM_KS3_MAXB", 256);
   const int64_t blocks64 = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
   const int nt_all = (int)cdiv(K, p.bk);
-  bool use_ks3 = prec == 0 && ks3 && p.bm == 64 && p.bn == 64 && ma == 0 && blocks64 <= ks3_maxb &&
+  bool use_ks3 = prec == 0 && ks3 && p.bm == 64 && ma == 0 && blocks64 <= ks3_maxb &&
                  nt_all % (2 * kquant) == 0 && nt_all >= 8 &&
                  ((p.splits == 1 && (mb == 5 || mb == 3)) ||
                   (ks3 >= 2 && p.splits == 2 && force_split <= 0 && g_override_split == 0 &&
@@ -370,13 +345,13 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   }
   static const int log_launches = env_int("A2M_GEMM_LOG", 0);
   if (log_launches)
-    std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%dx%d bk=%d splits=%d modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
-                 M, N, K, batch, p.bm, p.bn, p.bk, p.splits, ma, mb, E.som, E.so0, E.so1, E.so2, E.N1, E.N2);
+    std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
+                 M, N, K, batch, p.bm, p.bk, p.splits, ma, mb, E.som, E.so0, E.so1, E.so2, E.N1, E.N2);
   long tm = -1;
   if (g_timing) {
     char desc[96];
-    std::snprintf(desc, sizeof(desc), "M=%d N=%d K=%d b=%d tile=%dx%d split=%d modes=%d,%d", M, N, K,
-                  batch, p.bm, p.bn, p.splits, ma, mb);
+    std::snprintf(desc, sizeof(desc), "M=%d N=%d K=%d b=%d tile=%d split=%d modes=%d,%d", M, N, K,
+                  batch, p.bm, p.splits, ma, mb);
     tm = timing_open(2.0 * M * N * (double)K * batch, desc, stream);
   }
   if (prec == 1) {
@@ -387,21 +362,11 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
   } else {
     static const int ks2 = env_int("A2M_GEMM_KS2", 1);
-    // A2M_GEMM_KS2_MODES: bit 0 dense B (default on), bit 1 k-run B (mode 4), bit 2 row-vector
-    // B (mode 3) -- which B operands the two-wave-group tiles take
-    static const int ks2_modes = env_int("A2M_GEMM_KS2_MODES", 1);
-    const bool ks2_ok = ks2 && ma == 0 &&
-                        ((mb == 0 && (ks2_modes & 1)) || (mb == 4 && (ks2_modes & 2)) ||
-                         (mb == 3 && (ks2_modes & 4)));
-    if (p.bm == 128 && p.bn == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
-    else if (p.bm == 128) {
-      if (ks2_ok) launch_tile<128, 64, 32, 0, 2>(a, ma, mb, batch, stream);
-      else launch_tile<128, 64, 32, 0>(a, ma, mb, batch, stream);
-    } else if (p.bn == 128) launch_tile<64, 128, 32, 0>(a, ma, mb, batch, stream);
+    if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
     else if (use_ks3) launch_tile<64, 64, 32, 0, 3>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
-    // convs after im2col)
-    else if (ks2_ok) launch_tile<64, 64, 32, 0, 2>(a, ma, mb, batch, stream);
+    // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end
+    else if (ks2 && ma == 0 && (mb == 0 || mb == 6)) launch_tile<64, 64, 32, 0, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, 0>(a, ma, mb, batch, stream);
   }
   A2M_LAUNCH_CHECK();
@@ -428,8 +393,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
 extern "C" {
 
 int a2m_gemm_plan_override(int32_t tile, int32_t splits) {
-  A2M_CHECK_ARG((tile == 0 || tile == 64 || tile == 128 || tile == 12864 || tile == 64128) &&
-                    splits >= 0 && splits <= 256,
+  A2M_CHECK_ARG((tile == 0 || tile == 64 || tile == 128) && splits >= 0 && splits <= 256,
                 "gemm_plan_override: tile %d splits %d", tile, splits);
   a2m::g_override_tile = tile;
   a2m::g_override_split = splits;

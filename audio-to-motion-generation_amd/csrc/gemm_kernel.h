@@ -135,6 +135,10 @@ typedef float float4u __attribute__((ext_vector_type(4), aligned(4)));
 //           float4 along t once (tap 0) and stored transposed, shifted by tap - pad within each
 //           clip, for every tap -- the im2col operand without its 3x global traffic.  Tiles
 //           hold whole clips (BR % T == 0) so the shift wraps inside the tile (wrapped rows = 0).
+//   MODE 6: channels-last conv rows (Gather::nhwc): a k-tile is BK channels of one tap, so every
+//           row's slice is a contiguous run loaded as float4 along k like a dense row; the tap
+//           (i, j) and channel offset are uniform per tile, each row only adds its pixel offset
+//           and checks the pixel against the image (padding reads 0).
 #ifndef A2M_M3_TRANSPOSE
 #define A2M_M3_TRANSPOSE 1
 #endif
@@ -184,9 +188,6 @@ struct TileLoader {
   int tt;        // t of this thread's first row within its clip
   int64_t rb;    // element offset of (b, t) of that row
   int st_j;      // k-tile index of the next store (its tap)
-  int jstep;     // k-tiles between this loader's consecutive tiles (its stride / BK)
-  int held_cc;   // mode 5: the channel chunk whose window the registers hold
-  unsigned vmask;  // mode 0: which of the thread's rows / k quads of the last load are real
   KPos kp[NKP];   // k position of each of this thread's k groups at the next load (modes 1-3)
   KPos kstep;     // BK in (k0, k1, k2) digits
   float r[NREG];
@@ -208,8 +209,6 @@ struct TileLoader {
       tt = n - b * gg.R2;
       rb = nrow > 0 ? (int64_t)b * gg.sr0 + tt : 0;
       st_j = kbeg / BK;
-      jstep = kstride / BK;
-      held_cc = -1;
       return;
     }
     if (MODE == 3) {
@@ -233,10 +232,13 @@ struct TileLoader {
       for (int p = 0; p < NPASS; ++p) {
         lrow[p] = tid / QPR + p * RPP;
         ri[p] = row_info(gg, row0 + lrow[p], R);
+        // mode 6: row_info gives base = image offset, h / w = the row's input pixel origin
+        // (r1*ar1 + ch, r2*ar2 + cw); fold the origin into the base once
+        if (MODE == 6) ri[p].base += (ri[p].h * gg.Lw + ri[p].w) * gg.nhwc;
       }
       kq = (tid % QPR) * 4;
     }
-    if (MODE != 0) {
+    if (MODE != 0 && MODE != 6) {
       kstep = kpos(gg, kstride);
 #pragma unroll
       for (int p = 0; p < NKP; ++p) kp[p] = kpos(gg, kbeg + kq + (MODE == 3 ? eofs(p) : 0));
@@ -246,11 +248,7 @@ struct TileLoader {
   __device__ __forceinline__ void load(int k0) {
     if (MODE == 5) {
       const int j = k0 / BK, cc = j / g->tapconv;
-      // a chunk's window is loaded once per loader: its other taps re-store the registers
-      // (with the even / odd tile loaders of the k loop each loader loads the chunks it has
-      // tiles of)
-      if (cc == held_cc) return;
-      held_cc = cc;
+      if (j - cc * g->tapconv != 0) return;   // taps 1.. re-store the registers of tap 0
 #pragma unroll
       for (int p = 0; p < NKE; ++p) {
         const float* src = base + rb + (int64_t)(cc * BK + kq + eofs(p)) * g->sk0;
@@ -265,17 +263,24 @@ struct TileLoader {
       return;
     }
     if (MODE == 0) {
-      // unconditional loads (an out-of-range row / k quad reads element 0 instead) and the
-      // zeroing deferred to store(): a load inside a branch makes the compiler drain every
-      // outstanding load (vmcnt(0)) where the branches join, which would serialise the
-      // two-tile-deep pipeline of the k loop
-      vmask = 0;
 #pragma unroll
       for (int p = 0; p < NPASS; ++p) {
-        const int k = k0 + kq;
-        const bool ok = ri[p].valid && k < K;
-        vmask |= (unsigned)ok << p;
-        const float4 v = *reinterpret_cast<const float4*>(base + (ok ? ri[p].base + k : 0));
+        int k = k0 + kq;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ri[p].valid && k < K) v = *reinterpret_cast<const float4*>(base + ri[p].base + k);
+        r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
+      }
+    } else if (MODE == 6) {
+      const int Ci = g->nhwc;
+      const int tap = k0 / Ci, ci0 = k0 - tap * Ci;   // uniform: scalar arithmetic
+      const int i = tap / g->K2, j = tap - i * g->K2;
+      const int toff = (i * g->Lw + j) * Ci + ci0 + kq;
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p) {
+        const int h = ri[p].h + i, w = ri[p].w + j;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ri[p].valid && k0 < K && (unsigned)h < (unsigned)g->Lh && (unsigned)w < (unsigned)g->Lw)
+          v = *reinterpret_cast<const float4*>(base + ri[p].base + toff);
         r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
       }
     } else if (MODE == 4) {
@@ -371,32 +376,6 @@ struct TileLoader {
     }
   }
 
-  // Staging in parts (interleaved with MFMAs by the k loop): dense rows (mode 0) one pass per
-  // part, the other modes as one part.
-  static constexpr int NPARTS = MODE == 0 && P == 0 ? NPASS : 1;
-  __device__ __forceinline__ void load_part(int k0, int part) {
-    if constexpr (MODE == 0 && P == 0) {
-      const int p = part;
-      const int k = k0 + kq;
-      const bool ok = ri[p].valid && k < K;
-      vmask = (vmask & ~(1u << p)) | ((unsigned)ok << p);
-      const float4 v = *reinterpret_cast<const float4*>(base + (ok ? ri[p].base + k : 0));
-      r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
-    } else {
-      load(k0);
-    }
-  }
-  __device__ __forceinline__ void store_part(float* lds, int part) {
-    if constexpr (MODE == 0 && P == 0) {
-      const int p = part;
-      float4 v = make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
-      if (!((vmask >> p) & 1)) v = make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(lds + lrow[p] * LDK + kq) = v;
-    } else {
-      store(lds);
-    }
-  }
-
   // mode 5: the row (within the tile) that element e of this thread's 4-row group lands on for
   // the shift s = tap - pad, and whether it carries data (rows whose source t + s leaves the
   // clip take 0, written by the element that wraps onto them)
@@ -412,7 +391,7 @@ struct TileLoader {
   __device__ __forceinline__ void store(float* lds) {
     if constexpr (MODE == 5) {
       const int tap = st_j % g->tapconv;
-      st_j += jstep;
+      ++st_j;
       const int s = tap + g->cw;   // cw = -pad
       if constexpr (H) {
 #pragma unroll
@@ -449,7 +428,6 @@ struct TileLoader {
           for (int c = 0; c < 3; ++c) *reinterpret_cast<uint2*>(hl + c * PLANE + o) = q[c];
         }
       } else {
-        zero_masked();
 #pragma unroll
         for (int p = 0; p < NPASS; ++p) {
           uint2 q[3];
@@ -469,7 +447,6 @@ struct TileLoader {
 #pragma unroll
         for (int j = 0; j < KPT; j += 4) *reinterpret_cast<uint2*>(dst + j) = pack4(&r[j]);
       } else {
-        zero_masked();
 #pragma unroll
         for (int p = 0; p < NPASS; ++p)
           *reinterpret_cast<uint2*>(hl + lrow[p] * LDK + kq) = pack4(&r[p * 4]);
@@ -493,19 +470,9 @@ struct TileLoader {
         *reinterpret_cast<float4*>(dst + j) = make_float4(r[j], r[j + 1], r[j + 2], r[j + 3]);
     } else {
 #pragma unroll
-      for (int p = 0; p < NPASS; ++p) {
-        float4 v = make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
-        if (MODE == 0 && !((vmask >> p) & 1)) v = make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(lds + lrow[p] * LDK + kq) = v;
-      }
-    }
-  }
-
-  __device__ __forceinline__ void zero_masked() {   // mode 0: the deferred zeroing of load()
-    if constexpr (MODE == 0) {
-#pragma unroll
       for (int p = 0; p < NPASS; ++p)
-        if (!((vmask >> p) & 1)) r[p * 4] = r[p * 4 + 1] = r[p * 4 + 2] = r[p * 4 + 3] = 0.f;
+        *reinterpret_cast<float4*>(lds + lrow[p] * LDK + kq) =
+            make_float4(r[p * 4], r[p * 4 + 1], r[p * 4 + 2], r[p * 4 + 3]);
     }
   }
 
@@ -720,32 +687,6 @@ __device__ __forceinline__ void mfma_part(const Frags<TM, TN, 1, 1>& f, floatx16
         acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][c], f.b[u][c], acc[t][u], 0, 0, 0);
 }
 
-// sub-step s of a half (fp32: k pair s; bf16: K16 chunk s; bf16x6: product term s)
-template <int TM, int TN, int NS>
-__device__ __forceinline__ void mfma_part_one(const Frags<TM, TN, 0, NS>& f, floatx16 (&acc)[TM][TN], int s) {
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-      acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[t][s], f.b[u][s], acc[t][u], 0, 0, 0);
-}
-template <int TM, int TN>
-__device__ __forceinline__ void mfma_part_one(const Frags<TM, TN, 1, 1>& f, floatx16 (&acc)[TM][TN], int c) {
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-      acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][c], f.b[u][c], acc[t][u], 0, 0, 0);
-}
-template <int TM, int TN>
-__device__ __forceinline__ void mfma_part_one(const Frags<TM, TN, 2, 1>& f, floatx16 (&acc)[TM][TN], int j) {
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-      acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][x6_ia(j)], f.b[u][x6_ib(j)], acc[t][u], 0, 0, 0);
-}
-
 template <int TM, int TN, int NS>
 __device__ __forceinline__ void mfma_half(const Frags<TM, TN, 0, NS>& f, floatx16 (&acc)[TM][TN]) {
 #pragma unroll
@@ -766,41 +707,6 @@ __device__ __forceinline__ void mfma_half(const Frags<TM, TN, 1, 1>& f, floatx16
 #pragma unroll
       for (int u = 0; u < TN; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[t][c], f.b[u][c], acc[t][u], 0, 0, 0);
-}
-
-// The MFMAs of a k-tile's first half with the staging of the next tile interleaved: after
-// MFMA sub-step s the wave issues staging part s -- the tile stores of the next tile, pass by
-// pass (A then B), then the global loads of the tile after it, pass by pass -- each pinned in
-// place by sched_barriers, so every SIMD's matrix pipe has queued work while its wave waits
-// on a load's data or issues LDS stores.  Gathered operands (modes 1-5) stage as one part.
-template <class LA, class LB, int TM, int TN, int P, int NS>
-__device__ __forceinline__ void mfma_half_staged(const Frags<TM, TN, P, NS>& f, floatx16 (&acc)[TM][TN],
-                                                 LA& la, LB& lb, float* nxt, bool store, bool load,
-                                                 int kload) {
-  constexpr int NSUB = P == 0 ? 8 * NS : (P == 1 ? 2 : 6);
-  constexpr int PS = LA::NPARTS + LB::NPARTS;   // store parts, then as many load parts
-  constexpr int PER = (2 * PS + NSUB - 1) / NSUB;   // staging parts behind each sub-step
-#pragma unroll
-  for (int s = 0; s < NSUB; ++s) {
-    if (A2M_ABLATE != 1) mfma_part_one(f, acc, s);
-    else if (s == 0) ablate_touch(f, acc);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = s * PER; j < (s + 1) * PER && j < 2 * PS; ++j) {
-      if (j < LA::NPARTS) {
-        if (store) la.store_part(nxt, j);
-      } else if (j < PS) {
-        if (store) lb.store_part(nxt + LA::TILE, j - LA::NPARTS);
-      } else if (j < PS + LA::NPARTS) {
-        // dense loads go out unconditionally (clamped addresses past the end): a load under a
-        // branch makes the compiler drain every outstanding load where the branches join
-        if (LA::NPARTS > 1 || load) la.load_part(kload, j - PS);
-      } else {
-        if (LB::NPARTS > 1 || load) lb.load_part(kload, j - PS - LA::NPARTS);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
 }
 
 // A2M_ABLATE = 1: keep the fragments live with one VALU op instead of the MFMAs
@@ -877,14 +783,10 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
     else kbeg = mid;
   }
 
-  // KS = 2: group g stages k-tiles g, g + 2, ... so its loaders start one tile in and step two
-  // (the running k positions of the gathered modes advance by the loader's own stride)
   LA la;
   LB lb;
-  const int kfirst = KS == 2 ? kbeg + grp * BK : kbeg;
-  constexpr int kstr = KS == 2 ? 2 * BK : BK;
-  la.init(args.A, batch, m0, args.M, args.K, tid, kfirst, kstr);
-  lb.init(args.B, batch, n0, args.N, args.K, tid, kfirst, kstr);
+  la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
+  lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
 
   floatx16 acc[TM][TN];
 #pragma unroll
@@ -912,16 +814,21 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
     for (int i = 0; i < nk; ++i) {
       const float* cur = lds + (i & 1) * STAGE;
       float* nxt = lds + ((i + 1) & 1) * STAGE;
-      const bool more = i + 1 < nk, more2 = A2M_ABLATE != 2 && i + 2 < nk;
-      // First half: the staging of tile i + 1 (registers -> LDS[(i + 1) & 1]) and the global
-      // loads of tile i + 2 are interleaved, part by part, with the MFMAs of half 0 (fragments
-      // read last step), so the matrix pipe keeps running while a wave stages; then the half-1
-      // fragments of tile i.  LDS[(i + 1) & 1] is free at the start of step i: its last reads
-      // (tile i - 1, half 1) preceded step i - 1's barrier.
-      mfma_half_staged<LA, LB>(f0, acc, la, lb, nxt, more, more2, kbeg + (i + 2) * BK);
-      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < nk) {
+        la.store(nxt);
+        lb.store(nxt + LA::TILE);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the tile stores stay ahead of the fragment reads
+      if (A2M_ABLATE != 2 && i + 2 < nk) {
+        la.load(kbeg + (i + 2) * BK);
+        lb.load(kbeg + (i + 2) * BK);
+      }
       read_frags<BM, BN, TM, TN, P, NS, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
-      // The step's barrier.  Only this wave's tile stores must have landed: LDS ops retire in
+      if (A2M_ABLATE != 1) mfma_half(f0, acc);
+      else ablate_touch(f0, acc);
+      // The step's barrier, pinned after the first half's MFMAs (left to itself the compiler
+      // hoists it above them, and __syncthreads' fence would also wait for the second half's
+      // fragment reads).  Only this wave's tile stores must have landed: LDS ops retire in
       // order, so the 2 (TM + TN) fragment reads issued after them may stay in flight (the
       // second half's MFMAs wait for them where they are used).  s_waitcnt simm16 on gfx950:
       // vmcnt / expcnt at their maxima (no wait), lgkmcnt in bits 11:8.
@@ -937,7 +844,7 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
       constexpr int NSUB = P == 0 ? 8 * NS : (P == 1 ? 2 : 6);
       if (A2M_ABLATE != 1) mfma_part<0, SPLIT>(f1, acc);
       __builtin_amdgcn_sched_barrier(0);
-      if (more) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
+      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
       __builtin_amdgcn_sched_barrier(0);
       if (A2M_ABLATE != 1) mfma_part<SPLIT, NSUB>(f1, acc);
       else ablate_touch(f1, acc);
@@ -1099,12 +1006,8 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
   if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3(KS == 1 ? 256 : 512), 0, st, a); return; }
-  if constexpr (KS == 2) {  // dense weights x dense / row-vector / k-run operands (gemm.hip)
-    A2M_L(0, 0) A2M_L(0, 3) A2M_L(0, 4)
-    return;
-  }
-  if constexpr (BM != BN) {  // the non-square tiles: dense weights x the activation loaders
-    A2M_L(0, 0) A2M_L(0, 3) A2M_L(0, 4) A2M_L(0, 5)
+  if constexpr (KS == 2) {  // dense (or channels-last conv, mode 6) operands only (gemm.hip)
+    A2M_L(0, 0) A2M_L(0, 6)
     return;
   }
   if constexpr (KS == 3) {  // dense / gathered weights x tap-chunked conv1d operands (gemm.hip)
@@ -1116,7 +1019,7 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3) A2M_L(2, 4)
   A2M_L(3, 0) A2M_L(3, 1) A2M_L(3, 2) A2M_L(3, 3) A2M_L(3, 4)
   A2M_L(4, 0) A2M_L(4, 1) A2M_L(4, 2) A2M_L(4, 3) A2M_L(4, 4)
-  A2M_L(0, 5)
+  A2M_L(0, 5) A2M_L(0, 6)
 #undef A2M_L
 }
 
@@ -1124,9 +1027,6 @@ extern template void launch_tile<64, 64, 32, 0>(const GemmArgs&, int, int, int, 
 extern template void launch_tile<64, 64, 32, 0, 2>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 32, 0, 3>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<128, 64, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<64, 128, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<128, 64, 32, 0, 2>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 32, 2>(const GemmArgs&, int, int, int, hipStream_t);

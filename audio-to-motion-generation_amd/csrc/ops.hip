@@ -832,7 +832,28 @@ __global__ __launch_bounds__(256) void conv2d_c1_kernel(
   // input rows ho0*s - ph + i and the columns the live outputs read, zero outside the image
   const int c0 = w_lo * stride - pw, nc = (w_hi - 1 - w_lo) * stride + kw;
   const int nin = (nr - 1) * stride + kh;
-  for (int idx = tid; idx < nin * nc; idx += blockDim.x) {
+  // the input patch: the first C1_PRE elements per thread are loaded all at once (clamped
+  // addresses, zeroed after the loads), so their latencies overlap instead of one dependent
+  // round trip per element; wider patches finish in the plain loop
+  constexpr int C1_PRE = 8;
+  {
+    float pv[C1_PRE];
+    bool ok[C1_PRE];
+#pragma unroll
+    for (int u = 0; u < C1_PRE; ++u) {
+      const int idx = tid + u * 256;
+      const int i = idx / nc, c = idx - (idx / nc) * nc;
+      const int hi = ho0 * stride - ph + i, wi = c0 + c;
+      ok[u] = idx < nin * nc && hi >= 0 && hi < H && wi >= 0 && wi < W;
+      pv[u] = x[ok[u] ? ((int64_t)b * H + hi) * W + wi : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < C1_PRE; ++u) {
+      const int idx = tid + u * 256;
+      if (idx < nin * nc) rows[idx / nc][idx % nc] = ok[u] ? pv[u] : 0.f;
+    }
+  }
+  for (int idx = tid + C1_PRE * 256; idx < nin * nc; idx += blockDim.x) {
     const int i = idx / nc, c = idx % nc;
     const int hi = ho0 * stride - ph + i, wi = c0 + c;
     rows[i][c] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? x[((int64_t)b * H + hi) * W + wi] : 0.f;
@@ -928,7 +949,23 @@ int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, in
     return A2M_OK;
   }
   const int Wn = w_hi - w_lo;
+  Epilogue E;
+  if (y_nhwc) {
+    E = epi_bn(y + (int64_t)w_lo * Co, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+    E.N1 = Hout; E.N2 = Wn; E.so0 = Hout * Wout * Co; E.so1 = Wout * Co; E.so2 = Co; E.som = 1;
+  } else {
+    E = epi_bn(y + w_lo, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+    E.N1 = Hout; E.N2 = Wn; E.so0 = Co * Hout * Wout; E.so1 = Wout; E.so2 = 1; E.som = Hout * Wout;
+  }
   Gather A = dense_rk(packed, Ci * kh * kw);
+  if (Ci % gemm_k_tile() == 0) {
+    // every k-tile is one tap's slice of Ci channels: channels-last conv rows (loader mode 6)
+    Gather Bc{};
+    Bc.base = x; Bc.sr0 = H * W * Ci; Bc.R1 = Hout; Bc.R2 = Wn; Bc.ar1 = stride; Bc.ar2 = stride;
+    Bc.ch = -pad_h; Bc.cw = w_lo * stride - pad_w; Bc.Lh = H; Bc.Lw = W; Bc.K1 = kh; Bc.K2 = kw;
+    Bc.divh = Bc.divw = 1; Bc.nhwc = Ci; Bc.kcontig = 1;
+    return gemm(A, Bc, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, as_stream(stream));
+  }
   // rows n = (b, ho, wo - w_lo), k = (i, j, ci): the input element x[b][ho*s - ph + i]
   // [(w_lo + wo)*s - pw + j][ci] sits at w' = win * Ci + ci along the fused (w, c) axis, so the
   // inner k digit (j, ci) is a unit-stride run of kw * Ci floats (loader mode 4, float4 loads)
@@ -938,14 +975,6 @@ int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, in
   Bg.sk0 = 0; Bg.K1 = kh; Bg.K2 = kw * Ci; Bg.bk1 = 1; Bg.bk2 = 1;
   Bg.ch = -pad_h; Bg.cw = (w_lo * stride - pad_w) * Ci; Bg.divh = Bg.divw = 1;
   Bg.Lh = H; Bg.Lw = W * Ci; Bg.sh = W * Ci; Bg.sw = 1; Bg.kcontig = 1;
-  Epilogue E;
-  if (y_nhwc) {
-    E = epi_bn(y + (int64_t)w_lo * Co, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
-    E.N1 = Hout; E.N2 = Wn; E.so0 = Hout * Wout * Co; E.so1 = Wout * Co; E.so2 = Co; E.som = 1;
-  } else {
-    E = epi_bn(y + w_lo, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
-    E.N1 = Hout; E.N2 = Wn; E.so0 = Co * Hout * Wout; E.so1 = Wout; E.so2 = 1; E.som = Hout * Wout;
-  }
   return gemm(A, Bg, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, as_stream(stream));
 }
 
