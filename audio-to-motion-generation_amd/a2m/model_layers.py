@@ -238,10 +238,13 @@ class AudioEncoder(nn.Module):
             time_steps = x.shape[-2]
         if _grad_path(self, x):
             return _autograd().audio_encoder(self, x, time_steps)
+        return self._eval_chain(x.contiguous(), time_steps)
+
+    def _eval_chain(self, x, time_steps, out=None):
         cols = self.live_columns(x.shape[-1])
         nhwc = [_ENC_NHWC and self._nhwc_layer(i) for i in range(len(self.conv))]
         # the mel [B, T, F] is NHWC with C = 1 and NCHW with the channel unsqueezed, for free
-        h = x.contiguous().unsqueeze(-1 if nhwc[0] else 1)
+        h = x.unsqueeze(-1 if nhwc[0] else 1)
         for i, (layer, c) in enumerate(zip(self.conv, cols)):
             if nhwc[i]:
                 k, s, p = layer.geometry()
@@ -251,7 +254,7 @@ class AudioEncoder(nn.Module):
                                   cache=layer._nhwc)
             else:
                 h = layer(h, cols=c)
-        return F.interp_time(h, time_steps)
+        return F.interp_time(h, time_steps, out=out)
 
     def _nhwc_layer(self, i):
         """Channels-last for every layer the GEMM engine can read as contiguous channel runs:

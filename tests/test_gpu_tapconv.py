@@ -130,13 +130,17 @@ def test_bf16x6_generator_eval_golden(g_state):
 @pytest.mark.parametrize('B,Ci,Co,H,W,k,s,p,cols', [
     (4, 1, 64, 64, 128, (4, 4), 2, (1, 1), (9, 55)),      # encoder conv0 (mel, Ci = 1)
     (3, 64, 128, 32, 64, (4, 4), 2, (1, 1), (5, 27)),     # conv1
+    (2, 128, 256, 16, 32, (4, 4), 2, (1, 1), (3, 13)),    # conv2
+    (3, 32, 64, 10, 14, (3, 3), 1, (1, 1), (2, 11)),      # Ci = one k-tile
     (2, 256, 512, 8, 16, (3, 3), 1, (1, 1), (4, 12)),     # conv3
     (2, 512, 256, 8, 8, (3, 8), 1, (1, 0), (0, 1)),       # conv4 (3 x 8 kernel, W_out = 1)
     (2, 12, 20, 9, 11, (3, 3), 2, (1, 1), None)])
 @pytest.mark.parametrize('out_nhwc', [True, False])
 def test_conv2d_nhwc_matches_fp64(B, Ci, Co, H, W, k, s, p, cols, out_nhwc):
-    """Channels-last conv2d (a2m_conv2d_nhwc_fwd_f32: activation operand as unit-stride runs of
-    kw*Ci floats, loader mode 4) against an fp64 convolution, on the computed column range."""
+    """Channels-last conv2d (a2m_conv2d_nhwc_fwd_f32) against an fp64 convolution, on the
+    computed column range: Ci = 1 (conv0) through the direct kernel; Ci a multiple of the k-tile
+    through loader mode 6 (per-tap channel runs); other Ci through mode 4 (unit-stride runs of
+    kw*Ci floats)."""
     from a2m import functional as F
     g = torch.Generator().manual_seed(B + Ci + Co + H)
     x = torch.randn(B, Ci, H, W, generator=g)
