@@ -131,6 +131,40 @@ def conv1d(x, w, b=None, stride=1, pad=0, bn=None, act=ACT_NONE, slope=0.2, out=
     return out
 
 
+def _group_stride(ts):
+    """Element offset between consecutive problems of a grouped launch (uniform spacing; the
+    tensors may live in different allocations -- the kernels only add g * stride)."""
+    if len(ts) == 1:
+        return 0
+    d = ts[1].data_ptr() - ts[0].data_ptr()
+    for i in range(2, len(ts)):
+        assert ts[i].data_ptr() - ts[i - 1].data_ptr() == d, 'grouped operands must be evenly spaced'
+    assert d % 16 == 0
+    return d // 4
+
+
+def conv1d_tap_group(xs, packed, chunk, bias, Co, ks, pad, bn, act, slope, outs):
+    """G same-shape tap-chunked conv1d problems in one launch (a2m_conv1d_tap_group_fwd_f32).
+    xs / outs: lists of G [B, Ci, T] / [B, Co, T] views with equal strides; packed [G, n] and
+    bias / BN tensors [G, Co] stacked per problem (see group_params)."""
+    x0, y0 = xs[0], outs[0]
+    _check_dev(x0, y0, packed)
+    B, Ci, T = x0.shape
+    assert all(x.stride() == x0.stride() and x.shape == x0.shape for x in xs)
+    assert all(y.stride() == y0.stride() and tuple(y.shape) == (B, Co, T) for y in outs)
+    assert _tap_eligible(x0, ks, 1, pad, Ci) and Ci % chunk == 0 and chunk == N.lib.a2m_conv1d_tap_chunk()
+    G = len(xs)
+    xs_g, ys_g = _group_stride(xs), _group_stride(outs)
+    xsb, ysb = x0.stride(0), y0.stride(0)
+    if B == 1:
+        xsb, ysb = T * x0.stride(2), T * y0.stride(2)
+    _with_ws(x0.device, lambda wp, wn: N.lib.a2m_conv1d_tap_group_fwd_f32(
+        _p(x0), xs_g, xsb, x0.stride(1), G, B, Ci, T, _p(packed), packed.stride(0), chunk, _p(bias), Co,
+        ks, pad, *_bn_args(bn), act, slope, _p(y0), ys_g, ysb, y0.stride(1), y0.stride(2), wp, wn,
+        _stream()))
+    return outs
+
+
 def linear(x, w, b=None, out=None):
     """y = x W^T + b over the last dim of x ([..., I] -> [..., O])."""
     lead = x.shape[:-1]
@@ -348,6 +382,25 @@ def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=No
     if save is not None:
         save['qkv'], save['attn'] = qkv, attn
     return out
+
+
+def self_attention_group(xs, wqkv, bqkv, gamma, outs, res=None):
+    """G SelfAttention eval problems in one launch (a2m_self_attention_eval_group_f32): xs / outs
+    / res lists of G [B, C, T] views (channel stride T, equal batch strides), wqkv [G, C/4 + C, C],
+    bqkv [G, C/4 + C], gamma [G] stacked per problem."""
+    x0, y0 = xs[0], outs[0]
+    _check_dev(x0, y0, wqkv, bqkv, gamma)
+    B, C, T = x0.shape
+    assert N.lib.a2m_self_attention_eval_fits(C, T) and N.lib.a2m_get_gemm_precision() == 0
+    for t in list(xs) + list(outs) + list(res or []):
+        assert tuple(t.shape) == (B, C, T) and t.stride() == x0.stride() and t.stride(1) == T
+    assert x0.stride(0) % 4 == 0 and x0.data_ptr() % 16 == 0
+    assert wqkv.is_contiguous() and bqkv.is_contiguous() and gamma.is_contiguous()
+    N.check(N.lib.a2m_self_attention_eval_group_f32(
+        _p(x0), _group_stride(xs), x0.stride(0), len(xs), B, C, T, _p(wqkv), _p(bqkv), _p(gamma),
+        _p(res[0]) if res else None, _group_stride(res) if res else 0, _p(y0), _group_stride(outs),
+        _stream()))
+    return outs
 
 
 def channel_attention(x, w1, b1, w2, b2, out=None, att=None):

@@ -67,6 +67,7 @@ class SelfAttention_G(_GraphTopology):
         self.body_edge_index = S.edge_index(0, S.NUM_BODY)
         self.hand_edge_index = S.edge_index(10, S.NUM_HAND)
         self._register_topology()
+        self._grouped = {}   # stacked per-branch parameters of the grouped eval launches
         C, J = out_channels, self.joint_feat_dim
         for part, nj in (('body', S.NUM_BODY), ('hand', S.NUM_HAND)):
             if part == 'body':
@@ -137,6 +138,95 @@ class SelfAttention_G(_GraphTopology):
         nf = lg.weight.shape[0]
         F.conv1d(x, lg.weight, lg.bias, out=pose_out[:, :, f0:f0 + nf].permute(0, 2, 1))
 
+    # ------------------------------------------------------------------ grouped decoders
+    # The body and hand decoders share their layer shapes up to the graph stacks' joint counts:
+    # decoder_pre = ResBlock + ConvNormRelu (+ ChannelAttention / SelfAttention in either
+    # order), decoder_post = ResBlock + ConvNormRelu + SelfAttention (+ hand's ChannelAttention).
+    # Eval runs each shared layer for both branches as ONE grouped launch (batch = 2 problems
+    # with their own weights): twice the workgroups per launch at B = 64, half the launches,
+    # in place of two concurrent streams of small launches.
+    def _group(self, key, mods, build):
+        """Per-problem stacked parameters of `mods` (one per branch), rebuilt when any source
+        parameter changes (functional._wkey: weight epoch, pointer, version)."""
+        srcs = tuple(t for m in mods for t in _group_sources(m))
+        k = F._wkey(srcs)
+        c = self._grouped.get(key)
+        if c is None or c[0] != k:
+            c = self._grouped[key] = (k, build(mods))
+        return c[1]
+
+    def _cnr_group(self, key, mods, xs, outs):
+        def build(ms):
+            chunk = N_tap_chunk()
+            packed = torch.stack([F.conv1d_tap_packed(m.conv.weight, m._tap)[0] for m in ms])
+            st = lambda f: torch.stack([f(m) for m in ms]).contiguous()
+            bn = (st(lambda m: m.norm.weight), st(lambda m: m.norm.bias),
+                  st(lambda m: m.norm.running_mean), st(lambda m: m.norm.running_var), ms[0].norm.eps)
+            return packed, chunk, st(lambda m: m.conv.bias), bn
+        packed, chunk, bias, bn = self._group(key, mods, build)
+        m0 = mods[0]
+        k, s, p = m0.geometry()
+        F.conv1d_tap_group(xs, packed, chunk, bias, m0.conv.out_channels, k, p, bn, m0.act, 0.2, outs)
+        return outs
+
+    def _sa_group(self, key, mods, xs, outs, res=None):
+        def build(ms):
+            qkv = [F.stacked_qkv(*m.weights()[:6], cache=m._pack) for m in ms]
+            return (torch.stack([w for w, _ in qkv]), torch.stack([b for _, b in qkv]),
+                    torch.cat([m.gamma.reshape(1) for m in ms]))
+        wqkv, bqkv, gamma = self._group(key, mods, build)
+        return F.self_attention_group(xs, wqkv, bqkv, gamma, outs, res=res)
+
+    def _resblock_group(self, key, mods, xs, outs):
+        B, C, T = xs[0].shape
+        t1 = torch.empty(2, B, C, T, device=xs[0].device)
+        t2 = torch.empty(2, B, C, T, device=xs[0].device)
+        self._cnr_group(key + '.c1', [m.conv1 for m in mods], xs, list(t1))
+        self._cnr_group(key + '.c2', [m.conv2 for m in mods], list(t1), list(t2))
+        return self._sa_group(key + '.sa', [m.attention for m in mods], list(t2), outs, res=xs)
+
+    def _groupable(self, feats):
+        B, C, T = feats.shape
+        return (_GROUPED and F.N.lib.a2m_get_gemm_precision() == 0 and
+                F.N.lib.a2m_self_attention_eval_fits(C, T) and
+                F._tap_eligible(feats, 3, 1, 1, C) and C % N_tap_chunk() == 0)
+
+    def _decoders_grouped(self, feats, out):
+        B, C, T = feats.shape
+        dev = feats.device
+        bp, hp = self.body_decoder_pre, self.hand_decoder_pre
+        bq, hq = self.body_decoder_post, self.hand_decoder_post
+        buf = lambda: torch.empty(2, B, C, T, device=dev)
+        # pre: ResBlock, ConvNormRelu grouped; body CA -> SA | hand SA -> CA
+        a, b = buf(), buf()
+        self._resblock_group('pre.rb', [bp[0], hp[0]], [feats, feats], list(a))
+        self._cnr_group('pre.cnr', [bp[1], hp[1]], list(a), list(b))
+        body_ca = F.channel_attention(b[0], *bp[2].weights())
+        self._sa_group('pre.sa', [bp[3], hp[2]], [body_ca, b[1]], list(a))
+        hand_x = F.channel_attention(a[1], *hp[3].weights())
+        # graph stacks (10 / 42 joints): body on the side stream, hand on the caller's
+        g = buf()
+        if _BRANCH_STREAMS:
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._graph_stack('body', a[0], g[0])
+            self._graph_stack('hand', hand_x, g[1])
+            main.wait_stream(side)
+        else:
+            self._graph_stack('body', a[0], g[0])
+            self._graph_stack('hand', hand_x, g[1])
+        # post: ResBlock, ConvNormRelu, SelfAttention grouped; hand's ChannelAttention
+        self._resblock_group('post.rb', [bq[0], hq[0]], list(g), list(a))
+        self._cnr_group('post.cnr', [bq[1], hq[1]], list(a), list(b))
+        self._sa_group('post.sa', [bq[2], hq[2]], list(b), list(a))
+        hand_y = F.channel_attention(a[1], *hq[3].weights())
+        for part, x, f0 in (('body', a[0], 0), ('hand', hand_y, self.body_feats)):
+            lg = getattr(self, f'{part}_logits')
+            nf = lg.weight.shape[0]
+            F.conv1d(x, lg.weight, lg.bias, out=out[:, :, f0:f0 + nf].permute(0, 2, 1))
+
     def forward(self, audio, real_pose=None):
         (audio, real_pose), home = stage_inputs(self, audio, real_pose)
         out, losses = self._forward(audio, real_pose)
@@ -150,7 +240,9 @@ class SelfAttention_G(_GraphTopology):
         B, T, _ = audio.shape
         feats = self.unet(self.audio_encoder(audio))
         out = torch.empty(B, T, self.body_feats + self.hand_feats, device=audio.device)
-        if _BRANCH_STREAMS:
+        if self._groupable(feats):
+            self._decoders_grouped(feats, out)
+        elif _BRANCH_STREAMS:
             # the body and hand decoders are independent after the UNet: the body branch runs
             # on a side stream (forked from / joined to the caller's, so graph capture records
             # both), overlapping its latency-bound small launches with the hand branch's
@@ -202,6 +294,19 @@ class SelfAttention_G(_GraphTopology):
 
 
 _BRANCH_STREAMS = os.environ.get('A2M_BRANCH_STREAMS', '1') != '0'
+_GROUPED = os.environ.get('A2M_GROUPED_DEC', '1') != '0'   # body + hand layers as grouped launches
+
+
+def N_tap_chunk():
+    return F.N.lib.a2m_conv1d_tap_chunk()
+
+
+def _group_sources(m):
+    """The parameters / buffers a grouped launch stacks for module m."""
+    if isinstance(m, ConvNormRelu):
+        n = m.norm
+        return (m.conv.weight, m.conv.bias, n.weight, n.bias, n.running_mean, n.running_var)
+    return m.weights()   # SelfAttention
 _FUSED_STACK = os.environ.get('A2M_GRAPH_STACK', '1') != '0'   # one launch for the 5 graph layers
 _SIDE_STREAMS = {}
 

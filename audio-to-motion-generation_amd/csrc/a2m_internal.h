@@ -85,6 +85,7 @@ inline Gather dense_kr(const float* p, int ld, int64_t bstride = 0) {  // [K][R]
 
 // Output / epilogue: C[m][n] -> out[z*bstride + n0*so0 + n1*so1 + n2*so2 + m*som],
 // n = (n0*N1 + n1)*N2 + n2.  v = acc (+bias[m]); BN-eval affine; activation;
+// (grouped launches: problem z reads bias / BN entry m + z*pstride)
 // v = v*gamma[0] (if gamma); v += res1[addr] + res2[addr] (same addressing as out).
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_SIGMOID = 3 };
 
@@ -101,6 +102,7 @@ struct Epilogue {
   const float* gamma;
   const float* res1; const float* res2;
   int accumulate;  // 1: out += v
+  int pstride;     // grouped launches: bias / BN arrays of problem z start at z * pstride
 };
 
 inline Epilogue epi_dense(float* out, int ldn, int64_t bstride = 0) {  // out[m][n], ld = ldn
@@ -201,8 +203,10 @@ int attn_core(const float* qkv, int64_t qs_b, int B, int C, int T, const float* 
               hipStream_t st);
 // Eval-only QKV + attention in one launch (C in {128, 256}, T <= 64, T % 4 == 0).
 bool attn_fused_eval_fits(int C, int T);
+// G > 1: G problems with their own weights (wqkv / bqkv / gamma stacked per problem) over
+// x + g*x_gs, res + g*res_gs, y + g*y_gs (grouped decoder branches)
 int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const float* wqkv,
                     const float* bqkv, const float* gamma, const float* res, float* y,
-                    hipStream_t st);
+                    hipStream_t st, int G = 1, int64_t x_gs = 0, int64_t res_gs = 0, int64_t y_gs = 0);
 
 }  // namespace a2m

@@ -173,7 +173,16 @@ constexpr int FCOLS = 128;    // projection output columns: Q 32 | K 32 | V 64
 __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
     const float* __restrict__ x, int64_t x_bs, int C, int T, const float* __restrict__ wqkv,
     const float* __restrict__ bqkv, const float* __restrict__ gamma, const float* __restrict__ res,
-    float* __restrict__ y) {
+    float* __restrict__ y, int B, int64_t x_gs, int64_t res_gs, int64_t y_gs) {
+  {  // grouped launches: blockIdx.y = g * B + b, problem g with its own weights
+    const int g = blockIdx.y / B;
+    x += g * x_gs;
+    y += g * y_gs;
+    if (res) res += g * res_gs;
+    wqkv += (int64_t)g * (C / 4 + C) * C;
+    bqkv += (int64_t)g * (C / 4 + C);
+    gamma += g;
+  }
   constexpr int XT = AT * FKP, WTL = FCOLS * FKP, STG = XT + WTL;  // eight waves
   // stages (2 x (x tile + w tile)) early; Q^T, K^T, V, scores overlay them afterwards
   __shared__ __attribute__((aligned(16))) float lds[2 * STG];
@@ -182,7 +191,7 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   float* vs = ks + AT * QP;            // [c][j]  pitch AP
   float* ss = vs + ACH * AP;           // [i][j]  pitch AP
   static_assert(2 * AT * QP + 2 * ACH * AP <= 2 * STG, "overlay must fit the stages");
-  const int b = blockIdx.y, c0 = blockIdx.x * ACH;
+  const int b = blockIdx.y % B, c0 = blockIdx.x * ACH;
   const int Cq = C / 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
@@ -608,10 +617,10 @@ int attn_core_wide(const float* qkv, int64_t qs_b, int B, int C, int T, const fl
 
 int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const float* wqkv,
                     const float* bqkv, const float* gamma, const float* res, float* y,
-                    hipStream_t st) {
-  dim3 grid((unsigned)cdiv(C, ACH), (unsigned)B);
+                    hipStream_t st, int G, int64_t x_gs, int64_t res_gs, int64_t y_gs) {
+  dim3 grid((unsigned)cdiv(C, ACH), (unsigned)(B * G));
   hipLaunchKernelGGL(attn_fused_eval_kernel, grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
-                     res, y);
+                     res, y, B, x_gs, res_gs, y_gs);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

@@ -586,7 +586,7 @@ __device__ __forceinline__ float epi_value(const Epilogue& E, float v, int m) {
 
 __device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int m, int64_t a) {
   int64_t off = (int64_t)z * E.bstride + a;
-  v = epi_value(E, v, m);
+  v = epi_value(E, v, m + z * E.pstride);
   if (E.res1) v += E.res1[off];
   if (E.res2) v += E.res2[off];
   if (E.accumulate) v += E.out[off];

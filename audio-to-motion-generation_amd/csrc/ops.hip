@@ -584,6 +584,40 @@ int a2m_conv1d_tap_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B
   return gemm(A, Bg, E, Co, B * T, Ci * ks, 1, ws, ws_bytes, as_stream(stream));
 }
 
+int a2m_conv1d_tap_group_fwd_f32(const float* x, int64_t xs_g, int64_t xs_b, int64_t xs_c, int32_t G,
+                                 int32_t B, int32_t Ci, int32_t T, const float* packed, int64_t w_gs,
+                                 int32_t chunk, const float* bias, int32_t Co, int32_t ks, int32_t pad,
+                                 const float* bn_w, const float* bn_b, const float* bn_rm,
+                                 const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
+                                 int64_t ys_g, int64_t ys_b, int64_t ys_c, int64_t ys_t, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && packed && y && G > 0, "conv1d_tap_group: null pointer / G=%d", G);
+  A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && ks > 1 && 2 * pad == ks - 1,
+                "conv1d_tap_group: bad shape B=%d Ci=%d Co=%d k=%d p=%d (stride 1, same padding)", B,
+                Ci, Co, ks, pad);
+  A2M_CHECK_ARG(chunk == gemm_k_tile() && Ci % chunk == 0,
+                "conv1d_tap_group: weights packed in %d-channel chunks, the engine's k-tile is %d (Ci=%d)",
+                chunk, gemm_k_tile(), Ci);
+  A2M_CHECK_ARG(T > 0 && T % 4 == 0 && 64 % T == 0 && pad < T,
+                "conv1d_tap_group: clip length %d must divide the 64-row tile and be a multiple of 4", T);
+  A2M_CHECK_ARG(fits32(xs_b) && fits32(xs_c) && fits32((int64_t)B * xs_b) && fits32((int64_t)B * ys_b) &&
+                    fits32(ys_c) && fits32(ys_t) && ys_g != 0 && w_gs >= (int64_t)Co * Ci * ks,
+                "conv1d_tap_group: strides");
+  A2M_CHECK_ARG((reinterpret_cast<uintptr_t>(x) % 16) == 0 && xs_b % 4 == 0 && xs_c % 4 == 0 &&
+                    xs_g % 4 == 0 && w_gs % 4 == 0 && (reinterpret_cast<uintptr_t>(packed) % 16) == 0,
+                "conv1d_tap_group: x rows / packed weights must be 16-byte aligned");
+  Gather A = dense_rk(packed, Ci * ks, w_gs);
+  Gather Bg{};
+  Bg.base = x; Bg.bstride = xs_g;
+  Bg.sr0 = (int)xs_b; Bg.R1 = 1; Bg.R2 = T; Bg.sk0 = (int)xs_c;
+  Bg.K1 = Bg.K2 = 1; Bg.divh = Bg.divw = 1; Bg.Lh = Bg.Lw = 1;
+  Bg.cw = -pad; Bg.tapconv = ks;
+  Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+  E.N1 = 1; E.N2 = T; E.so0 = (int)ys_b; E.so1 = 0; E.so2 = (int)ys_t; E.som = (int)ys_c;
+  E.bstride = ys_g; E.pstride = Co;
+  return gemm(A, Bg, E, Co, B * T, Ci * ks, G, ws, ws_bytes, as_stream(stream));
+}
+
 int a2m_convt1d_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int32_t stride,
                          int32_t pad, float* packed, void* stream) {
   A2M_CHECK_ARG(w && packed && Ci > 0 && Co > 0 && ks > 0 && stride > 0 && pad >= 0,
@@ -832,6 +866,31 @@ __global__ __launch_bounds__(256) void conv2d_c1_kernel(
   // input rows ho0*s - ph + i and the columns the live outputs read, zero outside the image
   const int c0 = w_lo * stride - pw, nc = (w_hi - 1 - w_lo) * stride + kw;
   const int nin = (nr - 1) * stride + kh;
+  // this thread's 4 channels: taps, bias and BN terms requested first, so their round trip
+  // overlaps the patch loads below instead of following them
+  const int ng = Co / 4;                 // float4 channel groups
+  const int wpp = blockDim.x / ng;       // output columns per pass
+  const int g = tid % ng, wsub = tid / ng;
+  float wt[4][kh * kw];
+  float sc[4], sh[4], bo[4], rm[4], rv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = 4 * g + j;
+    const float4* wp = reinterpret_cast<const float4*>(packed + co * kh * kw);
+#pragma unroll
+    for (int t = 0; t < kh * kw / 4; ++t) {
+      const float4 v = wp[t];
+      wt[j][4 * t] = v.x; wt[j][4 * t + 1] = v.y; wt[j][4 * t + 2] = v.z; wt[j][4 * t + 3] = v.w;
+    }
+    // raw terms only here; the arithmetic on them waits until the patch loads are out
+    sh[j] = bias ? bias[co] : 0.f;
+    if (bn_w) {
+      sc[j] = bn_w[co];
+      bo[j] = bn_b[co];
+      rm[j] = bn_rm[co];
+      rv[j] = bn_rv[co];
+    }
+  }
   // the input patch: the first C1_PRE elements per thread are loaded all at once (clamped
   // addresses, zeroed after the loads), so their latencies overlap instead of one dependent
   // round trip per element; wider patches finish in the plain loop
@@ -858,29 +917,14 @@ __global__ __launch_bounds__(256) void conv2d_c1_kernel(
     const int hi = ho0 * stride - ph + i, wi = c0 + c;
     rows[i][c] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? x[((int64_t)b * H + hi) * W + wi] : 0.f;
   }
-  const int ng = Co / 4;                 // float4 channel groups
-  const int wpp = blockDim.x / ng;       // output columns per pass
-  const int g = tid % ng, wsub = tid / ng;
-  float wt[4][kh * kw];
-  float sc[4], sh[4], bo[4];
+  // epi_value order: + bias, then (v - rm) * (w / sqrt(rv + eps)) + b
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int co = 4 * g + j;
-    const float4* wp = reinterpret_cast<const float4*>(packed + co * kh * kw);
-#pragma unroll
-    for (int t = 0; t < kh * kw / 4; ++t) {
-      const float4 v = wp[t];
-      wt[j][4 * t] = v.x; wt[j][4 * t + 1] = v.y; wt[j][4 * t + 2] = v.z; wt[j][4 * t + 3] = v.w;
-    }
-    // epi_value order: + bias, then (v - rm) * (w / sqrt(rv + eps)) + b
-    const float bb = bias ? bias[co] : 0.f;
     if (bn_w) {
-      sc[j] = bn_w[co] / sqrtf(bn_rv[co] + bn_eps);
-      sh[j] = bb - bn_rm[co];
-      bo[j] = bn_b[co];
+      sc[j] = sc[j] / sqrtf(rv[j] + bn_eps);
+      sh[j] = sh[j] - rm[j];
     } else {
       sc[j] = 1.f;
-      sh[j] = bb;
       bo[j] = 0.f;
     }
   }
@@ -1094,6 +1138,20 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
 }
 
 int32_t a2m_self_attention_eval_fits(int32_t C, int32_t T) { return attn_fused_eval_fits(C, T) ? 1 : 0; }
+
+int a2m_self_attention_eval_group_f32(const float* x, int64_t x_gs, int64_t x_bs, int32_t G, int32_t B,
+                                      int32_t C, int32_t T, const float* wqkv, const float* bqkv,
+                                      const float* gamma, const float* res, int64_t res_gs, float* y,
+                                      int64_t y_gs, void* stream) {
+  A2M_CHECK_ARG(x && wqkv && bqkv && gamma && y && B > 0 && G > 0, "self_attention_eval_group: null pointer");
+  A2M_CHECK_ARG(attn_fused_eval_fits(C, T), "self_attention_eval_group: C=%d T=%d not supported", C, T);
+  A2M_CHECK_ARG(x_bs % 4 == 0 && x_gs % 4 == 0 && y_gs % 4 == 0 && res_gs % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+                "self_attention_eval_group: x / y layout");
+  A2M_CHECK_ARG(fits32((int64_t)B * x_bs), "self_attention_eval_group: too large");
+  return attn_fused_eval(x, x_bs, B, C, T, wqkv, bqkv, gamma, res, y, as_stream(stream), G, x_gs,
+                         res_gs, y_gs);
+}
 
 int a2m_self_attention_eval_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
                                 const float* wqkv, const float* bqkv, const float* gamma,

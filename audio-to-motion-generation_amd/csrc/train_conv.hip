@@ -113,20 +113,25 @@ int a2m_conv2d_wgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
   A2M_CHECK_ARG(dy && x && dw && B > 0 && Co > 0 && Ci > 0 && Ho > 0 && Wo > 0, "conv_wgrad: bad args");
   A2M_CHECK_ARG((int64_t)B * Co * Ho * Wo < (1LL << 31) && (int64_t)B * xs_b < (1LL << 31),
                 "conv_wgrad: too large");
+  // The reduction runs over k = (b, ho, wo') with wo' padded up to a multiple of 4 when the
+  // rows are unit-stride (dY's padded entries read as 0), so both operands load as float4 runs
+  // (loader mode 4) instead of element gathers: the encoder's (3, 8) conv has Wo = 15, and its
+  // wgrad took 0.9 ms a G-step on the scalar gathers.
+  const int Wk = (stride_w == 1 && xs_w == 1) ? (int)cdiv(Wo, 4) * 4 : Wo;
   // A(m=co, k=(b,ho,wo)) = dY[b][co][ho][wo]   (dY contiguous)
   Gather A{};
   A.base = dy; A.sr0 = Ho * Wo; A.R1 = A.R2 = 1;
-  A.sk0 = Co * Ho * Wo; A.K1 = Ho; A.K2 = Wo; A.bk1 = 1; A.bk2 = 1; A.Lh = Ho; A.Lw = Wo;
+  A.sk0 = Co * Ho * Wo; A.K1 = Ho; A.K2 = Wk; A.bk1 = 1; A.bk2 = 1; A.Lh = Ho; A.Lw = Wo;
   A.sh = Wo; A.sw = 1; A.divh = A.divw = 1; A.kcontig = 1;
   // B(n=(ci,ih,iw), k=(b,ho,wo)) = X[b][ci][ho*s + ih - ph][wo*s + iw - pw]
   Gather Bg{};
   Bg.base = x; Bg.sr0 = (int)xs_c; Bg.R1 = kh; Bg.R2 = kw; Bg.ar1 = 1; Bg.ar2 = 1;
-  Bg.sk0 = (int)xs_b; Bg.K1 = Ho; Bg.K2 = Wo; Bg.bk1 = stride_h; Bg.bk2 = stride_w;
+  Bg.sk0 = (int)xs_b; Bg.K1 = Ho; Bg.K2 = Wk; Bg.bk1 = stride_h; Bg.bk2 = stride_w;
   Bg.ch = -pad_h; Bg.cw = -pad_w; Bg.divh = Bg.divw = 1; Bg.Lh = H; Bg.Lw = W;
   Bg.sh = (int)xs_h; Bg.sw = (int)xs_w; Bg.kcontig = 1;
   Epilogue E = epi_dense(dw, Ci * kh * kw);
   E.accumulate = accumulate;
-  return gemm(A, Bg, E, Co, Ci * kh * kw, B * Ho * Wo, 1, ws, ws_bytes, as_stream(stream));
+  return gemm(A, Bg, E, Co, Ci * kh * kw, B * Ho * Wk, 1, ws, ws_bytes, as_stream(stream));
 }
 
 int a2m_gemm_f32(int32_t M, int32_t N, int32_t N1, int32_t K, int32_t K1, int32_t batch,

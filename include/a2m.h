@@ -101,6 +101,18 @@ int a2m_conv1d_tap_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B
                            const float* bn_b, const float* bn_rm, const float* bn_rv, float bn_eps,
                            int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
                            int64_t ys_t, void* ws, size_t ws_bytes, void* stream);
+/* G independent tap-chunked conv1d problems in one launch (the body and hand decoders' layers
+ * of equal shape): problem g reads x + g*xs_g, weights packed + g*w_gs (each packed by
+ * a2m_conv1d_tap_pack_f32), bias / BN arrays at + g*Co, and writes y + g*ys_g (group strides
+ * are element offsets of either sign; xs_g may be 0 for a shared input).  Any of
+ * bias / BN may be NULL for all problems.  Otherwise as a2m_conv1d_tap_fwd_f32. */
+int a2m_conv1d_tap_group_fwd_f32(const float* x, int64_t xs_g, int64_t xs_b, int64_t xs_c, int32_t G,
+                                 int32_t B, int32_t Ci, int32_t T, const float* packed, int64_t w_gs,
+                                 int32_t chunk, const float* bias, int32_t Co, int32_t ks, int32_t pad,
+                                 const float* bn_w, const float* bn_b, const float* bn_rm,
+                                 const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
+                                 int64_t ys_g, int64_t ys_b, int64_t ys_c, int64_t ys_t, void* ws,
+                                 size_t ws_bytes, void* stream);
 /* The same split in two: the per-phase weight packing (packed: Ci*Co*k floats) and the
  * forward on packed weights (callers cache the packing while the weights are unchanged). */
 int a2m_convt1d_pack_f32(const float* w, int32_t Ci, int32_t Co, int32_t ks, int32_t stride,
@@ -197,6 +209,14 @@ int32_t a2m_self_attention_eval_fits(int32_t C, int32_t T);
 int a2m_self_attention_eval_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
                                 const float* wqkv, const float* bqkv, const float* gamma,
                                 const float* res, float* y, int64_t y_bs, void* stream);
+
+/* G such problems in one launch (grid G*B): problem g has its own wqkv + g*(C/4 + C)*C,
+ * bqkv + g*(C/4 + C), gamma + g, and reads x + g*x_gs (batch stride x_bs, also y's), res +
+ * g*res_gs, writes y + g*y_gs. */
+int a2m_self_attention_eval_group_f32(const float* x, int64_t x_gs, int64_t x_bs, int32_t G, int32_t B,
+                                      int32_t C, int32_t T, const float* wqkv, const float* bqkv,
+                                      const float* gamma, const float* res, int64_t res_gs, float* y,
+                                      int64_t y_gs, void* stream);
 
 /* ChannelAttention (model_layers.py:149-174): y = x * (mlp(avg_T x) + mlp(max_T x)),
  * mlp = Linear(C, C/r) -> ReLU -> Linear(C/r, C) -> Sigmoid.  x, y contiguous [B][C][T];
