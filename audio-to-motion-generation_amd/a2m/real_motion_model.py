@@ -131,7 +131,9 @@ class SelfAttention_G(_GraphTopology):
         return F.layernorm_to_bct(rows.view(B * T, C), nrm.weight, nrm.bias, T, eps=nrm.eps, out=out_bct)
 
     def _branch(self, part, feats, pose_out, f0):
-        x = getattr(self, f'{part}_decoder_pre')(feats)
+        self._branch_tail(part, getattr(self, f'{part}_decoder_pre')(feats), pose_out, f0)
+
+    def _branch_tail(self, part, x, pose_out, f0):
         x = self._graph_stack(part, x, None)
         x = getattr(self, f'{part}_decoder_post')(x)
         lg = getattr(self, f'{part}_logits')
@@ -142,9 +144,13 @@ class SelfAttention_G(_GraphTopology):
     # The body and hand decoders share their layer shapes up to the graph stacks' joint counts:
     # decoder_pre = ResBlock + ConvNormRelu (+ ChannelAttention / SelfAttention in either
     # order), decoder_post = ResBlock + ConvNormRelu + SelfAttention (+ hand's ChannelAttention).
-    # Eval runs each shared layer for both branches as ONE grouped launch (batch = 2 problems
-    # with their own weights): twice the workgroups per launch at B = 64, half the launches,
-    # in place of two concurrent streams of small launches.
+    # Eval can run each shared layer for both branches as ONE grouped launch (batch = 2
+    # problems with their own weights): twice the workgroups per launch, half the launches.
+    # Per launch that is faster (two 256->256 k3 convs 62 -> 48 us, two attentions 40 -> 33 us),
+    # but the step measured slower than two concurrent branch streams (A2M_GROUPED_DEC 0 / 1 /
+    # 2: 2.787 / 2.824 / 2.851 ms, three interleaved 200-step runs each): the chip is already
+    # full at B = 64, and the grouped schedule leaves the latency-bound hand graph stack with
+    # less concurrent work beside it.  Off by default; tests/test_gpu_grouped.py keeps it exact.
     def _group(self, key, mods, build):
         """Per-problem stacked parameters of `mods` (one per branch), rebuilt when any source
         parameter changes (functional._wkey: weight epoch, pointer, version)."""
@@ -204,6 +210,21 @@ class SelfAttention_G(_GraphTopology):
         body_ca = F.channel_attention(b[0], *bp[2].weights())
         self._sa_group('pre.sa', [bp[3], hp[2]], [body_ca, b[1]], list(a))
         hand_x = F.channel_attention(a[1], *hp[3].weights())
+        if _GROUPED == 1:
+            # the rest per branch: the hand's graph stack (the longest launch, latency-bound)
+            # runs beside the body's stack and decoder_post instead of alone
+            if _BRANCH_STREAMS:
+                main = torch.cuda.current_stream(dev)
+                side = _side_stream(dev)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._branch_tail('hand', hand_x, out, self.body_feats)
+                self._branch_tail('body', a[0], out, 0)
+                main.wait_stream(side)
+            else:
+                self._branch_tail('body', a[0], out, 0)
+                self._branch_tail('hand', hand_x, out, self.body_feats)
+            return
         # graph stacks (10 / 42 joints): body on the side stream, hand on the caller's
         g = buf()
         if _BRANCH_STREAMS:
@@ -294,7 +315,9 @@ class SelfAttention_G(_GraphTopology):
 
 
 _BRANCH_STREAMS = os.environ.get('A2M_BRANCH_STREAMS', '1') != '0'
-_GROUPED = os.environ.get('A2M_GROUPED_DEC', '1') != '0'   # body + hand layers as grouped launches
+# body + hand decoder layers as grouped launches: 0 off, 1 decoder_pre grouped (the rest per
+# branch on two streams), 2 decoder_pre and decoder_post grouped
+_GROUPED = int(os.environ.get('A2M_GROUPED_DEC', '0'))
 
 
 def N_tap_chunk():

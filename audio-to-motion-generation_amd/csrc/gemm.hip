@@ -18,40 +18,106 @@ __device__ __forceinline__ void reduce_store(const GemmArgs& args, int z, float 
   epi_store(args.E, z, v, m, epi_addr(args.E, m, n));
 }
 
+// Four consecutive inner elements (in .. in+3) of output row / column o: the epilogue
+// constants and the column decomposition are computed once per float4 (mcontig: one column n,
+// rows in..in+3; otherwise one row m, columns in..in+3).
+__device__ __forceinline__ void reduce_store4(const GemmArgs& args, int z, const float4& v, int o, int in) {
+  const Epilogue& E = args.E;
+  const float vv[4] = {v.x, v.y, v.z, v.w};
+  if (args.mcontig) {
+    EpiCol c;
+    c.set(E, o);
+    const int64_t an = c.addr(E);
+    const int64_t off = (int64_t)z * E.bstride + an + in;
+    const int mp = in + z * E.pstride;
+    auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    if (E.som == 1 && !E.res1 && !E.res2 && !E.gamma && al16(E.out + off) && (!E.bias || al16(E.bias + mp)) &&
+        (!E.bn_w || (al16(E.bn_w + mp) && al16(E.bn_b + mp) && al16(E.bn_rm + mp) && al16(E.bn_rv + mp)))) {
+      // four consecutive channels of one output position: vector parameter loads and store
+      float4 bi = make_float4(0.f, 0.f, 0.f, 0.f), w = bi, b = bi, rm = bi, rv = bi;
+      if (E.bias) bi = *reinterpret_cast<const float4*>(E.bias + mp);
+      if (E.bn_w) {
+        w = *reinterpret_cast<const float4*>(E.bn_w + mp);
+        b = *reinterpret_cast<const float4*>(E.bn_b + mp);
+        rm = *reinterpret_cast<const float4*>(E.bn_rm + mp);
+        rv = *reinterpret_cast<const float4*>(E.bn_rv + mp);
+      }
+      const float bia[4] = {bi.x, bi.y, bi.z, bi.w}, wa[4] = {w.x, w.y, w.z, w.w};
+      const float ba[4] = {b.x, b.y, b.z, b.w}, rma[4] = {rm.x, rm.y, rm.z, rm.w};
+      const float rva[4] = {rv.x, rv.y, rv.z, rv.w};
+      float o4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const EpiRow r{bia[j], rma[j], E.bn_w ? wa[j] / sqrtf(rva[j] + E.bn_eps) : 1.f, ba[j]};
+        o4[j] = epi_value_p(E, vv[j], r);
+      }
+      float4 out4 = make_float4(o4[0], o4[1], o4[2], o4[3]);
+      if (E.accumulate) {
+        const float4 q = *reinterpret_cast<const float4*>(E.out + off);
+        out4.x += q.x; out4.y += q.y; out4.z += q.z; out4.w += q.w;
+      }
+      *reinterpret_cast<float4*>(E.out + off) = out4;
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = in + j;
+      epi_store_p(E, z, vv[j], epi_row(E, m + z * E.pstride), an + (int64_t)m * E.som);
+    }
+  } else {
+    const EpiRow r = epi_row(E, o + z * E.pstride);
+    const int64_t am = (int64_t)o * E.som;
+    EpiCol c;
+    c.set(E, in);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j) c.advance(E, 1);
+      epi_store_p(E, z, vv[j], r, c.addr(E) + am);
+    }
+  }
+}
+
+template <typename I>
+__device__ __forceinline__ void splitk_reduce4(const GemmArgs& args, int batch) {
+  const I MN = (I)args.M * args.N;
+  const int S = args.splits;
+  const I inner = args.mcontig ? args.M : args.N;
+  const I total4 = MN * batch / 4;
+  for (I i = blockIdx.x * (I)blockDim.x + threadIdx.x; i < total4; i += (I)gridDim.x * blockDim.x) {
+    const I e = i * 4;
+    const int z = (int)(e / MN);
+    const I mn = e - (I)z * MN;
+    const int o = (int)(mn / inner), in = (int)(mn - (I)o * inner);
+    const float* p = args.partial + (int64_t)z * S * MN + mn;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {
+      const float4 a0 = *reinterpret_cast<const float4*>(p + (int64_t)(s + 0) * MN);
+      const float4 a1 = *reinterpret_cast<const float4*>(p + (int64_t)(s + 1) * MN);
+      const float4 a2 = *reinterpret_cast<const float4*>(p + (int64_t)(s + 2) * MN);
+      const float4 a3 = *reinterpret_cast<const float4*>(p + (int64_t)(s + 3) * MN);
+      v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
+      v.x += a1.x; v.y += a1.y; v.z += a1.z; v.w += a1.w;
+      v.x += a2.x; v.y += a2.y; v.z += a2.z; v.w += a2.w;
+      v.x += a3.x; v.y += a3.y; v.z += a3.z; v.w += a3.w;
+    }
+    for (; s < S; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(p + (int64_t)s * MN);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    reduce_store4(args, z, v, o, in);
+  }
+}
+
 __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
   const int64_t MN = (int64_t)args.M * args.N;
   const int S = args.splits;
   const int inner = args.mcontig ? args.M : args.N;
   if ((inner & 3) == 0) {
-    const int64_t total4 = MN * batch / 4;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
-         i += (int64_t)gridDim.x * blockDim.x) {
-      const int64_t e = i * 4;
-      const int z = (int)(e / MN);
-      const int64_t mn = e - (int64_t)z * MN;
-      const int o = (int)(mn / inner), in = (int)(mn - (int64_t)o * inner);
-      const float* p = args.partial + (int64_t)z * S * MN + mn;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      int s = 0;
-      for (; s + 4 <= S; s += 4) {
-        const float4 a0 = *reinterpret_cast<const float4*>(p + (s + 0) * MN);
-        const float4 a1 = *reinterpret_cast<const float4*>(p + (s + 1) * MN);
-        const float4 a2 = *reinterpret_cast<const float4*>(p + (s + 2) * MN);
-        const float4 a3 = *reinterpret_cast<const float4*>(p + (s + 3) * MN);
-        v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
-        v.x += a1.x; v.y += a1.y; v.z += a1.z; v.w += a1.w;
-        v.x += a2.x; v.y += a2.y; v.z += a2.z; v.w += a2.w;
-        v.x += a3.x; v.y += a3.y; v.z += a3.z; v.w += a3.w;
-      }
-      for (; s < S; ++s) {
-        const float4 a = *reinterpret_cast<const float4*>(p + s * MN);
-        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
-      }
-      reduce_store(args, z, v.x, o, in);
-      reduce_store(args, z, v.y, o, in + 1);
-      reduce_store(args, z, v.z, o, in + 2);
-      reduce_store(args, z, v.w, o, in + 3);
-    }
+    // 32-bit index arithmetic whenever the slab set fits (the 64-bit divisions cost more than
+    // the float4 loads they address)
+    if (MN * batch < (int64_t)1 << 31) splitk_reduce4<int>(args, batch);
+    else splitk_reduce4<int64_t>(args, batch);
     return;
   }
   const int64_t total = MN * batch;
@@ -112,10 +178,7 @@ __global__ __launch_bounds__(RW_LANES * RW_COLS) void splitk_reduce_wide_kernel(
     v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
   }
   const int o = (int)(mn / inner), in = (int)(mn - (int64_t)o * inner);
-  reduce_store(args, z, v.x, o, in);
-  reduce_store(args, z, v.y, o, in + 1);
-  reduce_store(args, z, v.z, o, in + 2);
-  reduce_store(args, z, v.w, o, in + 3);
+  reduce_store4(args, z, v, o, in);
 }
 
 static int env_int(const char* name, int dflt) {

@@ -593,6 +593,60 @@ __device__ __forceinline__ void epi_store(const Epilogue& E, int z, float v, int
   E.out[off] = v;
 }
 
+// The per-channel epilogue constants of one output row m (bias, BN running mean, BN scale
+// w / sqrt(var + eps), BN shift), loaded and computed once per row instead of per element;
+// epi_value_p applies them with exactly epi_value's operations (same results).
+struct __attribute__((aligned(16))) EpiRow {
+  float bias, rm, sc, bb;
+};
+__device__ __forceinline__ EpiRow epi_row(const Epilogue& E, int m) {
+  EpiRow r{0.f, 0.f, 1.f, 0.f};
+  if (E.bias) r.bias = E.bias[m];
+  if (E.bn_w) {
+    r.rm = E.bn_rm[m];
+    r.sc = E.bn_w[m] / sqrtf(E.bn_rv[m] + E.bn_eps);
+    r.bb = E.bn_b[m];
+  }
+  return r;
+}
+__device__ __forceinline__ float epi_value_p(const Epilogue& E, float v, const EpiRow& r) {
+  if (E.bias) v += r.bias;
+  if (E.bn_w) v = (v - r.rm) * r.sc + r.bb;
+  if (E.act == ACT_RELU) v = v > 0.f ? v : 0.f;
+  else if (E.act == ACT_LRELU) v = v > 0.f ? v : v * E.slope;
+  else if (E.act == ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+  if (E.gamma) v *= E.gamma[0];
+  return v;
+}
+__device__ __forceinline__ void epi_store_p(const Epilogue& E, int z, float v, const EpiRow& r, int64_t a) {
+  const int64_t off = (int64_t)z * E.bstride + a;
+  v = epi_value_p(E, v, r);
+  if (E.res1) v += E.res1[off];
+  if (E.res2) v += E.res2[off];
+  if (E.accumulate) v += E.out[off];
+  E.out[off] = v;
+}
+// n -> (n0, n1, n2) of the output's 3-level column index, advanced incrementally
+struct EpiCol {
+  int n0, n1, n2;
+  __device__ __forceinline__ void set(const Epilogue& E, int n) {
+    n2 = n % E.N2;
+    const int t = n / E.N2;
+    n1 = t % E.N1;
+    n0 = t / E.N1;
+  }
+  __device__ __forceinline__ void advance(const Epilogue& E, int d) {
+    n2 += d;
+    while (n2 >= E.N2) {
+      n2 -= E.N2;
+      if (++n1 == E.N1) { n1 = 0; ++n0; }
+    }
+  }
+  __device__ __forceinline__ int64_t addr(const Epilogue& E) const {
+    return (int64_t)n0 * E.so0 + (int64_t)n1 * E.so1 + (int64_t)n2 * E.so2;
+  }
+};
+
 // Main loop, BK = 32 (two 16-k halves per k-tile), one barrier per k-step placed mid-step:
 //   step i:  store tile i+1 (registers) -> LDS[(i+1)&1]; issue global loads of tile i+2;
 //            read half-1 fragments of tile i; MFMAs of half 0 (fragments read last step);
@@ -742,6 +796,7 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
   using LB = TileLoader<BN, BK, MB, P>;
   constexpr int STAGE = LA::TILE + LB::TILE;
   __shared__ __attribute__((aligned(16))) float lds_all[(KS == 3 ? 4 : 2) * STAGE];
+  __shared__ EpiRow epr[BM];   // the block's per-row epilogue constants (final-output launches)
   static_assert(KS == 1 || (TM * TN * 16 * 256 <= 2 * STAGE), "KS = 2 partials must fit the stages");
   const int grp = KS == 1 ? 0 : (int)(threadIdx.x >> 8);
   float* lds = KS == 3 ? lds_all + grp * 2 * STAGE : lds_all;
@@ -782,6 +837,10 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
     if (grp == 0) kend = mid;
     else kbeg = mid;
   }
+
+  // epilogue constants of the block's rows, visible after the k loop's first barrier
+  if (!args.partial && grp == 0 && tid < BM && m0 + tid < args.M)
+    epr[tid] = epi_row(args.E, m0 + tid + batch * args.E.pstride);
 
   LA la;
   LB lb;
@@ -960,14 +1019,22 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
     const int ml = tid % BM;
     const int m = m0 + ml;
     if (m < args.M) {
-      for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
-        const int n = n0 + nl;
-        if (n >= args.N) break;
-        const float v = lds[nl * LDC + ml];
-        if (args.partial)
-          args.partial[(int64_t)zz * args.M * args.N + (int64_t)n * args.M + m] = v;
-        else
-          epi_store(args.E, batch, v, m, epi_addr(args.E, 0, n) + m);
+      if (args.partial) {
+        for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
+          const int n = n0 + nl;
+          if (n >= args.N) break;
+          args.partial[(int64_t)zz * args.M * args.N + (int64_t)n * args.M + m] = lds[nl * LDC + ml];
+        }
+      } else {
+        const EpiRow r = epr[ml];
+        const int64_t am = (int64_t)m * args.E.som;
+        EpiCol c;
+        c.set(args.E, n0 + tid / BM);
+        for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
+          if (n0 + nl >= args.N) break;
+          epi_store_p(args.E, batch, lds[nl * LDC + ml], r, c.addr(args.E) + am);
+          c.advance(args.E, 256 / BM);
+        }
       }
     }
     return;
@@ -991,8 +1058,9 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
       for (int t = 0; t < TM; ++t)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int m = m0 + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-          if (m < args.M) epi_store(args.E, batch, acc[t][u][q], m, an + (int64_t)m * args.E.som);
+          const int ml = wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+          const int m = m0 + ml;
+          if (m < args.M) epi_store_p(args.E, batch, acc[t][u][q], epr[ml], an + (int64_t)m * args.E.som);
         }
     }
   }

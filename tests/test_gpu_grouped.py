@@ -73,8 +73,9 @@ def test_self_attention_group(B, C, T, with_res):
         assert _rel(out[i], ref[i]) < 1e-6, (i, _rel(out[i], ref[i]))
 
 
+@pytest.mark.parametrize('mode', [1, 2])
 @pytest.mark.parametrize('B,T', [(64, 64), (2, 32)])
-def test_generator_grouped_vs_branches(B, T, monkeypatch):
+def test_generator_grouped_vs_branches(B, T, mode, monkeypatch):
     from a2m import real_motion_model as R
     torch.manual_seed(3)
     g = R.SelfAttention_G(time_steps=T).to(DEV).eval()
@@ -89,10 +90,10 @@ def test_generator_grouped_vs_branches(B, T, monkeypatch):
     audio = torch.randn(B, T, 128, device=DEV)
     with torch.no_grad():
         feats = g.unet(g.audio_encoder(audio))
+        monkeypatch.setattr(R, '_GROUPED', mode)
         assert g._groupable(feats)
-        monkeypatch.setattr(R, '_GROUPED', True)
         y1, l1 = g(audio)
-        monkeypatch.setattr(R, '_GROUPED', False)
+        monkeypatch.setattr(R, '_GROUPED', 0)
         y0, l0 = g(audio)
     torch.cuda.synchronize()
     assert _rel(y1, y0) < 1e-5, _rel(y1, y0)

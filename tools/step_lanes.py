@@ -19,3 +19,6 @@ for r in rows[a:b]:
     grid = f"{r.get('Grid_Size_X', r.get('Grid_Size', '?'))}"
     print(f'{q:3s} {s:8.1f} {e:8.1f} {e - s:7.1f}  {r["Kernel_Name"].split("(")[0][-56:]:56s} grid={grid}')
 print('queue end times:', {q: round(v, 1) for q, v in end.items()})
+durs = [(int(rows[steps[i + 1]]['Start_Timestamp']) - int(rows[steps[i]]['Start_Timestamp'])) / 1e3
+        for i in range(len(steps) - 1)]
+print('step start-to-start (us):', [round(d, 1) for d in durs])
