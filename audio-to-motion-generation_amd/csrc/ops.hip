@@ -48,8 +48,26 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(float* x, int rows, i
 // max(0, scale*(dst+0.5)-0.5), scale = in/out computed in fp32 (ATen's
 // area_pixel_compute_source_index); zero-weight taps are skipped so never-computed
 // (pruned) encoder columns are never read.
+__device__ __forceinline__ float interp_time_at(const float* p, int H, int W, int w0, int w1, float lw0,
+                                                float lw1, float sh, int t) {
+  float src = sh * ((float)t + 0.5f) - 0.5f;
+  src = src < 0.f ? 0.f : src;
+  const int h0 = (int)src;
+  const int h1 = h0 + (h0 < H - 1 ? 1 : 0);
+  const float lh1 = src - (float)h0, lh0 = 1.f - lh1;
+  auto row = [&](int h) {
+    float v = lw0 * p[h * W + w0];
+    if (lw1 != 0.f) v += lw1 * p[h * W + w1];
+    return v;
+  };
+  float v = lh0 * row(h0);
+  if (lh1 != 0.f) v += lh1 * row(h1);
+  return v;
+}
+
+// One thread per four consecutive t of a (b, c) row (T % 4 == 0, 32-bit indexing): float4
+// stores; otherwise one output per thread.
 __global__ void interp_time_kernel(const float* x, int B, int C, int H, int W, float* y, int T) {
-  const int64_t total = (int64_t)B * C * T;
   const float sh = (float)H / (float)T;
   const float sw = (float)W / 1.0f;
   float srcw = sw * 0.5f - 0.5f;
@@ -57,24 +75,27 @@ __global__ void interp_time_kernel(const float* x, int B, int C, int H, int W, f
   const int w0 = (int)srcw;
   const int w1 = w0 + (w0 < W - 1 ? 1 : 0);
   const float lw1 = srcw - (float)w0, lw0 = 1.f - lw1;
+  if ((T & 3) == 0) {
+    const int T4 = T >> 2;
+    const int total4 = B * C * T4;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+      const int bc = i / T4, t = (i - bc * T4) * 4;
+      const float* p = x + (int64_t)bc * H * W;
+      float4 v;
+      v.x = interp_time_at(p, H, W, w0, w1, lw0, lw1, sh, t);
+      v.y = interp_time_at(p, H, W, w0, w1, lw0, lw1, sh, t + 1);
+      v.z = interp_time_at(p, H, W, w0, w1, lw0, lw1, sh, t + 2);
+      v.w = interp_time_at(p, H, W, w0, w1, lw0, lw1, sh, t + 3);
+      *reinterpret_cast<float4*>(y + (int64_t)i * 4) = v;
+    }
+    return;
+  }
+  const int64_t total = (int64_t)B * C * T;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int t = (int)(i % T);
     const int64_t bc = i / T;
-    float src = sh * ((float)t + 0.5f) - 0.5f;
-    src = src < 0.f ? 0.f : src;
-    const int h0 = (int)src;
-    const int h1 = h0 + (h0 < H - 1 ? 1 : 0);
-    const float lh1 = src - (float)h0, lh0 = 1.f - lh1;
-    const float* p = x + bc * H * W;
-    auto row = [&](int h) {
-      float v = lw0 * p[h * W + w0];
-      if (lw1 != 0.f) v += lw1 * p[h * W + w1];
-      return v;
-    };
-    float v = lh0 * row(h0);
-    if (lh1 != 0.f) v += lh1 * row(h1);
-    y[i] = v;
+    y[i] = interp_time_at(x + bc * H * W, H, W, w0, w1, lw0, lw1, sh, t);
   }
 }
 
@@ -1046,7 +1067,9 @@ int a2m_repeat_time_f32(const float* x, int32_t B, int32_t C, int32_t T, float s
 int a2m_interp_time_f32(const float* x, int32_t B, int32_t C, int32_t H, int32_t W, float* y,
                         int32_t T, void* stream) {
   A2M_CHECK_ARG(x && y && B > 0 && C > 0 && H > 0 && W > 0 && T > 0, "interp: bad args");
-  const int64_t total = (int64_t)B * C * T;
+  A2M_CHECK_ARG((int64_t)B * C * T < (1LL << 31) && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
+                "interp: too large or y not 16-byte aligned");
+  const int64_t total = (int64_t)B * C * T / ((T & 3) == 0 ? 4 : 1);
   const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
   hipLaunchKernelGGL(interp_time_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, B, C,
                      H, W, y, T);
