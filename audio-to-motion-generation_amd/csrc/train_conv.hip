@@ -113,11 +113,10 @@ int a2m_conv2d_wgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
   A2M_CHECK_ARG(dy && x && dw && B > 0 && Co > 0 && Ci > 0 && Ho > 0 && Wo > 0, "conv_wgrad: bad args");
   A2M_CHECK_ARG((int64_t)B * Co * Ho * Wo < (1LL << 31) && (int64_t)B * xs_b < (1LL << 31),
                 "conv_wgrad: too large");
-  // The reduction runs over k = (b, ho, wo') with wo' padded up to a multiple of 4 when the
-  // rows are unit-stride (dY's padded entries read as 0), so both operands load as float4 runs
-  // (loader mode 4) instead of element gathers: the encoder's (3, 8) conv has Wo = 15, and its
-  // wgrad took 0.9 ms a G-step on the scalar gathers.
-  const int Wk = (stride_w == 1 && xs_w == 1) ? (int)cdiv(Wo, 4) * 4 : Wo;
+  // k = (b, ho, wo).  (Padding wo up to a multiple of 4 so that Wo = 15 rows load as mode-4
+  // float4 runs measured slower: the encoder's (3, 8) conv wgrad 0.91 -> 1.12 ms a call, the
+  // shifted x runs being unaligned; so odd widths keep the element gathers.)
+  const int Wk = Wo;
   // A(m=co, k=(b,ho,wo)) = dY[b][co][ho][wo]   (dY contiguous)
   Gather A{};
   A.base = dy; A.sr0 = Ho * Wo; A.R1 = A.R2 = 1;
