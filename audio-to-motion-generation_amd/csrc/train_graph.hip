@@ -26,12 +26,17 @@ constexpr int BMAXN = 128;
 constexpr int BZP = BF + 4;
 constexpr int BDEG = 8;
 constexpr int BPART = 3 * BF + 2 * BH * BF;  // dbias | dln_w | dln_b | dU[8][64]
+// 512 threads = 8 waves (two per SIMD, so one wave's LDS / barrier waits overlap the other's
+// work at one workgroup per CU): MFMA wave w owns rows 32 (w & 3).. and columns 32 (w >> 2)..;
+// the row-wise phases use 16 lanes per node row, BRG = 32 row groups of BRPT rows each.
+constexpr int BNT = 512, BRG = BNT / 16, BRPT = BMAXN / BRG;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// acc[t] += A[rows][64] (LDS, pitch BZP) . W^T where B(n=j, k=c) = Wt(j, c) given by functor
+// acc += A[rows][64] (LDS, pitch BZP) . W^T over output columns c0 + (0..31), where
+// B(n=j, k=c) = Wt(j, c) given by functor
 template <class WF>
-__device__ __forceinline__ void mfma_rows64(floatx16 (&acc)[2], const float* A, int arow, int lh,
+__device__ __forceinline__ void mfma_rows64(floatx16& acc, const float* A, int arow, int c0, int lh,
                                             int li, WF wf) {
 #pragma unroll
   for (int kc = 0; kc < 4; ++kc) {
@@ -39,37 +44,29 @@ __device__ __forceinline__ void mfma_rows64(floatx16 (&acc)[2], const float* A, 
     const float4 a0 = *reinterpret_cast<const float4*>(p);
     const float4 a1 = *reinterpret_cast<const float4*>(p + 4);
     const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    float bf[8];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      float bf[8];
+    for (int s = 0; s < 8; ++s) bf[s] = wf(c0 + li, kc * 16 + lh * 8 + s);
 #pragma unroll
-      for (int s = 0; s < 8; ++s) bf[s] = wf(t * 32 + li, kc * 16 + lh * 8 + s);
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
-    }
+    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
   }
 }
 
-__device__ __forceinline__ void acc_to_lds(const floatx16 (&acc)[2], float* dst, int wave, int lh,
+__device__ __forceinline__ void acc_to_lds(const floatx16& acc, float* dst, int rblk, int c0, int lh,
                                            int li, float scale) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int r = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-      dst[r * BZP + t * 32 + li] = acc[t][q] * scale;
-    }
+  for (int q = 0; q < 16; ++q) {
+    const int r = rblk * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+    dst[r * BZP + c0 + li] = acc[q] * scale;
+  }
 }
 
-__device__ __forceinline__ void zero_acc(floatx16 (&acc)[2]) {
+__device__ __forceinline__ void zero_acc(floatx16& acc) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 }
 
-__global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
+__global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, int F, int J, int kind, int norm_res,
     const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_idx, const float* __restrict__ w0,
     const float* __restrict__ w1, const float* __restrict__ Ug, const float* __restrict__ bias,
@@ -88,7 +85,7 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
   __shared__ unsigned char nbl[BMAXN][BDEG];
   __shared__ unsigned char rev[BMAXN][BDEG];  // GAT: slot of n in nbl[nbl[n][q]] (0xff: none)
   __shared__ unsigned char ndeg[BMAXN];
-  __shared__ float red[16][3 * BF];
+  __shared__ float red[BRG][3 * BF];
 
   const int fpb = BMAXN / J;
   const int NBmax = fpb * J;
@@ -96,21 +93,22 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
   const int NB = (int)min<int64_t>(NBmax, (int64_t)F * J - node0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5, cg = tid & 15, nr0 = tid >> 4;
-  const int arow = wave * 32 + li;
+  const int rblk = wave & 3, c0 = (wave >> 2) * 32;   // MFMA rows / columns of this wave
+  const int arow = rblk * 32 + li;
   const int ywidth = kind == 0 ? BH * BF : BF;
 
   {  // node tile: all loads of this thread in flight before the LDS writes
-    constexpr int NL = BMAXN * (BF / 4) / 256;
+    constexpr int NL = BMAXN * (BF / 4) / BNT;
     float4 v[NL];
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const int i = tid + j * 256, n = i / (BF / 4), q = i % (BF / 4);
+      const int i = tid + j * BNT, n = i / (BF / 4), q = i % (BF / 4);
       v[j] = n < NB ? *reinterpret_cast<const float4*>(x + (node0 + n) * BF + q * 4)
                     : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const int i = tid + j * 256, n = i / (BF / 4), q = i % (BF / 4);
+      const int i = tid + j * BNT, n = i / (BF / 4), q = i % (BF / 4);
       *reinterpret_cast<float4*>(xs + n * BZP + q * 4) = v[j];
     }
   }
@@ -175,7 +173,7 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
   };
 
   // ---------------------------------------------------------------- forward recompute
-  floatx16 acc[2];
+  floatx16 acc;
   zero_acc(acc);
   const int nseg = kind == 0 ? BH : 2;
   for (int seg = 0; seg < nseg; ++seg) {
@@ -206,19 +204,19 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
     } else {
       A = xs;
     }
-    mfma_rows64(acc, A, arow, lh, li, [&](int j, int c) { return Wseg[j * BF + c]; });
+    mfma_rows64(acc, A, arow, c0, lh, li, [&](int j, int c) { return Wseg[j * BF + c]; });
     __syncthreads();
   }
-  acc_to_lds(acc, bufA, wave, lh, li, kind == 0 ? 1.f / BH : 1.f);  // o (bias added below)
+  acc_to_lds(acc, bufA, rblk, c0, lh, li, kind == 0 ? 1.f / BH : 1.f);  // o (bias added below)
   __syncthreads();
 
   // ---------------------------------------------------------------- LN / act / residual bwd
-  float dxa[8][4];
+  float dxa[BRPT][4];
   float pb[4] = {0.f, 0.f, 0.f, 0.f}, plw[4] = {0.f, 0.f, 0.f, 0.f}, plb[4] = {0.f, 0.f, 0.f, 0.f};
   const float oscale = kind == 0 ? 1.f / BH : 1.f;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int n = nr0 + 16 * r;
+  for (int r = 0; r < BRPT; ++r) {
+    const int n = nr0 + BRG * r;
     float o[4], g4[4];
     const float4 dy4 = n < NB ? *reinterpret_cast<const float4*>(dy + (node0 + n) * BF + cg * 4)
                               : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -272,16 +270,15 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
   }
   __syncthreads();
 
-  float dU[2];  // per-thread slice of the dU partial: items tid and tid + 256 of [8][64]
-  dU[0] = dU[1] = 0.f;
+  float dU = 0.f;  // per-thread item tid of the dU partial [8][64]
   if (kind == 0) {
     for (int h = 0; h < BH; ++h) {
       edge_softmax(h);
       // dY_h = do W_h / 4  -> bufA
       zero_acc(acc);
       const float* Wh = w0 + (int64_t)h * BF * BF;
-      mfma_rows64(acc, bufB, arow, lh, li, [&](int j, int c) { return Wh[c * BF + j]; });
-      acc_to_lds(acc, bufA, wave, lh, li, 1.f / BH);
+      mfma_rows64(acc, bufB, arow, c0, lh, li, [&](int j, int c) { return Wh[c * BF + j]; });
+      acc_to_lds(acc, bufA, rblk, c0, lh, li, 1.f / BH);
       __syncthreads();
       // dalpha[n][q] = dY_h[n] . x[nbl[n][q]]  (16 lanes per node)
       for (int i = tid; i < BMAXN * 16; i += blockDim.x) {
@@ -335,8 +332,8 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
       __syncthreads();
       // dx += aggregation adjoint + logit adjoint;  dU partials
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int n = nr0 + 16 * r;
+      for (int r = 0; r < BRPT; ++r) {
+        const int n = nr0 + BRG * r;
         if (n >= NB) continue;
         float a[4] = {0.f, 0.f, 0.f, 0.f};
         float4 gv[BDEG];
@@ -359,30 +356,28 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
       }
       __syncthreads();
     }
-    // dU partials, all heads in one pass over the block's nodes (every thread: items tid and
-    // tid + 256 of [8][64], q = which * 4 + h)
-#pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      const int item = tid + 256 * k2;
-      const int qq = item / BF, k = item % BF;
+    // dU partials, all heads in one pass over the block's nodes (thread tid: item tid of
+    // [8][64], q = which * 4 + h)
+    {
+      const int qq = tid / BF, k = tid % BF;
       const float* dl = dalh[qq & 3][qq >> 2];
       float s = 0.f;
       for (int n = 0; n < NB; ++n) s += dl[n] * xs[n * BZP + k];
-      dU[k2] = s;
+      dU = s;
     }
   } else {
     // dagg = do W_rel -> bufA ; dx_root = do W_root -> xs (x no longer needed)
     zero_acc(acc);
-    mfma_rows64(acc, bufB, arow, lh, li, [&](int j, int c) { return w0[c * BF + j]; });
-    acc_to_lds(acc, bufA, wave, lh, li, 1.f);
+    mfma_rows64(acc, bufB, arow, c0, lh, li, [&](int j, int c) { return w0[c * BF + j]; });
+    acc_to_lds(acc, bufA, rblk, c0, lh, li, 1.f);
     zero_acc(acc);
-    mfma_rows64(acc, bufB, arow, lh, li, [&](int j, int c) { return w1[c * BF + j]; });
+    mfma_rows64(acc, bufB, arow, c0, lh, li, [&](int j, int c) { return w1[c * BF + j]; });
     __syncthreads();
-    acc_to_lds(acc, xs, wave, lh, li, 1.f);
+    acc_to_lds(acc, xs, rblk, c0, lh, li, 1.f);
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int n = nr0 + 16 * r;
+    for (int r = 0; r < BRPT; ++r) {
+      const int n = nr0 + BRG * r;
       if (n >= NB) continue;
       float a[4];
 #pragma unroll
@@ -401,13 +396,13 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
   }
 
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int n = nr0 + 16 * r;
+  for (int r = 0; r < BRPT; ++r) {
+    const int n = nr0 + BRG * r;
     if (n < NB)
       *reinterpret_cast<float4*>(dx + (node0 + n) * BF + cg * 4) =
           make_float4(dxa[r][0], dxa[r][1], dxa[r][2], dxa[r][3]);
   }
-  // per-workgroup partials: reduce the 16 row-groups through LDS
+  // per-workgroup partials: reduce the BRG row groups through LDS
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     red[nr0][cg * 4 + q] = pb[q];
@@ -418,13 +413,10 @@ __global__ __launch_bounds__(256) void graph_layer_bwd_kernel(
   float* pp = part + (int64_t)blockIdx.x * BPART;
   for (int c = tid; c < 3 * BF; c += blockDim.x) {
     float s = 0.f;
-    for (int g = 0; g < 16; ++g) s += red[g][c];
+    for (int g = 0; g < BRG; ++g) s += red[g][c];
     pp[c] = s;
   }
-  if (kind == 0) {
-    pp[3 * BF + tid] = dU[0];
-    pp[3 * BF + 256 + tid] = dU[1];
-  }
+  if (kind == 0) pp[3 * BF + tid] = dU;
 }
 
 // dU -> att gradients and the extra dW terms: U_q[k] = sum_c W_h[c][k] att_q[c]
@@ -501,7 +493,7 @@ extern "C" int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t 
     hipLaunchKernelGGL(graph_att_proj_kernel2, dim3(1), dim3(2 * BH * BF), 0, st, w0, att_src, att_dst, Ug);
     A2M_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(graph_layer_bwd_kernel, dim3(blocks), dim3(256), 0, st, x, dy, F, J, kind, norm_res,
+  hipLaunchKernelGGL(graph_layer_bwd_kernel, dim3(blocks), dim3(BNT), 0, st, x, dy, F, J, kind, norm_res,
                      nbr_ptr, nbr_idx, w0, w1, Ug, bias, ln_w, ln_b, slope, dx, ybuf, dob, part);
   A2M_LAUNCH_CHECK();
   const int cols = kind == 0 ? BPART : 3 * BF;
