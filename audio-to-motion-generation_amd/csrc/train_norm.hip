@@ -12,7 +12,9 @@
 
 namespace a2m {
 
-constexpr int kSlice = 4096;  // elements of one channel per workgroup
+// elements of one channel per workgroup: four per thread, issued together (a [64, 256, 64]
+// activation is 1,024 workgroups instead of 256 at one latency-bound round trip per element)
+constexpr int kSlice = 1024;
 
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
   uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;
@@ -61,8 +63,9 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(BNArgs a, double* part) {
   const int64_t N = (int64_t)a.B * a.L;
   const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int b = (int)(i / a.L), l = (int)(i % a.L);
+  #pragma unroll 4
+  for (int i = (int)i0 + threadIdx.x; i < (int)i1; i += blockDim.x) {
+    const int b = i / a.L, l = i - (i / a.L) * a.L;
     const float z = a.x[b * a.xs_b + c * a.xs_c + l] * pre_drop(a, b, c, l);
     s1 += z;
     s2 += (double)z * z;
@@ -124,8 +127,9 @@ __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNArgs a, const dou
   __syncthreads();
   const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
   const float mu = stat[0], rs = stat[1], g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int b = (int)(i / a.L), l = (int)(i % a.L);
+  #pragma unroll 4
+  for (int i = (int)i0 + threadIdx.x; i < (int)i1; i += blockDim.x) {
+    const int b = i / a.L, l = i - (i / a.L) * a.L;
     const float z = a.x[b * a.xs_b + c * a.xs_c + l] * pre_drop(a, b, c, l);
     float v = act_fwd((z - mu) * rs * g + bt, act, slope);
     if (a.mode == DROP_AFTER) v *= drop_scale(a.seed, ((uint64_t)b * a.C + c) * a.L + l, a.p);
@@ -141,8 +145,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(BNArgs a, const float* me
   const int64_t N = (int64_t)a.B * a.L;
   const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
   const float mu = mean[c], rs = rstd[c], g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int b = (int)(i / a.L), l = (int)(i % a.L);
+  #pragma unroll 4
+  for (int i = (int)i0 + threadIdx.x; i < (int)i1; i += blockDim.x) {
+    const int b = i / a.L, l = i - (i / a.L) * a.L;
     const float z = a.x[b * a.xs_b + c * a.xs_c + l] * pre_drop(a, b, c, l);
     float v = act_fwd((z - mu) * rs * g + bt, act, slope);
     if (a.mode == DROP_AFTER) v *= drop_scale(a.seed, ((uint64_t)b * a.C + c) * a.L + l, a.p);
@@ -174,8 +179,9 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(BNBwdArgs a, double* 
   const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
   const float mu = a.mean[c], rs = a.rstd[c];
   double sg = 0.0, sgx = 0.0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int b = (int)(i / f.L), l = (int)(i % f.L);
+  #pragma unroll 4
+  for (int i = (int)i0 + threadIdx.x; i < (int)i1; i += blockDim.x) {
+    const int b = i / f.L, l = i - (i / f.L) * f.L;
     const float xhat = (f.x[b * f.xs_b + c * f.xs_c + l] * pre_drop(f, b, c, l) - mu) * rs;
     const float g = bn_g(a, b, c, l, xhat);
     sg += g;
@@ -201,8 +207,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a, const fl
   const float mu = a.mean[c], rs = a.rstd[c], gm = a.gamma ? a.gamma[c] : 1.f;
   const float mg = sums[2 * c] / a.n_div, mgx = sums[2 * c + 1] / a.n_div;
   double sd = 0.0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int b = (int)(i / f.L), l = (int)(i % f.L);
+  #pragma unroll 4
+  for (int i = (int)i0 + threadIdx.x; i < (int)i1; i += blockDim.x) {
+    const int b = i / f.L, l = i - (i / f.L) * f.L;
     const float ds = pre_drop(f, b, c, l);
     const float xhat = (f.x[b * f.xs_b + c * f.xs_c + l] * ds - mu) * rs;
     const float g = bn_g(a, b, c, l, xhat);
@@ -244,8 +251,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(BNBwdArgs a, co
   const float mu = a.mean[c], rs = a.rstd[c], gm = a.gamma ? a.gamma[c] : 1.f;
   const float mg = sums[0] / a.n_div, mgx = sums[1] / a.n_div;
   double sd = 0.0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int b = (int)(i / f.L), l = (int)(i % f.L);
+  #pragma unroll 4
+  for (int i = (int)i0 + threadIdx.x; i < (int)i1; i += blockDim.x) {
+    const int b = i / f.L, l = i - (i / f.L) * f.L;
     const float ds = pre_drop(f, b, c, l);
     const float xhat = (f.x[b * f.xs_b + c * f.xs_c + l] * ds - mu) * rs;
     const float g = bn_g(a, b, c, l, xhat);
@@ -401,7 +409,8 @@ __global__ __launch_bounds__(1024) void reduce_cols_kernel(const float* part, in
   }
 }
 
-static int bn_slices(int64_t N) { return (int)cdiv(N, kSlice); }
+// the kernels index a channel's B * L elements in 32 bits
+static int bn_slices(int64_t N) { return N < (1LL << 31) ? (int)cdiv(N, kSlice) : -1; }
 
 int reduce_cols(const float* part, int rows, int stride, int cols, float* out, int accumulate,
                 hipStream_t st) {
@@ -435,6 +444,7 @@ int a2m_bn_train_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, 
   A2M_CHECK_ARG(x && y && save_mean && save_rstd && B > 0 && C > 0 && L > 0, "bn_train_fwd: bad args");
   const int64_t N = (int64_t)B * L;
   const int S = bn_slices(N);
+  A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
   const size_t need = sizeof(double) * 2 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_train_fwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
@@ -458,6 +468,7 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
   A2M_CHECK_ARG(dy && x && dx && save_mean && save_rstd && B > 0 && C > 0 && L > 0, "bn_train_bwd: bad args");
   const int64_t N = (int64_t)B * L;
   const int S = bn_slices(N);
+  A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
   const size_t need = sizeof(double) * 3 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_train_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNBwdArgs a;
@@ -488,6 +499,7 @@ int a2m_bn_sync_stats_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B,
   A2M_CHECK_ARG(x && sums && B > 0 && C > 0 && L > 0, "bn_sync_stats: bad args");
   const int64_t N = (int64_t)B * L;
   const int S = bn_slices(N);
+  A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
   const size_t need = sizeof(double) * 2 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_sync_stats: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
@@ -531,6 +543,7 @@ int a2m_bn_sync_bwd_stats_f32(const float* dy, int64_t dys_b, int64_t dys_c, con
                 "bn_sync_bwd_stats: bad args");
   const int64_t N = (int64_t)B * L;
   const int S = bn_slices(N);
+  A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
   const size_t need = sizeof(double) * 2 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_sync_bwd_stats: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNBwdArgs a;
@@ -559,6 +572,7 @@ int a2m_bn_sync_bwd_apply_f32(const float* dy, int64_t dys_b, int64_t dys_c, con
                 n_total > 0, "bn_sync_bwd_apply: bad args");
   const int64_t N = (int64_t)B * L;
   const int S = bn_slices(N);
+  A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
   const size_t need = sizeof(double) * (size_t)C * S + sizeof(float) * 2 * (size_t)C + 16;
   if (!ws || ws_bytes < need) { set_error("bn_sync_bwd_apply: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNBwdArgs a;
