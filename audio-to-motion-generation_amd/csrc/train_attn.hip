@@ -44,9 +44,17 @@ __global__ __launch_bounds__(256) void sum_vector_kernel(const float* x, int n, 
   }
 }
 
-// ChannelAttention backward, one workgroup per batch element; weight-gradient partials
-// per batch element go to part[b][W1 (Cr*C) | b1 (Cr) | W2 (C*Cr) | b2 (C)].
-__global__ __launch_bounds__(256) void channel_attention_bwd_kernel(
+// ChannelAttention backward, one workgroup of 512 threads per batch element; weight-gradient
+// partials per batch element go to part[b][W1 (Cr*C) | b1 (Cr) | W2 (C*Cr) | b2 (C)].
+// The reductions over channels / time run on groups of 8 lanes (strided partial sums, then
+// three xor shuffles), so every phase keeps all waves busy instead of one thread per output.
+constexpr int CAB_NT = 512, CAB_G = 8;
+__device__ __forceinline__ float group8_sum(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  return v + __shfl_xor(v, 4);
+}
+__global__ __launch_bounds__(CAB_NT) void channel_attention_bwd_kernel(
     const float* dy, const float* x, int C, int T, const float* w1, const float* b1, int Cr,
     const float* w2, const float* b2, float* dx, float* part) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -62,29 +70,32 @@ __global__ __launch_bounds__(256) void channel_attention_bwd_kernel(
   const int b = blockIdx.x;
   const float* xb = x + (int64_t)b * C * T;
   const float* gb = dy + (int64_t)b * C * T;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int tid = threadIdx.x, gl = tid & (CAB_G - 1), grp = tid / CAB_G;
+  constexpr int NGRP = CAB_NT / CAB_G;
   const int P = 2 * Cr * C + Cr + C;
   float* pb = part + (int64_t)b * P;
-  // pooled stats (first-occurrence argmax, like ATen's adaptive max pool) and da = sum dy*x
-  for (int c = wv; c < C; c += 4) {
+  // pooled stats (first-occurrence argmax, like ATen's adaptive max pool) and da = sum dy*x:
+  // one 8-lane group per channel, lane g over t = g, g + 8, ...
+  for (int c = grp; c < C; c += NGRP) {
     const float* p = xb + (int64_t)c * T;
     const float* q = gb + (int64_t)c * T;
     float sm_ = 0.f, mx = -INFINITY, da = 0.f;
     int ai = T;
-    for (int t = lane; t < T; t += 64) {
+    for (int t = gl; t < T; t += CAB_G) {
       const float v = p[t];
       sm_ += v;
       da += v * q[t];
-      if (v > mx || (v == mx && t < ai)) { mx = v; ai = t; }
+      if (v > mx) { mx = v; ai = t; }
     }
-    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+    for (int o = 1; o < CAB_G; o <<= 1) {
       sm_ += __shfl_xor(sm_, o);
       da += __shfl_xor(da, o);
       const float om = __shfl_xor(mx, o);
       const int oi = __shfl_xor(ai, o);
       if (om > mx || (om == mx && oi < ai)) { mx = om; ai = oi; }
     }
-    if (lane == 0) {
+    if (gl == 0) {
       pavg[c] = sm_ / (float)T;
       pmax[c] = mx;
       amax[c] = ai;
@@ -92,15 +103,17 @@ __global__ __launch_bounds__(256) void channel_attention_bwd_kernel(
     }
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < 2 * Cr; j += blockDim.x) {
+  // h = relu(W1 pooled + b1) for both pools: one 8-lane group per output
+  for (int j = grp; j < 2 * Cr; j += NGRP) {
     const int r = j % Cr;
     const float* in = j < Cr ? pavg : pmax;
-    float a = b1[r];
-    for (int c = 0; c < C; ++c) a += w1[(int64_t)r * C + c] * in[c];
-    h[j] = a > 0.f ? a : 0.f;
+    float a = 0.f;
+    for (int c = gl; c < C; c += CAB_G) a += w1[(int64_t)r * C + c] * in[c];
+    a = group8_sum(a) + b1[r];
+    if (gl == 0) h[j] = a > 0.f ? a : 0.f;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  for (int c = tid; c < C; c += CAB_NT) {
     float a0 = b2[c], a1 = b2[c];
     for (int r = 0; r < Cr; ++r) {
       a0 += w2[(int64_t)c * Cr + r] * h[r];
@@ -116,28 +129,28 @@ __global__ __launch_bounds__(256) void channel_attention_bwd_kernel(
   }
   __syncthreads();
   // dW2[c][r] = dz1[c] h1[r] + dz2[c] h2[r]; db2[c] = dz1 + dz2
-  for (int i = threadIdx.x; i < C * Cr; i += blockDim.x) {
-    const int c = i / Cr, r = i % Cr;
+  for (int i = tid; i < C * Cr; i += CAB_NT) {
+    const int c = i / Cr, r = i - c * Cr;
     pb[Cr * C + Cr + i] = dz[c] * h[r] + dz[C + c] * h[Cr + r];
   }
-  for (int c = threadIdx.x; c < C; c += blockDim.x) pb[2 * Cr * C + Cr + c] = dz[c] + dz[C + c];
+  for (int c = tid; c < C; c += CAB_NT) pb[2 * Cr * C + Cr + c] = dz[c] + dz[C + c];
   // dh = W2^T dz * relu'
-  for (int j = threadIdx.x; j < 2 * Cr; j += blockDim.x) {
+  for (int j = grp; j < 2 * Cr; j += NGRP) {
     const int r = j % Cr;
     const float* d = j < Cr ? dz : dz + C;
     float a = 0.f;
-    for (int c = 0; c < C; ++c) a += w2[(int64_t)c * Cr + r] * d[c];
-    dh[j] = h[j] > 0.f ? a : 0.f;
+    for (int c = gl; c < C; c += CAB_G) a += w2[(int64_t)c * Cr + r] * d[c];
+    a = group8_sum(a);
+    if (gl == 0) dh[j] = h[j] > 0.f ? a : 0.f;
   }
   __syncthreads();
   // dW1[r][c] = dh1[r] avg[c] + dh2[r] max[c]; db1[r] = dh1 + dh2; dpool = W1^T dh
-  for (int i = threadIdx.x; i < Cr * C; i += blockDim.x) {
-    const int r = i / C, c = i % C;
+  for (int i = tid; i < Cr * C; i += CAB_NT) {
+    const int r = i / C, c = i - r * C;
     pb[i] = dh[r] * pavg[c] + dh[Cr + r] * pmax[c];
   }
-  for (int r = threadIdx.x; r < Cr; r += blockDim.x) pb[Cr * C + r] = dh[r] + dh[Cr + r];
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  for (int r = tid; r < Cr; r += CAB_NT) pb[Cr * C + r] = dh[r] + dh[Cr + r];
+  for (int c = tid; c < C; c += CAB_NT) {
     float a0 = 0.f, a1 = 0.f;
     for (int r = 0; r < Cr; ++r) {
       a0 += w1[(int64_t)r * C + c] * dh[r];
@@ -148,11 +161,27 @@ __global__ __launch_bounds__(256) void channel_attention_bwd_kernel(
   }
   __syncthreads();
   float* db_ = dx + (int64_t)b * C * T;
-  for (int64_t i = threadIdx.x; i < (int64_t)C * T; i += blockDim.x) {
-    const int c = (int)(i / T), t = (int)(i % T);
-    float v = gb[i] * att[c] + dpool[c];
-    if (t == amax[c]) v += dpool[C + c];
-    db_[i] = v;
+  if ((T & 3) == 0) {   // float4 runs along t (rows start 16-byte aligned: C*T and T multiples of 4)
+    const int n4 = C * T / 4;
+    for (int i = tid; i < n4; i += CAB_NT) {
+      const int c = (4 * i) / T, t = 4 * i - c * T;
+      const float4 g = *reinterpret_cast<const float4*>(gb + 4 * (int64_t)i);
+      const float at = att[c], dp = dpool[c], dm = dpool[C + c];
+      const int am = amax[c] - t;
+      float4 v;
+      v.x = g.x * at + dp + (am == 0 ? dm : 0.f);
+      v.y = g.y * at + dp + (am == 1 ? dm : 0.f);
+      v.z = g.z * at + dp + (am == 2 ? dm : 0.f);
+      v.w = g.w * at + dp + (am == 3 ? dm : 0.f);
+      *reinterpret_cast<float4*>(db_ + 4 * (int64_t)i) = v;
+    }
+  } else {
+    for (int i = tid; i < C * T; i += CAB_NT) {
+      const int c = i / T, t = i - c * T;
+      float v = gb[i] * att[c] + dpool[c];
+      if (t == amax[c]) v += dpool[C + c];
+      db_[i] = v;
+    }
   }
 }
 
@@ -291,7 +320,10 @@ int a2m_channel_attention_bwd_f32(const float* dy, const float* x, int32_t B, in
   A2M_CHECK_ARG(lds <= 64 * 1024, "channel_attention_bwd: C too large");
   hipStream_t st = as_stream(stream);
   float* part = static_cast<float*>(ws);
-  hipLaunchKernelGGL(channel_attention_bwd_kernel, dim3(B), dim3(256), lds, st, dy, x, C, T, w1, b1, Cr,
+  A2M_CHECK_ARG((int64_t)C * T < (1LL << 31) && (T % 4 != 0 || ((reinterpret_cast<uintptr_t>(dy) |
+                                                                    reinterpret_cast<uintptr_t>(dx)) & 15) == 0),
+                "channel_attention_bwd: too large, or dy / dx not 16-byte aligned");
+  hipLaunchKernelGGL(channel_attention_bwd_kernel, dim3(B), dim3(CAB_NT), lds, st, dy, x, C, T, w1, b1, Cr,
                      w2, b2, dx, part);
   A2M_LAUNCH_CHECK();
   ColOuts outs{};

@@ -111,17 +111,19 @@ def test_self_attention_train(C, T, res):
     _check_grads(pairs)
 
 
-def test_channel_attention_train():
+@pytest.mark.parametrize('B,C,T', [(3, 64, 20), (3, 256, 64), (2, 128, 33)])
+def test_channel_attention_train(B, C, T):
+    """T = 64: the backward's float4 path; T = 20 / 33: its element path."""
     from a2m.model_layers import ChannelAttention
     from oracle import model as OM
     torch.manual_seed(2)
-    m = ChannelAttention(64)
+    m = ChannelAttention(C)
     sd = {'c.' + k: v.clone().requires_grad_(True) for k, v in m.state_dict().items()}
     m.to(DEV).train()
-    xd, xc = _leaf(_r(3, 64, 20, seed=8))
+    xd, xc = _leaf(_r(B, C, T, seed=8))
     yd, yc = m(xd), OM.channel_attention(OM.Ctx(sd), 'c', xc)
     assert rel_err(yd.detach().cpu(), yc.detach()) < TOL
-    gy = _r(3, 64, 20, seed=9)
+    gy = _r(B, C, T, seed=9)
     yd.backward(gy.to(DEV))
     yc.backward(gy)
     _check_grads({'x': (xd.grad, xc.grad), 'w1': (m.fc[0].weight.grad, sd['c.fc.0.weight'].grad),
