@@ -1074,20 +1074,19 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
   if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3(KS == 1 ? 256 : 512), 0, st, a); return; }
+  // (else-chained, so a wave-group variant instantiates only the mode pairs it serves)
   if constexpr (KS == 2) {  // dense (or channels-last conv, mode 6) operands only (gemm.hip)
     A2M_L(0, 0) A2M_L(0, 6)
-    return;
-  }
-  if constexpr (KS == 3) {  // dense / gathered weights x tap-chunked conv1d operands (gemm.hip)
+  } else if constexpr (KS == 3) {  // dense / gathered weights x tap-chunked conv1d operands (gemm.hip)
     A2M_L(0, 5) A2M_L(0, 3) A2M_L(0, 0)
-    return;
+  } else {
+    A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3) A2M_L(0, 4)
+    A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2) A2M_L(1, 3) A2M_L(1, 4)
+    A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3) A2M_L(2, 4)
+    A2M_L(3, 0) A2M_L(3, 1) A2M_L(3, 2) A2M_L(3, 3) A2M_L(3, 4)
+    A2M_L(4, 0) A2M_L(4, 1) A2M_L(4, 2) A2M_L(4, 3) A2M_L(4, 4)
+    A2M_L(0, 5) A2M_L(0, 6)
   }
-  A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3) A2M_L(0, 4)
-  A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2) A2M_L(1, 3) A2M_L(1, 4)
-  A2M_L(2, 0) A2M_L(2, 1) A2M_L(2, 2) A2M_L(2, 3) A2M_L(2, 4)
-  A2M_L(3, 0) A2M_L(3, 1) A2M_L(3, 2) A2M_L(3, 3) A2M_L(3, 4)
-  A2M_L(4, 0) A2M_L(4, 1) A2M_L(4, 2) A2M_L(4, 3) A2M_L(4, 4)
-  A2M_L(0, 5) A2M_L(0, 6)
 #undef A2M_L
 }
 
