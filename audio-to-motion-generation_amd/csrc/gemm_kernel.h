@@ -40,6 +40,7 @@ struct GemmArgs {
   int xcd_group;   // >0: XCD-aware block remap with this many M-tiles per group; 0: identity
   int mcontig;     // output has unit m stride: the tile is staged through LDS and written
                    // along m (split-K slabs then are [N][M])
+  int skew;        // KS = 3: wave group 1 runs its k-steps half a step after group 0's
 };
 
 struct RowInfo {
@@ -188,6 +189,12 @@ struct TileLoader {
   int tt;        // t of this thread's first row within its clip
   int64_t rb;    // element offset of (b, t) of that row
   int st_j;      // k-tile index of the next store (its tap)
+  int st_tap, ld_tap, ld_cc;   // tap of the next store; tap / channel chunk of the next load
+  // fp32, up to 3 taps: each tap's LDS offsets of this thread's 4 rows and their data bits
+  // (row5 evaluated once here instead of per element and k-tile)
+  static constexpr int T5 = 3;
+  int o5[MODE == 5 && !H ? T5 : 1][4];
+  int ok5;
   KPos kp[NKP];   // k position of each of this thread's k groups at the next load (modes 1-3)
   KPos kstep;     // BK in (k0, k1, k2) digits
   float r[NREG];
@@ -209,6 +216,19 @@ struct TileLoader {
       tt = n - b * gg.R2;
       rb = nrow > 0 ? (int64_t)b * gg.sr0 + tt : 0;
       st_j = kbeg / BK;
+      st_tap = ld_tap = st_j % gg.tapconv;
+      ld_cc = st_j / gg.tapconv;
+      if constexpr (!H) {
+        ok5 = 0;
+#pragma unroll
+        for (int t = 0; t < T5; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bool ok;
+            o5[t][e] = row5(e, t + gg.cw, ok) * LDK + kq;
+            ok5 |= (ok ? 1 : 0) << (t * 4 + e);
+          }
+      }
       return;
     }
     if (MODE == 3) {
@@ -247,8 +267,12 @@ struct TileLoader {
 
   __device__ __forceinline__ void load(int k0) {
     if (MODE == 5) {
-      const int j = k0 / BK, cc = j / g->tapconv;
-      if (j - cc * g->tapconv != 0) return;   // taps 1.. re-store the registers of tap 0
+      // loads come in k-tile order (k0 = kbeg, kbeg + BK, ...): tap / chunk kept as counters
+      const int cc = ld_cc;
+      const bool first = ld_tap == 0;
+      if (++ld_tap == g->tapconv) { ld_tap = 0; ++ld_cc; }
+      if (!first) return;   // taps 1.. re-store the registers of tap 0
+      (void)k0;
 #pragma unroll
       for (int p = 0; p < NKE; ++p) {
         const float* src = base + rb + (int64_t)(cc * BK + kq + eofs(p)) * g->sk0;
@@ -390,8 +414,24 @@ struct TileLoader {
 
   __device__ __forceinline__ void store(float* lds) {
     if constexpr (MODE == 5) {
-      const int tap = st_j % g->tapconv;
+      const int tap = st_tap;
+      if (++st_tap == g->tapconv) st_tap = 0;
       ++st_j;
+      if constexpr (!H) {
+        if (g->tapconv <= T5) {   // precomputed offsets (tap is uniform: one branch per tile)
+          auto put = [&](const int (&o)[4], int sh) {
+#pragma unroll
+            for (int p = 0; p < NP3; ++p)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                lds[o[e] + p * KPP] = ((ok5 >> (sh + e)) & 1) ? r[p * 4 + e] : 0.f;
+          };
+          if (tap == 0) put(o5[0], 0);
+          else if (tap == 1) put(o5[T5 > 1 ? 1 : 0], 4);
+          else put(o5[T5 > 2 ? 2 : 0], 8);
+          return;
+        }
+      }
       const int s = tap + g->cw;   // cw = -pad
       if constexpr (H) {
 #pragma unroll
@@ -870,6 +910,35 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
     }
     __syncthreads();
     if (nk > 0) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
+    if (KS == 3 && grp == 1 && args.skew) {
+      // Group 1 issues both halves' MFMAs before the (shared) barrier and the next tile's first
+      // fragment reads after it, so between two barriers its staging comes first and its MFMAs
+      // last, while group 0's second-half MFMAs come first: the two groups' MFMA phases are
+      // offset instead of meeting at every barrier.  Hazards as for group 0: the barrier follows
+      // all of this wave's tile stores (lgkmcnt 0), and a stage is overwritten only after the
+      // barrier that follows its last fragment reads.
+      for (int i = 0; i < nk; ++i) {
+        const float* cur = lds + (i & 1) * STAGE;
+        float* nxt = lds + ((i + 1) & 1) * STAGE;
+        if (i + 1 < nk) {
+          la.store(nxt);
+          lb.store(nxt + LA::TILE);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (i + 2 < nk) {
+          la.load(kbeg + (i + 2) * BK);
+          lb.load(kbeg + (i + 2) * BK);
+        }
+        read_frags<BM, BN, TM, TN, P, NS, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
+        mfma_half(f0, acc);
+        mfma_half(f1, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
+      }
+    } else
     for (int i = 0; i < nk; ++i) {
       const float* cur = lds + (i & 1) * STAGE;
       float* nxt = lds + ((i + 1) & 1) * STAGE;
