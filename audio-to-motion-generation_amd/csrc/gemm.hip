@@ -396,7 +396,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   a.kchunk = p.kchunk;
   a.partial = nullptr;
   a.xcd_group = gemm_xcd_group();
-  static const int skew = env_int("A2M_GEMM_KS3_SKEW", 0);
+  static const int skew = env_int("A2M_GEMM_KS3_SKEW", 1);
   a.skew = skew;
   static const int stage_m = env_int("A2M_GEMM_MCONTIG", 1);
   a.mcontig = stage_m && E.som == 1 && M > 1;
