@@ -22,9 +22,6 @@ constexpr int GF = 64;          // joint feature dim
 #ifndef STACK_PINGPONG
 #define STACK_PINGPONG 0
 #endif
-#ifndef STACK_HOIST
-#define STACK_HOIST 1
-#endif
 #ifndef STACK_WG_PER_CU
 #define STACK_WG_PER_CU 3
 #endif
@@ -419,10 +416,6 @@ __device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)
   for (int st = 0; st < 8; ++st) {
     float4 bc[GHEADS][2];
     load_b(st, bc);
-    // keep the step's weight-fragment loads ahead of its gathers: left alone, the scheduler
-    // sinks each load next to its MFMA (recycling the gather registers), exposing the full
-    // L2 round trip at every MFMA
-    if (STACK_HOIST) __builtin_amdgcn_sched_barrier(0);
     step(st, bc);
   }
 #endif
