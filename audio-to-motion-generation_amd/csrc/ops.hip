@@ -879,7 +879,7 @@ __global__ __launch_bounds__(256) void conv2d_c1_kernel(
     const float* __restrict__ bn_b, const float* __restrict__ bn_rm, const float* __restrict__ bn_rv,
     float bn_eps, int act, float slope, float* __restrict__ y, int y_nhwc, int Hout, int Wout, int w_lo, int w_hi) {
   constexpr int kh = C1_K, kw = C1_K;
-  __shared__ float rows[C1_IN_ROWS][C1_MAXW];
+  __shared__ __attribute__((aligned(16))) float rows[C1_IN_ROWS][C1_MAXW];
   const int rb = (Hout + C1_ROWS - 1) / C1_ROWS;
   const int b = blockIdx.x / rb, ho0 = (blockIdx.x % rb) * C1_ROWS;
   const int nr = min(C1_ROWS, Hout - ho0);
@@ -956,13 +956,26 @@ __global__ __launch_bounds__(256) void conv2d_c1_kernel(
     for (int wo = w_lo + wsub; wo < w_hi; wo += wpp) {
       const int cb = (wo - w_lo) * stride;
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      if (stride == 2) {   // cb even: each kernel row's 4 inputs as two 8-byte LDS reads
 #pragma unroll
-      for (int i = 0; i < kh; ++i) {
+        for (int i = 0; i < kh; ++i) {
+          const float2 p0 = *reinterpret_cast<const float2*>(&rows[r * 2 + i][cb]);
+          const float2 p1 = *reinterpret_cast<const float2*>(&rows[r * 2 + i][cb + 2]);
+          const float xr[4] = {p0.x, p0.y, p1.x, p1.y};
 #pragma unroll
-        for (int j = 0; j < kw; ++j) {
-          const float xv = rows[r * stride + i][cb + j];
+          for (int j = 0; j < kw; ++j)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) acc[c] = fmaf(wt[c][i * kw + j], xv, acc[c]);
+            for (int c = 0; c < 4; ++c) acc[c] = fmaf(wt[c][i * kw + j], xr[j], acc[c]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kh; ++i) {
+#pragma unroll
+          for (int j = 0; j < kw; ++j) {
+            const float xv = rows[r * stride + i][cb + j];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = fmaf(wt[c][i * kw + j], xv, acc[c]);
+          }
         }
       }
       float o[4];
