@@ -83,7 +83,7 @@ def test_convt_bn_relu_train():
                   'b': (m.bn.weight.grad, ref[1].weight.grad)})
 
 
-@pytest.mark.parametrize('C,T,res', [(64, 16, False), (256, 64, True), (16, 5, True), (2048, 16, True), (2048, 4, False)])
+@pytest.mark.parametrize('C,T,res', [(64, 16, False), (256, 64, True), (256, 64, False), (16, 5, True), (2048, 16, True), (2048, 4, False)])
 def test_self_attention_train(C, T, res):
     from a2m.model_layers import SelfAttention
     from oracle import model as OM
