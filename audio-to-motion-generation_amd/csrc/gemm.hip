@@ -376,13 +376,14 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     p.splits = (int)cdiv(K, p.kchunk);
   }
   if (K == 0) { p.splits = 1; p.kchunk = p.bk; }
-  // few-block launches (one 64x64 block per CU or less) with a tap-chunked or row-gathered B
-  // split the k range across the block's two wave groups (KS = 3): each SIMD runs two
-  // independent k pipelines.  A2M_GEMM_KS3=2 also turns the planner's two-way split-K plans on
-  // such launches into KS = 3 (no partial-sum round trip or reduce launch); measured slower on
-  // every such launch of the bench step (the groups share every barrier; two independent
-  // blocks per CU do not), so off by default
-  static const int ks3 = env_int("A2M_GEMM_KS3", 1);
+  // A2M_GEMM_KS3=1: few-block launches (one 64x64 block per CU or less) with a tap-chunked or
+  // row-gathered B split the k range across the block's two wave groups (KS = 3): each SIMD
+  // runs two independent k pipelines.  Faster alone (the decoder conv 30.7 -> 28.8 us) and
+  // in the round-2 step, but off since round 3: in the two-stream step its 75 KB-LDS blocks
+  // cannot share a CU with the graph stack's workgroups, and the plain 64x64 tile measured
+  // 2.704-2.713 vs 2.717-2.724 ms (three pairs).  A2M_GEMM_KS3=2 also turns two-way split-K
+  // plans on such launches into KS = 3 (measured slower on every such launch).
+  static const int ks3 = env_int("A2M_GEMM_KS3", 0);
   static const int ks3_maxb = env_int("A2M_GEMM_KS3_MAXB", 256);
   const int64_t blocks64 = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
   const int nt_all = (int)cdiv(K, p.bk);
