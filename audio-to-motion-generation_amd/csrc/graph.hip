@@ -22,6 +22,9 @@ constexpr int GF = 64;          // joint feature dim
 #ifndef STACK_PINGPONG
 #define STACK_PINGPONG 0
 #endif
+#ifndef STACK_IGLP   // the backend's MFMA / VALU interleaving hint for the k steps (-1: none)
+#define STACK_IGLP 2
+#endif
 #ifndef STACK_WG_PER_CU
 #define STACK_WG_PER_CU 3
 #endif
@@ -375,6 +378,9 @@ __device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)
     }
   };
   auto step = [&](int st, const float4 (&bc)[GHEADS][2]) {
+#if STACK_IGLP >= 0
+    __builtin_amdgcn_iglp_opt(STACK_IGLP);
+#endif
     const int off = (st >> 1) * 16 + lh * 8 + (st & 1) * 4;
     f2 a01[NS], a23[NS];
 #pragma unroll
