@@ -13,5 +13,5 @@ done
 done
 unset A2M_LIB
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/trainprof4 -o run -- python bench.py --mode train --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/trainprof4.log 2>&1 || { tail -5 gpurun_out/trainprof4.log; exit 4; }
-python tools/prof_summary.py gpurun_out/trainprof4/run_kernel_trace.csv 6 > gpurun_out/r03_train_breakdown_v4.txt
-head -8 gpurun_out/r03_train_breakdown_v4.txt
+python tools/prof_summary.py gpurun_out/trainprof4/run_kernel_trace.csv 6 > gpurun_out/r03_train_breakdown_v5.txt
+head -8 gpurun_out/r03_train_breakdown_v5.txt
