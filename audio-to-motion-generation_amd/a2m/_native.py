@@ -43,6 +43,9 @@ SIGNATURES = {
     'a2m_conv2d_nhwc_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32,
                                                I32, P, P, P, P, F32, I32, F32, P, I32, I32, I32,
                                                I32, I32, P, SZ, P]),
+    'a2m_conv2d_nhwc_interp_fwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32,
+                                                      I32, P, P, P, P, F32, I32, F32, P, I32, I32, I32,
+                                                      I32, P, SZ, P]),
     'a2m_graph_att_proj_f32': (ctypes.c_int, [P, P, P, P, P]),
     'a2m_graph_stack_fwd_f32': (ctypes.c_int, [P, I32, I32, P, P, I32, P, P, P, P, P, P, P, F32,
                                                P, P]),

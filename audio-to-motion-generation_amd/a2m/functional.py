@@ -288,6 +288,26 @@ def conv2d_nhwc(x, w, b=None, stride=1, pad=(0, 0), bn=None, act=ACT_NONE, slope
     return out
 
 
+def conv2d_nhwc_interp(x, w, b, stride, pad, T, col, bn=None, act=ACT_NONE, slope=0.2, cache=None, out=None):
+    """The encoder's last conv restricted to its one live output column `col`, with the
+    bilinear time resample to T fused into the GEMM's reduce: [B, Co, T], equal bit for bit to
+    interp_time(conv2d_nhwc(..., cols=(col, col + 1), out_nhwc=False), T)."""
+    _check_dev(x, w, b, out)
+    assert x.is_contiguous() and w.is_contiguous()
+    B, H, W, Ci = x.shape
+    Co, _, kh, kw = w.shape
+    ph, pw = pad
+    Ho, Wo = (H + 2 * ph - kh) // stride + 1, (W + 2 * pw - kw) // stride + 1
+    packed = conv2d_nhwc_packed(w, cache)
+    if out is None:
+        out = torch.empty(B, Co, T, device=x.device, dtype=x.dtype)
+    assert out.is_contiguous() and tuple(out.shape) == (B, Co, T)
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_conv2d_nhwc_interp_fwd_f32(
+        _p(x), B, Ci, H, W, _p(packed), _p(b), Co, kh, kw, stride, ph, pw, *_bn_args(bn), act,
+        slope, _p(out), T, Ho, Wo, col, wp, wn, _stream()))
+    return out
+
+
 def interp_time(x, T, out=None):
     _check_dev(x)
     assert x.is_contiguous()

@@ -195,6 +195,9 @@ class ConvTranspose1D(nn.Module):
 
 _ENC_NHWC = __import__('os').environ.get('A2M_ENC_NHWC', '1') != '0'
 _ENC_NHWC_ALL = __import__('os').environ.get('A2M_ENC_NHWC_ALL', '1') != '0'
+# the last conv + time resample as one GEMM whose reduce writes the resampled output
+# (a2m_conv2d_nhwc_interp_fwd_f32); A2M_ENC_FUSED_INTERP=0 restores conv + interp_time
+_ENC_FUSED_INTERP = __import__('os').environ.get('A2M_ENC_FUSED_INTERP', '1') != '0'
 
 
 class AudioEncoder(nn.Module):
@@ -246,6 +249,12 @@ class AudioEncoder(nn.Module):
         # the mel [B, T, F] is NHWC with C = 1 and NCHW with the channel unsqueezed, for free
         h = x.unsqueeze(-1 if nhwc[0] else 1)
         for i, (layer, c) in enumerate(zip(self.conv, cols)):
+            if nhwc[i] and i + 1 == len(self.conv) and _ENC_FUSED_INTERP and self._single_live_column(h, c):
+                # the last conv's one live column straight into the resampled [B, C, T] output
+                k, s, p = layer.geometry()
+                return F.conv2d_nhwc_interp(h, layer.conv.weight, layer.conv.bias, s, tuple(p), time_steps,
+                                            c[0], bn=layer.bn_eval(), act=layer.act, cache=layer._nhwc,
+                                            out=out)
             if nhwc[i]:
                 k, s, p = layer.geometry()
                 out_nhwc = i + 1 < len(self.conv) and nhwc[i + 1]
@@ -255,6 +264,14 @@ class AudioEncoder(nn.Module):
             else:
                 h = layer(h, cols=c)
         return F.interp_time(h, time_steps, out=out)
+
+    def _single_live_column(self, h, c):
+        """The last layer's live columns c are one column the resample reads with weight 1
+        (its source position Wout/2 - 1/2 is that integer column): the fused path's condition."""
+        k, s, p = self.conv[-1].geometry()
+        Wo = (h.shape[2] + 2 * p[1] - k[1]) // s + 1
+        src = max(Wo * 0.5 - 0.5, 0.0)
+        return c[1] - c[0] == 1 and src == c[0]
 
     def _nhwc_layer(self, i):
         """Channels-last for every layer the GEMM engine can read as contiguous channel runs:

@@ -103,6 +103,11 @@ struct Epilogue {
   const float* res1; const float* res2;
   int accumulate;  // 1: out += v
   int pstride;     // grouped launches: bias / BN arrays of problem z start at z * pstride
+  // > 0: the AudioEncoder's last conv with its bilinear time resample fused into the split-K
+  // reduce (gemm.hip splitk_reduce_interp_kernel): C[m][n], n = b * interp_H + h, is one live
+  // output column of weight interp_lw0, and out is y[b][m][t] with t < interp_T
+  int interp_T, interp_H;
+  float interp_lw0;
 };
 
 inline Epilogue epi_dense(float* out, int ldn, int64_t bstride = 0) {  // out[m][n], ld = ldn

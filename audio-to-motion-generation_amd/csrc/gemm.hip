@@ -181,6 +181,61 @@ __global__ __launch_bounds__(RW_LANES * RW_COLS) void splitk_reduce_wide_kernel(
   reduce_store4(args, z, v, o, in);
 }
 
+// The AudioEncoder's last conv (one live output column, model_layers.py:272) with the
+// bilinear time resample (model_layers.py:277-279) fused into its split-K reduce: phase 1 sums
+// the slabs of RB whole (m, b) rows of H values in fixed order s = 0, 1, ... (the order of
+// splitk_reduce_kernel, or splitk_reduce_wide_kernel's where the unfused path would use that
+// kernel) and applies the epilogue into LDS; phase 2 writes those rows' T
+// outputs y[b][m][t] from the LDS rows with exactly interp_time_at's operations (ops.hip), so
+// the result is the unfused conv + interp_time_kernel's bit for bit, without the [B][Co][H][W]
+// round trip and the second launch.  Slabs are [M][N], n = b * H + h (rows (m, b) contiguous).
+__global__ __launch_bounds__(256) void splitk_reduce_interp_kernel(GemmArgs args, int nb, int RB, int wide) {
+  extern __shared__ float sv[];   // [RB][H]
+  const Epilogue& E = args.E;
+  const int H = E.interp_H, T = E.interp_T, M = args.M, S = args.splits;
+  const int64_t MN = (int64_t)M * args.N;
+  const int rows = M * nb;
+  const int r0 = blockIdx.x * RB;
+  const int nr = min(RB, rows - r0);
+  for (int e = threadIdx.x; e < nr * H; e += blockDim.x) {
+    const float* p = args.partial + (int64_t)r0 * H + e;   // row r0 + e / H, h = e % H
+    float v = 0.f;
+    if (wide) {
+      // the order of splitk_reduce_wide_kernel (which the unfused path uses at these sizes):
+      // RW_LANES strided partial sums, then added in lane order
+      for (int l = 0; l < RW_LANES; ++l) {
+        float vl = 0.f;
+        for (int s = l; s < S; s += RW_LANES) vl += p[s * MN];
+        if (l == 0) v = vl;
+        else v += vl;
+      }
+    } else {
+      int s = 0;
+      for (; s + 4 <= S; s += 4) {
+        const float a0 = p[(s + 0) * MN], a1 = p[(s + 1) * MN], a2 = p[(s + 2) * MN], a3 = p[(s + 3) * MN];
+        v += a0; v += a1; v += a2; v += a3;
+      }
+      for (; s < S; ++s) v += p[s * MN];
+    }
+    const int m = (r0 + e / H) / nb;
+    sv[e] = epi_value_p(E, v, epi_row(E, m));
+  }
+  __syncthreads();
+  const float sh = (float)H / (float)T, lw0 = E.interp_lw0;
+  for (int o = threadIdx.x; o < nr * T; o += blockDim.x) {
+    const int rl = o / T, t = o - rl * T;
+    const int r = r0 + rl, m = r / nb, b = r - m * nb;
+    float src = sh * ((float)t + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+    const int h0 = (int)src;
+    const int h1 = h0 + (h0 < H - 1 ? 1 : 0);
+    const float lh1 = src - (float)h0, lh0 = 1.f - lh1;
+    float v = lh0 * (lw0 * sv[rl * H + h0]);
+    if (lh1 != 0.f) v += lh1 * (lw0 * sv[rl * H + h1]);
+    E.out[((int64_t)b * M + m) * T + t] = v;
+  }
+}
+
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v ? std::atoi(v) : dflt;
@@ -247,7 +302,7 @@ static int gemm_xcd_group() {
 static int g_override_tile = 0, g_override_split = 0;   // a2m_gemm_plan_override (tuning)
 
 static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int tile, int kchunk,
-                           int splits, int prec) {
+                           int splits, int prec, bool conv_rows = false) {
   static const double thr64[4] = {340e3, 428e3, 435e3, 440e3};   // flop / us per CU
   static const double thr128[2] = {464e3, 500e3};
   // bf16x6 (fitted to a plan sweep of the G forward's shapes, tools/sweep_summary.py): three
@@ -262,6 +317,12 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   double thr = prec == 2 ? (tile == 128 ? x6_thr128[c - 1] : x6_thr64[c - 1])
                          : (tile == 128 ? thr128[c - 1] : thr64[c - 1]);
   if (gathered && tile == 64) thr *= 0.84;
+  // channels-last conv rows (mode 6: per-row pixel offsets and padding checks in the loader):
+  // the 64x64 two-group tile measured ~13 % below the dense-operand fit on the encoder layers
+  // (tools/enc_plan_sweep.py: 512x4096x2304 64/1 109 us vs the fit's 95; the 128x128 tile
+  // with 4 splits 101.6 us, fit 104.5), so those launches move to the larger tile
+  static const double rows6 = env_int("A2M_GEMM_MODE6_THR", 87) / 100.0;
+  if (conv_rows && tile == 64 && prec == 0) thr *= rows6;
   if (prec == 1) thr *= 4.0;  // staging-bound rather than MFMA-bound (16x MFMA rate); rough
   const double block_flops = 2.0 * tile * tile * (double)kchunk;
   const double fixed = prec == 2 ? (tile == 128 ? 15.0 : 2.0)
@@ -273,7 +334,8 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   return t;
 }
 
-static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, int kquant = 1) {
+static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, int kquant = 1,
+                     bool conv_rows = false) {
   static const int env_tile = env_int("A2M_GEMM_TILE", 0);
   static const int env_split = env_int("A2M_GEMM_SPLIT", 0);
   const int force_tile = g_override_tile ? g_override_tile : env_tile;
@@ -291,7 +353,7 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, in
       const int se = (int)cdiv(std::max(K, 1), kchunk);
       if (!force_split && se > 1 && kchunk < 128) continue;
       if (se != s && s > 1 && !force_split) continue;   // the same plan at a smaller s
-      const double t = plan_cost_us(M, N, K, batch, gathered, tile, kchunk, se, prec);
+      const double t = plan_cost_us(M, N, K, batch, gathered, tile, kchunk, se, prec, conv_rows);
       if (t < best) {
         best = t;
         p.bm = tile;
@@ -313,10 +375,11 @@ size_t gemm_ws_bytes(int M, int N, int K, int batch) {
   // either precision
   size_t need = 0;
   for (bool gathered : {false, true})
-    for (int prec : {0, 1, 2}) {
-      const Plan p = plan_for(M, N, K, batch, gathered, prec);
-      if (p.splits > 1) need = std::max(need, (size_t)p.splits * batch * M * N * sizeof(float));
-    }
+    for (int prec : {0, 1, 2})
+      for (bool rows6 : {false, true}) {
+        const Plan p = plan_for(M, N, K, batch, gathered, prec, 1, rows6);
+        if (p.splits > 1) need = std::max(need, (size_t)p.splits * batch * M * N * sizeof(float));
+      }
   return need;
 }
 
@@ -370,7 +433,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   const int kquant = mb == 5 ? B.tapconv : 1;
   // gathered: row-vector staging (modes 2 / 3) or gathers; k-contiguous conv rows (mode 6) load
   // like dense rows
-  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || (mb >= 3 && mb != 6), prec, kquant);
+  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || (mb >= 3 && mb != 6), prec, kquant,
+                    mb == 6);
   if (force_split > 0) {
     p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk * kquant) * p.bk * kquant);
     p.splits = (int)cdiv(K, p.kchunk);
@@ -400,8 +464,14 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   static const int skew = env_int("A2M_GEMM_KS3_SKEW", 1);
   a.skew = skew;
   static const int stage_m = env_int("A2M_GEMM_MCONTIG", 1);
-  a.mcontig = stage_m && E.som == 1 && M > 1;
-  if (p.splits > 1) {
+  // fused resample (E.interp_T): the tile always writes raw slabs (also at one split) and the
+  // reduce kernel runs epilogue + resample
+  const bool interp = E.interp_T > 0;
+  A2M_CHECK_ARG(!interp || (batch == 1 && E.interp_H > 0 && N % E.interp_H == 0 &&
+                            (size_t)E.interp_H * sizeof(float) <= 32768),
+                "gemm: fused resample needs batch 1, N a multiple of H = %d <= 8192", E.interp_H);
+  a.mcontig = stage_m && E.som == 1 && M > 1 && !interp;
+  if (p.splits > 1 || interp) {
     const size_t need = (size_t)p.splits * batch * M * N * sizeof(float);
     if (ws == nullptr || ws_bytes < need) {
       set_error("gemm: workspace too small (%zu < %zu bytes)", ws_bytes, need);
@@ -437,7 +507,16 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   }
   A2M_LAUNCH_CHECK();
   if (tm >= 0) timing_mark(tm, 1, false, stream);
-  if (p.splits > 1) {
+  if (interp) {
+    const int H = E.interp_H, nb = N / H;
+    // whole (m, b) rows per block: ~2,048 outputs, the rows' H values staged in LDS
+    const int RB = std::max(1, std::min(2048 / std::max(E.interp_T, 1), 8192 / H));
+    static const int wide_on = env_int("A2M_GEMM_WIDE_REDUCE", 1);
+    const int wide = wide_on && (N & 3) == 0 && p.splits >= 2 * RW_LANES && (int64_t)M * N / 4 <= 65536;
+    hipLaunchKernelGGL(splitk_reduce_interp_kernel, dim3((unsigned)cdiv((int64_t)M * nb, RB)), dim3(256),
+                       (size_t)RB * H * sizeof(float), stream, a, nb, RB, wide);
+    A2M_LAUNCH_CHECK();
+  } else if (p.splits > 1) {
     const int inner = a.mcontig ? M : N;
     const int64_t total = (int64_t)M * N * batch / ((inner & 3) == 0 ? 4 : 1);
     static const int wide_on = env_int("A2M_GEMM_WIDE_REDUCE", 1);
@@ -450,7 +529,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     }
     A2M_LAUNCH_CHECK();
   }
-  if (tm >= 0) timing_mark(tm, 2, p.splits > 1, stream);
+  if (tm >= 0) timing_mark(tm, 2, p.splits > 1 || interp, stream);
   return A2M_OK;
 }
 

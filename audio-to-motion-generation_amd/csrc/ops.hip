@@ -440,6 +440,31 @@ __global__ __launch_bounds__(256) void bct_to_btc_kernel(const float* __restrict
   }
 }
 
+// The GEMM of a channels-last conv2d over output columns [w_lo, w_lo + Wn) with epilogue E.
+static int conv2d_nhwc_gemm(const float* x, int B, int Ci, int H, int W, const float* packed, int Co,
+                            int kh, int kw, int stride, int pad_h, int pad_w, int Hout, int w_lo, int Wn,
+                            const Epilogue& E, void* ws, size_t ws_bytes, hipStream_t st) {
+  Gather A = dense_rk(packed, Ci * kh * kw);
+  if (Ci % gemm_k_tile() == 0) {
+    // every k-tile is one tap's slice of Ci channels: channels-last conv rows (loader mode 6)
+    Gather Bc{};
+    Bc.base = x; Bc.sr0 = H * W * Ci; Bc.R1 = Hout; Bc.R2 = Wn; Bc.ar1 = stride; Bc.ar2 = stride;
+    Bc.ch = -pad_h; Bc.cw = w_lo * stride - pad_w; Bc.Lh = H; Bc.Lw = W; Bc.K1 = kh; Bc.K2 = kw;
+    Bc.divh = Bc.divw = 1; Bc.nhwc = Ci; Bc.kcontig = 1;
+    return gemm(A, Bc, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, st);
+  }
+  // rows n = (b, ho, wo - w_lo), k = (i, j, ci): the input element x[b][ho*s - ph + i]
+  // [(w_lo + wo)*s - pw + j][ci] sits at w' = win * Ci + ci along the fused (w, c) axis, so the
+  // inner k digit (j, ci) is a unit-stride run of kw * Ci floats (loader mode 4, float4 loads)
+  Gather Bg{};
+  Bg.base = x; Bg.bstride = 0; Bg.sr0 = H * W * Ci;
+  Bg.R1 = Hout; Bg.R2 = Wn; Bg.ar1 = stride; Bg.ar2 = stride * Ci;
+  Bg.sk0 = 0; Bg.K1 = kh; Bg.K2 = kw * Ci; Bg.bk1 = 1; Bg.bk2 = 1;
+  Bg.ch = -pad_h; Bg.cw = (w_lo * stride - pad_w) * Ci; Bg.divh = Bg.divw = 1;
+  Bg.Lh = H; Bg.Lw = W * Ci; Bg.sh = W * Ci; Bg.sw = 1; Bg.kcontig = 1;
+  return gemm(A, Bg, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, st);
+}
+
 extern "C" {
 
 int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t, int32_t B,
@@ -1027,7 +1052,7 @@ int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, in
     return A2M_OK;
   }
   const int Wn = w_hi - w_lo;
-  Epilogue E;
+  Epilogue E{};
   if (y_nhwc) {
     E = epi_bn(y + (int64_t)w_lo * Co, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
     E.N1 = Hout; E.N2 = Wn; E.so0 = Hout * Wout * Co; E.so1 = Wout * Co; E.so2 = Co; E.som = 1;
@@ -1035,25 +1060,44 @@ int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, in
     E = epi_bn(y + w_lo, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
     E.N1 = Hout; E.N2 = Wn; E.so0 = Co * Hout * Wout; E.so1 = Wout; E.so2 = 1; E.som = Hout * Wout;
   }
-  Gather A = dense_rk(packed, Ci * kh * kw);
-  if (Ci % gemm_k_tile() == 0) {
-    // every k-tile is one tap's slice of Ci channels: channels-last conv rows (loader mode 6)
-    Gather Bc{};
-    Bc.base = x; Bc.sr0 = H * W * Ci; Bc.R1 = Hout; Bc.R2 = Wn; Bc.ar1 = stride; Bc.ar2 = stride;
-    Bc.ch = -pad_h; Bc.cw = w_lo * stride - pad_w; Bc.Lh = H; Bc.Lw = W; Bc.K1 = kh; Bc.K2 = kw;
-    Bc.divh = Bc.divw = 1; Bc.nhwc = Ci; Bc.kcontig = 1;
-    return gemm(A, Bc, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, as_stream(stream));
-  }
-  // rows n = (b, ho, wo - w_lo), k = (i, j, ci): the input element x[b][ho*s - ph + i]
-  // [(w_lo + wo)*s - pw + j][ci] sits at w' = win * Ci + ci along the fused (w, c) axis, so the
-  // inner k digit (j, ci) is a unit-stride run of kw * Ci floats (loader mode 4, float4 loads)
-  Gather Bg{};
-  Bg.base = x; Bg.bstride = 0; Bg.sr0 = H * W * Ci;
-  Bg.R1 = Hout; Bg.R2 = Wn; Bg.ar1 = stride; Bg.ar2 = stride * Ci;
-  Bg.sk0 = 0; Bg.K1 = kh; Bg.K2 = kw * Ci; Bg.bk1 = 1; Bg.bk2 = 1;
-  Bg.ch = -pad_h; Bg.cw = (w_lo * stride - pad_w) * Ci; Bg.divh = Bg.divw = 1;
-  Bg.Lh = H; Bg.Lw = W * Ci; Bg.sh = W * Ci; Bg.sw = 1; Bg.kcontig = 1;
-  return gemm(A, Bg, E, Co, B * Hout * Wn, Ci * kh * kw, 1, ws, ws_bytes, as_stream(stream));
+  return conv2d_nhwc_gemm(x, B, Ci, H, W, packed, Co, kh, kw, stride, pad_h, pad_w, Hout, w_lo, Wn, E,
+                          ws, ws_bytes, as_stream(stream));
+}
+
+// The encoder's last ConvNormRelu (one live output column w_col) with the bilinear time
+// resample fused into the GEMM's reduce (gemm.hip splitk_reduce_interp_kernel): y [B][Co][T] is
+// a2m_conv2d_nhwc_fwd_f32 (y_nhwc = 0, columns [w_col, w_col + 1)) followed by
+// a2m_interp_time_f32, bit for bit, in one GEMM launch and one reduce launch.
+int a2m_conv2d_nhwc_interp_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
+                                   const float* packed, const float* bias, int32_t Co, int32_t kh,
+                                   int32_t kw, int32_t stride, int32_t pad_h, int32_t pad_w,
+                                   const float* bn_w, const float* bn_b, const float* bn_rm,
+                                   const float* bn_rv, float bn_eps, int32_t act, float slope,
+                                   float* y, int32_t T, int32_t Hout, int32_t Wout, int32_t w_col,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(x && packed && y, "conv2d_nhwc_interp: null pointer");
+  A2M_CHECK_ARG(B > 0 && Ci > 0 && Co > 0 && kh > 0 && kw > 0 && stride > 0 && T > 0,
+                "conv2d_nhwc_interp: bad shape");
+  A2M_CHECK_ARG(Hout == (H + 2 * pad_h - kh) / stride + 1 && Wout == (W + 2 * pad_w - kw) / stride + 1,
+                "conv2d_nhwc_interp: output geometry mismatch");
+  A2M_CHECK_ARG((kw * Ci) % 4 == 0 && (reinterpret_cast<uintptr_t>(x) % 4) == 0,
+                "conv2d_nhwc_interp: kw * Ci = %d must be a multiple of 4", kw * Ci);
+  A2M_CHECK_ARG(fits32((int64_t)B * Ci * H * W) && fits32((int64_t)B * Co * T) && fits32((int64_t)B * Co * Hout),
+                "conv2d_nhwc_interp: too large");
+  // the resample's column weights (interp_time_kernel): w_col must be its only live column
+  float srcw = (float)Wout * 0.5f - 0.5f;
+  srcw = srcw < 0.f ? 0.f : srcw;
+  const int w0 = (int)srcw;
+  const float lw1 = srcw - (float)w0;
+  A2M_CHECK_ARG(w0 == w_col && lw1 == 0.f,
+                "conv2d_nhwc_interp: column %d is not the resample's only live column (Wout %d)", w_col, Wout);
+  Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
+  E.N1 = Hout; E.N2 = 1; E.so0 = 0; E.so1 = 0; E.so2 = 0; E.som = 0;
+  E.interp_T = T;
+  E.interp_H = Hout;
+  E.interp_lw0 = 1.f - lw1;
+  return conv2d_nhwc_gemm(x, B, Ci, H, W, packed, Co, kh, kw, stride, pad_h, pad_w, Hout, w_col, 1, E,
+                          ws, ws_bytes, as_stream(stream));
 }
 
 int a2m_mean_time_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,

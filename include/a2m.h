@@ -153,6 +153,20 @@ int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, in
                             const float* bn_rv, float bn_eps, int32_t act, float slope, float* y,
                             int32_t y_nhwc, int32_t Hout, int32_t Wout, int32_t w_lo, int32_t w_hi,
                             void* ws, size_t ws_bytes, void* stream);
+/* The AudioEncoder's last ConvNormRelu plus its time resample (model_layers.py:272-279): the
+ * channels-last conv of a2m_conv2d_nhwc_fwd_f32 restricted to the one output column w_col that
+ * F.interpolate(size=(T,1), mode='bilinear', align_corners=False) reads (it must be that
+ * resample's only live column: Wout/2 - 1/2 == w_col, else A2M_EINVAL), with the resample fused
+ * into the GEMM's reduce: y [B][Co][T] equals a2m_conv2d_nhwc_fwd_f32 (y_nhwc = 0) followed by
+ * a2m_interp_time_f32, bit for bit, without the intermediate tensor or the second launch.
+ * Replaces the last conv + interpolate of AudioEncoder.forward (model_layers.py:271-280). */
+int a2m_conv2d_nhwc_interp_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
+                                   const float* packed, const float* bias, int32_t Co, int32_t kh,
+                                   int32_t kw, int32_t stride, int32_t pad_h, int32_t pad_w,
+                                   const float* bn_w, const float* bn_b, const float* bn_rm,
+                                   const float* bn_rv, float bn_eps, int32_t act, float slope,
+                                   float* y, int32_t T, int32_t Hout, int32_t Wout, int32_t w_col,
+                                   void* ws, size_t ws_bytes, void* stream);
 /* AudioEncoder's Conv2d ConvNormRelu layers (model_layers.py:219-276) on contiguous
  * [B][Ci][H][W] -> [B][Co][Hout][Wout].  Only output columns [w_lo, w_hi) are computed
  * (the encoder's dead-column pruning); the rest of y is untouched. */

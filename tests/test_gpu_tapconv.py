@@ -153,3 +153,57 @@ def test_conv2d_nhwc_matches_fp64(B, Ci, Co, H, W, k, s, p, cols, out_nhwc):
     y = (y.permute(0, 3, 1, 2) if out_nhwc else y).cpu().double()
     e = rel_err(y[..., lo:hi], ref[..., lo:hi])
     assert e < TOL32, e
+
+
+@pytest.mark.parametrize('B,T,split', [(64, 64, 0), (3, 64, 1), (2, 480, 0), (1, 33, 0), (5, 100, 3)])
+def test_conv2d_nhwc_interp_equals_conv_then_interp(B, T, split):
+    """The encoder's last conv with its time resample fused into the GEMM reduce
+    (a2m_conv2d_nhwc_interp_fwd_f32) equals conv2d_nhwc (the live column, NCHW) followed by
+    interp_time bit for bit -- at the bench shape, long-form H = 60 (configs[3]), odd T, and
+    with the planner forced to one split (the tile writes a raw slab) or three."""
+    from a2m import functional as F
+    from a2m import _native as N
+    g = torch.Generator().manual_seed(B * 1000 + T)
+    H = T // 8
+    x = torch.randn(B, H, 16, 512, generator=g).to(DEV)   # conv3's NHWC output [B, H, 16, 512]
+    w = (torch.randn(256, 512, 3, 8, generator=g) / np.sqrt(512 * 24)).to(DEV)
+    b = torch.randn(256, generator=g).to(DEV)
+    bn = tuple(t.to(DEV) for t in (torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g),
+                                     torch.randn(256, generator=g) * 0.1, torch.rand(256, generator=g) + 0.5)) + (1e-5,)
+    cache = {}
+    N.check(N.lib.a2m_gemm_plan_override(64 if split else 0, split))
+    try:
+        y = F.conv2d_nhwc(x, w, b, 1, (1, 3), bn=bn, act=F.ACT_LRELU, cols=(7, 8), out_nhwc=False, cache=cache)
+        ref = F.interp_time(y, T)
+        fused = F.conv2d_nhwc_interp(x, w, b, 1, (1, 3), T, 7, bn=bn, act=F.ACT_LRELU, cache=cache)
+    finally:
+        N.check(N.lib.a2m_gemm_plan_override(0, 0))
+    torch.cuda.synchronize()
+    assert fused.shape == (B, 256, T)
+    assert torch.equal(fused, ref), (fused - ref).abs().max().item()
+
+
+def test_conv2d_nhwc_interp_rejects_non_live_column():
+    """A column the resample does not read with weight 1 is refused (A2M_EINVAL), not computed."""
+    from a2m import functional as F
+    x = torch.randn(1, 8, 16, 512, device=DEV)
+    w = torch.randn(256, 512, 3, 8, device=DEV)
+    with pytest.raises(Exception, match='live column'):
+        F.conv2d_nhwc_interp(x, w, None, 1, (1, 3), 64, 6, cache={})
+
+
+def test_encoder_eval_fused_interp_matches_golden_chain():
+    """AudioEncoder eval through the fused last layer equals the unfused chain bit for bit."""
+    import a2m.model_layers as ML
+    from a2m.real_motion_model import SelfAttention_G
+    torch.manual_seed(0)
+    enc = SelfAttention_G(p=0.0).to(DEV).eval().audio_encoder
+    x = torch.randn(4, 64, 128, device=DEV)
+    with torch.no_grad():
+        fused = enc(x)
+        ML._ENC_FUSED_INTERP = False
+        try:
+            ref = enc(x)
+        finally:
+            ML._ENC_FUSED_INTERP = True
+    assert torch.equal(fused, ref), (fused - ref).abs().max().item()
