@@ -317,11 +317,12 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   double thr = prec == 2 ? (tile == 128 ? x6_thr128[c - 1] : x6_thr64[c - 1])
                          : (tile == 128 ? thr128[c - 1] : thr64[c - 1]);
   if (gathered && tile == 64) thr *= 0.84;
-  // channels-last conv rows (mode 6: per-row pixel offsets and padding checks in the loader):
-  // the 64x64 two-group tile measured ~13 % below the dense-operand fit on the encoder layers
-  // (tools/enc_plan_sweep.py: 512x4096x2304 64/1 109 us vs the fit's 95; the 128x128 tile
-  // with 4 splits 101.6 us, fit 104.5), so those launches move to the larger tile
-  static const double rows6 = env_int("A2M_GEMM_MODE6_THR", 87) / 100.0;
+  // channels-last conv rows (mode 6) at the 64x64 tile, percent of the dense fit
+  // (A2M_GEMM_MODE6_THR).  With the two-group tile (KS = 2) these launches ran ~13 % below the
+  // fit (512x4096x2304: 64/1 109 us vs the fit's 95, tools/enc_plan_sweep.py) and 87 moved them
+  // to the 128x128 tile; on the one-group tile, the default for mode 6 since, the fit's own
+  // choices are the fastest measured (encoder 300.0 us; 87: 303.2 us; tools/enc_plan_ab.py)
+  static const double rows6 = env_int("A2M_GEMM_MODE6_THR", 100) / 100.0;
   if (conv_rows && tile == 64 && prec == 0) thr *= rows6;
   if (prec == 1) thr *= 4.0;  // staging-bound rather than MFMA-bound (16x MFMA rate); rough
   const double block_flops = 2.0 * tile * tile * (double)kchunk;
@@ -502,7 +503,9 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     else if (use_ks3) launch_tile<64, 64, 32, 0, 3>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
     // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end
-    else if (ks2 && ma == 0 && (mb == 0 || mb == 6)) launch_tile<64, 64, 32, 0, 2>(a, ma, mb, batch, stream);
+    // (A2M_GEMM_KS2=2 also for channels-last conv rows, mode 6: the encoder measured 305.8 us
+    // with it against 303.2 without, tools/enc_plan_ab.py, four interleaved rounds)
+    else if (ks2 && ma == 0 && (mb == 0 || (ks2 == 2 && mb == 6))) launch_tile<64, 64, 32, 0, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, 0>(a, ma, mb, batch, stream);
   }
   A2M_LAUNCH_CHECK();

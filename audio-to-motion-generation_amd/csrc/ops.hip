@@ -1023,6 +1023,120 @@ __global__ __launch_bounds__(256) void conv2d_c1_kernel(
   }
 }
 
+}  // extern "C"
+
+// The same layer on the matrix cores (NHWC output, Co a multiple of 32): the workgroup's
+// C1_ROWS x Wn output pixels and Co channels are (32-pixel, 32-channel) jobs of one
+// v_mfma_f32_32x32x2_f32 chain each (K = 16 taps = 8 MFMAs): the channel taps are the A operand
+// (8 registers per lane, loaded once per channel tile), the pixels' taps the B operand, read
+// from the LDS patch (lanes along pixels: stride-2 columns, the two k of a step adjacent, so a
+// wave's 64 reads cover 64 consecutive words).  The VALU kernel above spends ~1,800 VALU
+// instructions per wave on the same work (PMC, profiles/r03_conv0_pmc.txt); here the per-pixel
+// cost is 8 LDS reads and the epilogue.  Lane (li, lh) ends with pixel li and channels
+// 8 (q / 4) + 4 lh + q % 4, so each lane stores four float4 channel runs of its pixel.
+typedef float c1x16 __attribute__((ext_vector_type(16)));
+constexpr int C1_MAXCO = 1024;
+__global__ __launch_bounds__(256) void conv2d_c1_mfma_kernel(
+    const float* __restrict__ x, int H, int W, const float* __restrict__ packed, const float* __restrict__ bias,
+    int Co, int stride, int ph, int pw, const float* __restrict__ bn_w,
+    const float* __restrict__ bn_b, const float* __restrict__ bn_rm, const float* __restrict__ bn_rv,
+    float bn_eps, int act, float slope, float* __restrict__ y, int Hout, int Wout, int w_lo, int w_hi) {
+  constexpr int kh = C1_K, kw = C1_K;
+  __shared__ __attribute__((aligned(16))) float rows[C1_IN_ROWS][C1_MAXW];
+  __shared__ __attribute__((aligned(16))) float e_sh[C1_MAXCO], e_sc[C1_MAXCO], e_bo[C1_MAXCO];
+  const int rb = (Hout + C1_ROWS - 1) / C1_ROWS;
+  const int b = blockIdx.x / rb, ho0 = (blockIdx.x % rb) * C1_ROWS;
+  const int nr = min(C1_ROWS, Hout - ho0);
+  const int tid = threadIdx.x;
+  const int c0 = w_lo * stride - pw, nc = (w_hi - 1 - w_lo) * stride + kw;
+  const int nin = (nr - 1) * stride + kh;
+  constexpr int C1_PRE = 8;
+  {
+    float pv[C1_PRE];
+    bool ok[C1_PRE];
+#pragma unroll
+    for (int u = 0; u < C1_PRE; ++u) {
+      const int idx = tid + u * 256;
+      const int i = idx / nc, c = idx - (idx / nc) * nc;
+      const int hi = ho0 * stride - ph + i, wi = c0 + c;
+      ok[u] = idx < nin * nc && hi >= 0 && hi < H && wi >= 0 && wi < W;
+      pv[u] = x[ok[u] ? ((int64_t)b * H + hi) * W + wi : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < C1_PRE; ++u) {
+      const int idx = tid + u * 256;
+      if (idx < nin * nc) rows[idx / nc][idx % nc] = ok[u] ? pv[u] : 0.f;
+    }
+  }
+  for (int idx = tid + C1_PRE * 256; idx < nin * nc; idx += blockDim.x) {
+    const int i = idx / nc, c = idx % nc;
+    const int hi = ho0 * stride - ph + i, wi = c0 + c;
+    rows[i][c] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? x[((int64_t)b * H + hi) * W + wi] : 0.f;
+  }
+  // per-channel epilogue (conv2d_c1_kernel's order): (acc + (bias - rm)) * (w / sqrt(rv + eps)) + b
+  for (int co = tid; co < Co; co += blockDim.x) {
+    const float bi = bias ? bias[co] : 0.f;
+    if (bn_w) {
+      e_sh[co] = bi - bn_rm[co];
+      e_sc[co] = bn_w[co] / sqrtf(bn_rv[co] + bn_eps);
+      e_bo[co] = bn_b[co];
+    } else {
+      e_sh[co] = bi;
+      e_sc[co] = 1.f;
+      e_bo[co] = 0.f;
+    }
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, li = lane & 31, lh = lane >> 5;
+  const int Wn = w_hi - w_lo, npix = nr * Wn, npt = (npix + 31) / 32, nct = Co / 32;
+  float a[8];
+  int cur = -1;
+  for (int job = wave; job < npt * nct; job += 4) {
+    const int ct = job % nct, pt = job / nct;
+    if (ct != cur) {   // wave-uniform: this channel tile's taps, A[m = li][k = 2 s + lh]
+      const float* wp = packed + (ct * 32 + li) * (kh * kw) + lh;
+#pragma unroll
+      for (int st = 0; st < 8; ++st) a[st] = wp[2 * st];
+      cur = ct;
+    }
+    const int p = pt * 32 + li;
+    const bool valid = p < npix;
+    const int pr = valid ? p / Wn : 0, pc = valid ? p - pr * Wn : 0;
+    const float* rp = &rows[pr * stride][pc * stride];
+    c1x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const int k = 2 * st + lh;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], rp[(k / kw) * C1_MAXW + (k % kw)], acc, 0, 0, 0);
+    }
+    if (!valid) continue;
+    float* yp = y + (((int64_t)b * Hout + ho0 + pr) * Wout + w_lo + pc) * Co + ct * 32 + 4 * lh;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch0 = ct * 32 + 8 * g + 4 * lh;
+      const float4 sh4 = *reinterpret_cast<const float4*>(&e_sh[ch0]);
+      const float4 sc4 = *reinterpret_cast<const float4*>(&e_sc[ch0]);
+      const float4 bo4 = *reinterpret_cast<const float4*>(&e_bo[ch0]);
+      const float shq[4] = {sh4.x, sh4.y, sh4.z, sh4.w}, scq[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+      const float boq[4] = {bo4.x, bo4.y, bo4.z, bo4.w};
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v = (acc[4 * g + q] + shq[q]) * scq[q] + boq[q];
+        if (act == ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (act == ACT_LRELU) v = v > 0.f ? v : v * slope;
+        else if (act == ACT_SIGMOID) v = 1.f / (1.f + expf(-v));
+        o[q] = v;
+      }
+      *reinterpret_cast<float4*>(yp + 8 * g) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+extern "C" {
+
 int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t W,
                             const float* packed, const float* bias, int32_t Co, int32_t kh,
                             int32_t kw, int32_t stride, int32_t pad_h, int32_t pad_w,
@@ -1044,6 +1158,14 @@ int a2m_conv2d_nhwc_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, in
   if (Ci == 1 && kh == C1_K && kw == C1_K && stride <= 2 && Co % 4 == 0 && Co <= 1024 &&
       (w_hi - 1 - w_lo) * stride + kw <= C1_MAXW && reinterpret_cast<uintptr_t>(packed) % 16 == 0 &&
       (!y_nhwc || reinterpret_cast<uintptr_t>(y) % 16 == 0)) {
+    static const int c1_mfma = std::getenv("A2M_C1_MFMA") ? std::atoi(std::getenv("A2M_C1_MFMA")) : 1;
+    if (c1_mfma && y_nhwc && Co % 32 == 0 && Co <= C1_MAXCO) {
+      hipLaunchKernelGGL(conv2d_c1_mfma_kernel, dim3((unsigned)(B * cdiv(Hout, C1_ROWS))), dim3(256), 0,
+                         as_stream(stream), x, H, W, packed, bias, Co, stride, pad_h, pad_w, bn_w, bn_b,
+                         bn_rm, bn_rv, bn_eps, act, slope, y, Hout, Wout, w_lo, w_hi);
+      A2M_LAUNCH_CHECK();
+      return A2M_OK;
+    }
     hipLaunchKernelGGL(conv2d_c1_kernel, dim3((unsigned)(B * cdiv(Hout, C1_ROWS))), dim3(256), 0,
                        as_stream(stream), x, H, W,
                        packed, bias, Co, stride, pad_h, pad_w, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act,
