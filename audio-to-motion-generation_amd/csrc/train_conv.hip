@@ -117,11 +117,14 @@ int a2m_conv2d_wgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
   // float4 runs measured slower: the encoder's (3, 8) conv wgrad 0.91 -> 1.12 ms a call, the
   // shifted x runs being unaligned; so odd widths keep the element gathers.)
   const int Wk = Wo;
-  // A(m=co, k=(b,ho,wo)) = dY[b][co][ho][wo]   (dY contiguous)
+  // A(m=co, k=(b,ho,wo)) = dY[b][co][ho][wo]   (dY contiguous): (ho, wo) is one unit-stride
+  // digit of Ho * Wo, so the rows load as float4 runs (loader mode 4) whenever Ho * Wo % 4 == 0,
+  // also for odd Wo (the encoder's (3, 8) conv, Wo = 15) -- the same k order as X's (b, ho, wo)
+  // digits, so the same products in the same order as the element gather it replaces
   Gather A{};
   A.base = dy; A.sr0 = Ho * Wo; A.R1 = A.R2 = 1;
-  A.sk0 = Co * Ho * Wo; A.K1 = Ho; A.K2 = Wk; A.bk1 = 1; A.bk2 = 1; A.Lh = Ho; A.Lw = Wo;
-  A.sh = Wo; A.sw = 1; A.divh = A.divw = 1; A.kcontig = 1;
+  A.sk0 = Co * Ho * Wo; A.K1 = 1; A.K2 = Ho * Wk; A.bk1 = 1; A.bk2 = 1; A.Lh = 1; A.Lw = Ho * Wo;
+  A.sh = 0; A.sw = 1; A.divh = A.divw = 1; A.kcontig = 1;
   // B(n=(ci,ih,iw), k=(b,ho,wo)) = X[b][ci][ho*s + ih - ph][wo*s + iw - pw]
   Gather Bg{};
   Bg.base = x; Bg.sr0 = (int)xs_c; Bg.R1 = kh; Bg.R2 = kw; Bg.ar1 = 1; Bg.ar2 = 1;
