@@ -124,6 +124,11 @@ SIGNATURES = {
     'a2m_get_gemm_precision': (I32, []),
     'a2m_gemm_timing_end': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
                                            ctypes.POINTER(F64), ctypes.POINTER(I64)]),
+    'a2m_gemm_timing_stop': (ctypes.c_int, []),
+    'a2m_gemm_timing_read': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
+                                            ctypes.POINTER(F64), ctypes.POINTER(I64)]),
+    'a2m_timing_mark': (ctypes.c_int, [I32, ctypes.c_void_p]),
+    'a2m_timing_mark_elapsed': (ctypes.c_int, [I32, I32, ctypes.POINTER(ctypes.c_float)]),
 }
 
 A2M_EINVAL, A2M_EHIP, A2M_EWS = -1, -2, -3

@@ -907,18 +907,49 @@ def adam_(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
 class gemm_timing:
     """Context manager: HIP-event timing of every implicit-GEMM launch issued inside it
     (a2m_gemm_timing_begin/_end).  After exit: .launches, .flops, .ms_tile, .ms_reduce,
-    .reduces.  Eager code only (events are not graph-capturable)."""
+    .reduces.  With keep=True the events outlive the block: launches captured into a HIP graph
+    inside it carry event-record nodes, and read() after each replay of that graph returns the
+    latest replay's sums; release() frees them."""
+
+    def __init__(self, keep=False):
+        self.keep = keep
 
     def __enter__(self):
         N.check(N.lib.a2m_gemm_timing_begin())
         return self
 
-    def __exit__(self, *exc):
+    def _sums(self, fn):
         import ctypes
         n, r = ctypes.c_int64(), ctypes.c_int64()
         f, mt, mr = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-        N.check(N.lib.a2m_gemm_timing_end(ctypes.byref(n), ctypes.byref(f), ctypes.byref(mt),
-                                          ctypes.byref(mr), ctypes.byref(r)))
+        N.check(fn(ctypes.byref(n), ctypes.byref(f), ctypes.byref(mt), ctypes.byref(mr), ctypes.byref(r)))
         self.launches, self.flops, self.ms_tile = n.value, f.value, mt.value
         self.ms_reduce, self.reduces = mr.value, r.value
+        return self
+
+    def read(self):
+        return self._sums(N.lib.a2m_gemm_timing_read)
+
+    def release(self):
+        return self._sums(N.lib.a2m_gemm_timing_end)
+
+    def __exit__(self, *exc):
+        if self.keep:
+            N.check(N.lib.a2m_gemm_timing_stop())
+        else:
+            self.release()
         return False
+
+
+def timing_mark(slot):
+    """Store the GPU wall clock into mark `slot` from a one-thread kernel on the current stream
+    (a node of the graph when capturing; needs gemm_timing to have been entered once)."""
+    N.check(N.lib.a2m_timing_mark(int(slot), _stream()))
+
+
+def timing_mark_elapsed(a, b):
+    """ms from mark a to mark b (synchronises the device)."""
+    import ctypes
+    ms = ctypes.c_float()
+    N.check(N.lib.a2m_timing_mark_elapsed(int(a), int(b), ctypes.byref(ms)))
+    return ms.value

@@ -109,7 +109,7 @@ __device__ __forceinline__ void splitk_reduce4(const GemmArgs& args, int batch) 
   }
 }
 
-__global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
+__device__ __forceinline__ void splitk_reduce(const GemmArgs& args, int batch) {
   const int64_t MN = (int64_t)args.M * args.N;
   const int S = args.splits;
   const int inner = args.mcontig ? args.M : args.N;
@@ -133,14 +133,24 @@ __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
   }
 }
 
+// the reduce's span stamps go to slots 2, 3 of the launch's record
+__device__ __forceinline__ unsigned long long* reduce_span(const GemmArgs& args) {
+  return args.ts ? args.ts + 2 : nullptr;
+}
+
+__global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
+  span_begin(reduce_span(args));
+  splitk_reduce(args, batch);
+  span_end(reduce_span(args));
+}
+
 // Many splits over few outputs (graph-layer weight gradients: 64 x 64 outputs, K up to 172,032
 // nodes, 128-256 splits): the per-thread serial sum above would be latency-bound on a handful of
 // blocks, so here 16 lanes of a block share one float4 of outputs, each summing the splits
 // s = lane, lane + 16, ... in order, and the 16 lane sums are added in lane order (a fixed order:
 // still bitwise reproducible).  Inner extent a multiple of 4.
 constexpr int RW_LANES = 16, RW_COLS = 16;
-__global__ __launch_bounds__(RW_LANES * RW_COLS) void splitk_reduce_wide_kernel(GemmArgs args,
-                                                                               int batch) {
+__device__ __forceinline__ void splitk_reduce_wide(const GemmArgs& args, int batch) {
   __shared__ float4 red[RW_LANES][RW_COLS];
   const int64_t MN = (int64_t)args.M * args.N;
   const int S = args.splits;
@@ -181,6 +191,13 @@ __global__ __launch_bounds__(RW_LANES * RW_COLS) void splitk_reduce_wide_kernel(
   reduce_store4(args, z, v, o, in);
 }
 
+__global__ __launch_bounds__(RW_LANES * RW_COLS) void splitk_reduce_wide_kernel(GemmArgs args,
+                                                                               int batch) {
+  span_begin(reduce_span(args));
+  splitk_reduce_wide(args, batch);
+  span_end(reduce_span(args));
+}
+
 // The AudioEncoder's last conv (one live output column, model_layers.py:272) with the
 // bilinear time resample (model_layers.py:277-279) fused into its split-K reduce: phase 1 sums
 // the slabs of RB whole (m, b) rows of H values in fixed order s = 0, 1, ... (the order of
@@ -190,6 +207,7 @@ __global__ __launch_bounds__(RW_LANES * RW_COLS) void splitk_reduce_wide_kernel(
 // the result is the unfused conv + interp_time_kernel's bit for bit, without the [B][Co][H][W]
 // round trip and the second launch.  Slabs are [M][N], n = b * H + h (rows (m, b) contiguous).
 __global__ __launch_bounds__(256) void splitk_reduce_interp_kernel(GemmArgs args, int nb, int RB, int wide) {
+  span_begin(reduce_span(args));
   extern __shared__ float sv[];   // [RB][H]
   const Epilogue& E = args.E;
   const int H = E.interp_H, T = E.interp_T, M = args.M, S = args.splits;
@@ -234,6 +252,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_interp_kernel(GemmArgs args
     if (lh1 != 0.f) v += lh1 * (lw0 * sv[rl * H + h1]);
     E.out[((int64_t)b * M + m) * T + t] = v;
   }
+  span_end(reduce_span(args));
 }
 
 static int env_int(const char* name, int dflt) {
@@ -384,43 +403,68 @@ size_t gemm_ws_bytes(int M, int N, int K, int batch) {
   return need;
 }
 
-// Optional per-launch timing of the engine (bench.py's live roofline): HIP events recorded on
-// the launch stream around the tile kernel and the split-K reduce.  Off by default; not for
-// use inside graph capture.
+// Optional per-launch timing of the engine (bench.py's live roofline).  While enabled, every
+// launch gets a record of four span stamps in a device buffer (GemmArgs::ts): the tile kernel's
+// earliest block start / latest wave end and the split-K reduce's, on the GPU's constant-rate
+// wall clock (span_begin / span_end, gemm_kernel.h).  The stamps are written by the kernels
+// themselves, so they time the same launches eagerly and in every replay of a graph captured
+// while timing was on (bench.py's in-step roofline: the step captured once more, replayed, read
+// after each replay).  HIP event records were tried first: inside a graph they become
+// separate nodes whose timestamps include each kernel's dispatch (+3.5 us a launch against the
+// rocprof kernel trace, r04_v1), and hipExtLaunchKernel's kernel-timestamp events are not
+// updated under capture (tools/micro/ext_events.hip).  Off by default, no cost when off.
 struct GemmTiming {
-  hipEvent_t e0, e1, e2;
   double flops;
   bool reduce;
-  char desc[96];   // shape/plan, printed per launch by a2m_gemm_timing_end under A2M_GEMM_LOG=2
+  char desc[96];   // shape/plan, printed per launch by a2m_gemm_timing_read under A2M_GEMM_LOG=2
 };
+constexpr int kTimingRecs = 4096;   // launches per timing window
 static std::mutex g_timing_mu;
 static bool g_timing = false;
+static bool g_timing_overflow = false;
 static std::vector<GemmTiming> g_timing_recs;
+static unsigned long long* g_ts = nullptr;   // [kTimingRecs][4] + [A2M_TIMING_MARKS] mark slots
+static double g_wall_mhz = 0.0;
 
-static long timing_open(double flops, const char* desc, hipStream_t st) {
+// (re)arm the stamps: start slots at the maximum, end slots at 0
+static int timing_reset_stamps() {
+  std::vector<unsigned long long> init((size_t)kTimingRecs * 4, 0ull);
+  for (int i = 0; i < kTimingRecs; ++i) init[(size_t)i * 4] = init[(size_t)i * 4 + 2] = ~0ull;
+  return hipMemcpy(g_ts, init.data(), init.size() * sizeof(unsigned long long), hipMemcpyHostToDevice) ==
+         hipSuccess ? A2M_OK : A2M_EHIP;
+}
+
+__global__ void timing_mark_kernel(unsigned long long* p) {
+  if (threadIdx.x == 0) *p = (unsigned long long)wall_clock64();
+}
+
+static int timing_alloc() {
+  if (g_ts) return A2M_OK;
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0 ||
+      hipMalloc(&g_ts, ((size_t)kTimingRecs * 4 + A2M_TIMING_MARKS) * sizeof(unsigned long long)) != hipSuccess) {
+    set_error("gemm timing: device stamp buffer / wall clock rate unavailable");
+    g_ts = nullptr;
+    return A2M_EHIP;
+  }
+  g_wall_mhz = khz / 1e3;
+  return hipMemset(g_ts, 0, ((size_t)kTimingRecs * 4 + A2M_TIMING_MARKS) * sizeof(unsigned long long)) ==
+         hipSuccess ? A2M_OK : A2M_EHIP;
+}
+
+static unsigned long long* timing_open(double flops, const char* desc) {
   std::lock_guard<std::mutex> lk(g_timing_mu);
-  if (!g_timing) return -1;
+  if (!g_timing || !g_ts) return nullptr;
+  if ((int)g_timing_recs.size() >= kTimingRecs) {
+    g_timing_overflow = true;
+    return nullptr;
+  }
   GemmTiming t{};
   t.flops = flops;
   std::snprintf(t.desc, sizeof(t.desc), "%s", desc);
-  if (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess ||
-      hipEventCreate(&t.e2) != hipSuccess)
-    return -1;
-  (void)hipEventRecord(t.e0, st);
   g_timing_recs.push_back(t);
-  return (long)g_timing_recs.size() - 1;
-}
-
-static void timing_mark(long i, int which, bool reduce, hipStream_t st) {
-  std::lock_guard<std::mutex> lk(g_timing_mu);
-  if (i < 0 || i >= (long)g_timing_recs.size()) return;
-  GemmTiming& t = g_timing_recs[i];
-  if (which == 1) {
-    (void)hipEventRecord(t.e1, st);
-  } else {
-    t.reduce = reduce;
-    (void)hipEventRecord(t.e2, st);
-  }
+  return g_ts + 4 * (g_timing_recs.size() - 1);
 }
 
 int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int K, int batch,
@@ -484,12 +528,13 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   if (log_launches)
     std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
                  M, N, K, batch, p.bm, p.bk, p.splits, ma, mb, E.som, E.so0, E.so1, E.so2, E.N1, E.N2);
-  long tm = -1;
+  a.ts = nullptr;
   if (g_timing) {
     char desc[96];
     std::snprintf(desc, sizeof(desc), "M=%d N=%d K=%d b=%d tile=%d split=%d modes=%d,%d", M, N, K,
                   batch, p.bm, p.splits, ma, mb);
-    tm = timing_open(2.0 * M * N * (double)K * batch, desc, stream);
+    a.ts = timing_open(2.0 * M * N * (double)K * batch, desc);
+    if (a.ts) g_timing_recs.back().reduce = p.splits > 1 || interp;
   }
   if (prec == 1) {
     if (p.bm == 128) launch_tile<128, 128, 64, 1>(a, ma, mb, batch, stream);
@@ -509,7 +554,6 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     else launch_tile<64, 64, 32, 0>(a, ma, mb, batch, stream);
   }
   A2M_LAUNCH_CHECK();
-  if (tm >= 0) timing_mark(tm, 1, false, stream);
   if (interp) {
     const int H = E.interp_H, nb = N / H;
     // whole (m, b) rows per block: ~2,048 outputs, the rows' H values staged in LDS
@@ -532,7 +576,6 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     }
     A2M_LAUNCH_CHECK();
   }
-  if (tm >= 0) timing_mark(tm, 2, p.splits > 1 || interp, stream);
   return A2M_OK;
 }
 
@@ -558,25 +601,48 @@ int32_t a2m_get_gemm_precision(void) { return a2m::g_gemm_prec; }
 
 int a2m_gemm_timing_begin(void) {
   std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+  int rc = a2m::timing_alloc();
+  if (rc == A2M_OK) rc = a2m::timing_reset_stamps();
+  if (rc != A2M_OK) return rc;
   a2m::g_timing_recs.clear();
+  a2m::g_timing_overflow = false;
   a2m::g_timing = true;
   return A2M_OK;
 }
 
-int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
-                        int64_t* reduces) {
+int a2m_gemm_timing_stop(void) {
   std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
   a2m::g_timing = false;
+  return A2M_OK;
+}
+
+int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
+                         int64_t* reduces) {
+  std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+  A2M_CHECK_ARG(a2m::g_ts != nullptr, "gemm_timing_read: timing was never begun");
+  A2M_CHECK_ARG(!a2m::g_timing_overflow, "gemm_timing_read: more than %d launches in the window",
+                a2m::kTimingRecs);
+  const size_t nrec = a2m::g_timing_recs.size();
+  std::vector<unsigned long long> st(nrec * 4 + 1);
+  if (hipDeviceSynchronize() != hipSuccess ||
+      (nrec && hipMemcpy(st.data(), a2m::g_ts, nrec * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
+                   hipSuccess)) {
+    a2m::set_error("gemm timing: stamp read failed");
+    return A2M_EHIP;
+  }
   int64_t n = 0, nr = 0;
   double f = 0, mt = 0, mr = 0;
   int rc = A2M_OK;
-  for (auto& t : a2m::g_timing_recs) {
-    float a = 0.f, b = 0.f;
-    if (hipEventSynchronize(t.e2) != hipSuccess || hipEventElapsedTime(&a, t.e0, t.e1) != hipSuccess ||
-        hipEventElapsedTime(&b, t.e1, t.e2) != hipSuccess) {
-      a2m::set_error("gemm timing: event query failed");
+  const double tick_ms = 1.0 / (a2m::g_wall_mhz * 1e3);
+  for (size_t i = 0; i < nrec; ++i) {
+    const a2m::GemmTiming& t = a2m::g_timing_recs[i];
+    const unsigned long long* s = &st[i * 4];
+    if (s[1] < s[0] || (t.reduce && s[3] < s[2])) {   // a launch that did not run since the reset
+      a2m::set_error("gemm timing: launch %zu (%s) has no stamps", i, t.desc);
       rc = A2M_EHIP;
+      continue;
     }
+    const double a = (double)(s[1] - s[0]) * tick_ms, b = t.reduce ? (double)(s[3] - s[2]) * tick_ms : 0.0;
     ++n;
     f += t.flops;
     static const int log_launches = a2m::env_int("A2M_GEMM_LOG", 0);
@@ -585,17 +651,52 @@ int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, doubl
                    1e3 * a, 1e3 * b, a > 0 ? t.flops / (1e9 * a) : 0.0);
     mt += a;
     if (t.reduce) { mr += b; ++nr; }
-    (void)hipEventDestroy(t.e0);
-    (void)hipEventDestroy(t.e1);
-    (void)hipEventDestroy(t.e2);
   }
-  a2m::g_timing_recs.clear();
   if (launches) *launches = n;
   if (flops) *flops = f;
   if (ms_tile) *ms_tile = mt;
   if (ms_reduce) *ms_reduce = mr;
   if (reduces) *reduces = nr;
+  // re-arm for the next replay of a graph that carries these launches
+  if (a2m::timing_reset_stamps() != A2M_OK) {
+    a2m::set_error("gemm timing: stamp reset failed");
+    return A2M_EHIP;
+  }
   return rc;
+}
+
+int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
+                        int64_t* reduces) {
+  a2m_gemm_timing_stop();
+  const int rc = a2m_gemm_timing_read(launches, flops, ms_tile, ms_reduce, reduces);
+  std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+  a2m::g_timing_recs.clear();
+  return rc;
+}
+
+// Named wall-clock marks (bench.py's in-step phase split: step start, log-mel done, encoder
+// done): a one-thread kernel stores the clock into the mark's slot, so a mark captured into a
+// graph re-stamps on every replay.  Its own dispatch is ~1-2 us of the interval it opens.
+int a2m_timing_mark(int32_t slot, void* stream) {
+  A2M_CHECK_ARG(slot >= 0 && slot < A2M_TIMING_MARKS, "timing_mark: slot %d", slot);
+  A2M_CHECK_ARG(a2m::g_ts != nullptr, "timing_mark: call a2m_gemm_timing_begin first (stamp buffer)");
+  hipLaunchKernelGGL(a2m::timing_mark_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     a2m::g_ts + (size_t)a2m::kTimingRecs * 4 + slot);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_timing_mark_elapsed(int32_t a, int32_t b, float* ms) {
+  A2M_CHECK_ARG(a >= 0 && a < A2M_TIMING_MARKS && b >= 0 && b < A2M_TIMING_MARKS && a2m::g_ts && ms,
+                "timing_mark_elapsed: slots %d, %d", a, b);
+  unsigned long long m[A2M_TIMING_MARKS];
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(m, a2m::g_ts + (size_t)a2m::kTimingRecs * 4, sizeof(m), hipMemcpyDeviceToHost) != hipSuccess) {
+    a2m::set_error("timing_mark_elapsed: stamp read failed");
+    return A2M_EHIP;
+  }
+  *ms = (float)((double)((long long)(m[b] - m[a])) / (a2m::g_wall_mhz * 1e3));
+  return A2M_OK;
 }
 
 }  // extern "C"

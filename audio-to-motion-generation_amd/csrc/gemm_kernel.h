@@ -41,7 +41,21 @@ struct GemmArgs {
   int mcontig;     // output has unit m stride: the tile is staged through LDS and written
                    // along m (split-K slabs then are [N][M])
   int skew;        // KS = 3: wave group 1 runs its k-steps half a step after group 0's
+  unsigned long long* ts;   // measurement only (a2m_gemm_timing_*; null otherwise): this launch's
+                            // [tile first start, tile last end, reduce first start, reduce last
+                            // end] on the GPU wall clock
 };
+
+// Launch-span stamps (bench.py's in-step roofline): the earliest block start and the latest
+// wave end of a launch, from the constant-rate wall clock, by vector atomics into the launch's
+// slots.  They work identically eagerly and inside a replayed HIP graph (where event records
+// between kernels are not timestamps of the kernel: DESIGN.md 6).
+__device__ __forceinline__ void span_begin(unsigned long long* p) {
+  if (p && threadIdx.x == 0) atomicMin(p, (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void span_end(unsigned long long* p) {
+  if (p && (threadIdx.x & 63) == 0) atomicMax(p + 1, (unsigned long long)wall_clock64());
+}
 
 struct RowInfo {
   int base, h, w;
@@ -826,7 +840,7 @@ __device__ __forceinline__ void ablate_touch(const FR& f, floatx16 (&acc)[TM][TN
 // barrier waits.  The host splits the k range on whole k-tile groups (mode 5: whole channel
 // chunks, all taps).
 template <int BM, int BN, int BK, int MA, int MB, int P, int KS = 1>
-__global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs args) {
+__device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
   static_assert(P == 0 ? (BK == 32 || BK == 64) : BK == (P == 1 ? 64 : 32),
                 "the k-step pipeline assumes two halves per k-tile");
   constexpr int NS = P == 0 ? BK / 32 : 1;   // fp32: 16-k fragment chunks per half
@@ -1133,6 +1147,13 @@ __global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs 
         }
     }
   }
+}
+
+template <int BM, int BN, int BK, int MA, int MB, int P, int KS = 1>
+__global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs args) {
+  span_begin(args.ts);
+  gemm_tile<BM, BN, BK, MA, MB, P, KS>(args);
+  span_end(args.ts);
 }
 
 

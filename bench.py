@@ -7,9 +7,10 @@ replicas (inference does not shard further: "replicas only", weak scaling), laun
 process per GPU by torch.distributed.run; max-over-ranks time.
 
 Printed JSON adds `roofline` (the dominant kernel family -- the implicit-GEMM engine's
-gemm_kernel, ~70 % of step time -- every launch of one step timed with HIP events on its
-launch stream, algorithmic FLOPs 2*M*N*K per launch, against the fp32 MFMA peak; `traffic`
-from the committed PMC pass, profiles/traffic_latest.json), `mel_roofline`
+gemm_kernel, ~65 % of kernel time -- every launch of the replayed step graph timed by its own
+span stamps (first block start to last wave end on the GPU wall clock, the interval rocprof's
+kernel trace reports), algorithmic FLOPs 2*M*N*K per launch, against the fp32 MFMA peak;
+`traffic` from the committed PMC pass, profiles/traffic_latest.json), `mel_roofline`
 (log-mel kernel vs HBM peak), `path_roofline` (the whole G forward's useful FLOPs) and
 `cpu_baseline` (the torch-CPU oracle port on a bounded sample, rank 0 at N=1 only).
 """
@@ -146,11 +147,11 @@ def mel_encoder_roofline(dev, g, wave, mel_ms, mel_bytes, peak):
 
 
 def gemm_engine_timing(step):
-    """Run one eager step with every implicit-GEMM launch bracketed by HIP events on its own
-    stream (a2m_gemm_timing_*): the engine's launches/step, algorithmic FLOPs (2*M*N*K) and
-    summed tile-kernel / split-K-reduce time.  rocprof's gemm_kernel<...> rows of the same
-    command (profiles/) must agree with ms_tile / launches.  The generator's decoder branches
-    run serialised for this pass, so no launch's duration includes a concurrent one's."""
+    """Run one eager step with every implicit-GEMM launch timed by its span stamps
+    (a2m_gemm_timing_*): the engine's launches/step, algorithmic FLOPs (2*M*N*K) and summed
+    tile-kernel / split-K-reduce time.  The generator's decoder branches run serialised for this
+    pass, so no launch's duration includes a concurrent one's (`roofline.serialised_eager`: each
+    launch alone on the chip)."""
     from a2m import functional as F
     from a2m import real_motion_model as RM
     torch.cuda.synchronize()
@@ -162,6 +163,58 @@ def gemm_engine_timing(step):
     finally:
         RM._BRANCH_STREAMS = branch
     return t
+
+
+def instep_timing(dev, g, wave, reps=20):
+    """The bench step captured once more with the engine's span stamps on (every implicit-GEMM
+    launch stamps its own first-block start / last-wave end; nothing is added between kernels,
+    so the two decoder branches overlap exactly as in the timed graph) and three wall-clock
+    mark kernels (step start, after the log-mel, after the encoder); the graph is replayed
+    `reps` times and each replay read back.  Returns per-step means: the engine's launches /
+    FLOPs / tile ms / reduce ms, and the step's log-mel and log-mel + encoder phases (ms).
+    This is the basis of `roofline` and of `mel_encoder_roofline.path_frac_instep`;
+    tools/step_pmc.sh's rocprof kernel trace of the replayed bench graph is its cross-check
+    (profiles/)."""
+    from a2m import functional as F
+    from a2m.mel_features import log_mel_batch
+    hook = g.audio_encoder.register_forward_hook(lambda m, i, o: F.timing_mark(2))
+
+    def step():
+        F.timing_mark(0)
+        mel = log_mel_batch(wave)
+        F.timing_mark(1)
+        return g(mel)[0]
+    try:
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            graph = torch.cuda.CUDAGraph()
+            with F.gemm_timing(keep=True) as t:
+                with torch.cuda.graph(graph, stream=s):
+                    step()
+        torch.cuda.current_stream(dev).wait_stream(s)
+    finally:
+        hook.remove()
+    acc = {'launches': 0, 'flops': 0.0, 'ms_tile': 0.0, 'ms_reduce': 0.0, 'mel_ms': 0.0, 'mel_enc_ms': 0.0}
+    try:
+        graph.replay()
+        torch.cuda.synchronize()
+        for _ in range(reps):
+            graph.replay()
+            torch.cuda.synchronize()
+            t.read()
+            acc['launches'] += t.launches
+            acc['flops'] += t.flops
+            acc['ms_tile'] += t.ms_tile
+            acc['ms_reduce'] += t.ms_reduce
+            acc['mel_ms'] += F.timing_mark_elapsed(0, 1)
+            acc['mel_enc_ms'] += F.timing_mark_elapsed(0, 2)
+    finally:
+        t.release()
+        del graph
+    out = {k: v / reps for k, v in acc.items()}
+    out['launches'] = int(round(out['launches']))
+    return out
 
 
 def load_traffic(name):
@@ -373,19 +426,30 @@ def mfma_peak(dtype):
             'bf16x6': BF16_MFMA_PEAK_TFLOPS / 6}[dtype]
 
 
-def roofline_entry(gt, peak=None):
+def roofline_entry(it, gt, peak=None):
+    """`roofline` for the dominant family (the implicit-GEMM engine's gemm_kernel): algorithmic
+    FLOPs per step / summed tile-kernel time per step, both from `instep_timing` (the replayed
+    step graph, branches concurrent).  `serialised_eager` keeps the round-3 basis (one eager step,
+    decoder branches serialised, every launch alone on the chip) for comparison."""
     peak = peak or FP32_MFMA_PEAK_TFLOPS
-    tf = gt.flops / (gt.ms_tile * 1e-3) / 1e12
+    tf = it['flops'] / (it['ms_tile'] * 1e-3) / 1e12
+    tf_ser = gt.flops / (gt.ms_tile * 1e-3) / 1e12
     tr = load_traffic('gemm_kernel') if peak == FP32_MFMA_PEAK_TFLOPS else None
+    n = max(it['launches'], 1)
     return {'bound': 'mfma', 'kernel': 'gemm_kernel (implicit-GEMM engine: every launch of one step)',
             'achieved': round(tf, 2), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(tf / peak, 4),
             'traffic': tr['bytes_per_launch'] if tr else None,
             'traffic_source': tr['source'] if tr else None,
-            'launches_per_step': gt.launches, 'ms_per_launch': round(gt.ms_tile / max(gt.launches, 1), 4),
-            'gflop_per_launch': round(gt.flops / max(gt.launches, 1) / 1e9, 3),
-            'ms_tile_per_step': round(gt.ms_tile, 4),
-            'splitk_reduce_ms_per_step': round(gt.ms_reduce, 4)}
+            'basis': 'in-step: the bench graph re-captured with the engine launches stamping their own '
+                     'spans (first block start .. last wave end, GPU wall clock), replayed 20 times; '
+                     'cross-check: rocprof kernel trace of replayed steps only (tools/step_pmc.sh, profiles/)',
+            'launches_per_step': it['launches'], 'ms_per_launch': round(it['ms_tile'] / n, 4),
+            'gflop_per_launch': round(it['flops'] / n / 1e9, 3),
+            'ms_tile_per_step': round(it['ms_tile'], 4),
+            'splitk_reduce_ms_per_step': round(it['ms_reduce'], 4),
+            'serialised_eager': {'achieved': round(tf_ser, 2), 'frac': round(tf_ser / peak, 4),
+                                 'ms_tile_per_step': round(gt.ms_tile, 4)}}
 
 
 def spawn_ranks(n):
@@ -505,8 +569,12 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         value = world * B * T / (elapsed / args.steps)
         gt = gemm_engine_timing(step)
+        it = instep_timing(dev, g, wave)
         mel_ms, mel_bytes = run_mel_kernel(dev, wave)
         mel_enc = mel_encoder_roofline(dev, g, wave, mel_ms, mel_bytes, mfma_peak(args.dtype))
+        mel_enc['instep_mel_ms'] = round(it['mel_ms'], 4)
+        mel_enc['instep_mel_encoder_ms'] = round(it['mel_enc_ms'], 4)
+        mel_enc['path_frac_instep'] = round(mel_enc['path_roofline_ms'] / it['mel_enc_ms'], 4)
     path_tf = g_forward_flops(B, T) / (ms_step * 1e-3) / 1e12
     peak = mfma_peak(args.dtype)
     if args.dtype == 'bf16':
@@ -526,7 +594,7 @@ def main():
         'data': 'synthetic 16 kHz speech-like audio, random-init weights',
         'config': {'workload': workload, 'global_batch': B * world, 'seq_len': T,
                    'parallelism': f'replicas{world}', 'hip_graph': 'none' if graph is None else ('per-branch graphs, two streams' if args.branch_graphs else 'one graph')},
-        'roofline': roofline_entry(gt, peak),
+        'roofline': roofline_entry(it, gt, peak),
         'mel_roofline': {'bound': 'hbm', 'achieved': round(mel_bytes / (mel_ms * 1e-3) / 1e9, 1),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(mel_bytes / (mel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

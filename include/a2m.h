@@ -483,10 +483,14 @@ int a2m_window_gather_f32(const float* data, int64_t length, int32_t C, const in
                           int32_t n_windows, int32_t window, int32_t interval, const float* mean,
                           const float* std_, float* out, void* stream);
 
-/* Measurement hook (bench.py): while enabled, every launch of the implicit-GEMM engine is
- * bracketed by HIP events on its stream; _end synchronises them and returns the launch count,
- * the launches' algorithmic FLOPs (2*M*N*K*batch), the summed tile-kernel time and the summed
- * split-K reduce time (ms).  Not graph-capturable; no effect when disabled. */
+/* Measurement hook (bench.py): while enabled, every launch of the implicit-GEMM engine (up to
+ * 4096 per window) carries a record of span stamps that its tile kernel and split-K reduce write
+ * themselves (earliest block start, latest wave end, GPU wall clock), eagerly or inside a graph
+ * captured while enabled.  _read synchronises the device and returns the launch count, the
+ * launches' algorithmic FLOPs (2*M*N*K*batch), the summed tile-kernel spans and the summed
+ * split-K reduce spans (ms) of the latest execution, then re-arms the stamps (so it can follow
+ * each replay of such a graph); _stop ends recording of new launches, _end = _stop + _read +
+ * forget the records.  No effect when disabled. */
 int a2m_gemm_timing_begin(void);
 /* Tuning hook: force the engine's tile (64 | 128) and split-K count for subsequent launches
  * (0 = the planner's choice); workspace sizing follows.  Process-global, not for production. */
@@ -503,6 +507,16 @@ int a2m_set_gemm_precision(int32_t prec);
 int32_t a2m_get_gemm_precision(void);
 int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                         int64_t* reduces);
+int a2m_gemm_timing_stop(void);
+int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
+                         int64_t* reduces);
+/* Named wall-clock marks (measurement only; after a2m_gemm_timing_begin has allocated the stamp
+ * buffer): a one-thread kernel on the stream stores the GPU wall clock into mark `slot`
+ * (0 .. A2M_TIMING_MARKS-1), also as a node of a graph being captured; _elapsed synchronises the
+ * device and returns mark b - mark a in ms. */
+#define A2M_TIMING_MARKS 16
+int a2m_timing_mark(int32_t slot, void* stream);
+int a2m_timing_mark_elapsed(int32_t a, int32_t b, float* ms);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,6 @@
 """MFMA utilisation per kernel family from a rocprofv3 PMC pass of
 SQ_VALU_MFMA_BUSY_CYCLES + SQ_BUSY_CYCLES + GRBM_GUI_ACTIVE and a kernel-trace pass of the
-same command (tools/step_pmc.sh).
+same command (tools/step_pmc.sh), replayed steps only (tools/replay_filter.py).
 
   busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycles), cycles = GRBM_GUI_ACTIVE / 8
   (rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs: MI355X_MICROARCH.md, DVFS give-back).
@@ -10,11 +10,13 @@ The counter's scale is calibrated in DESIGN.md against the engine's known MFMA c
     python tools/pmc_mfma.py MFMA_DIR TRACE_DIR [--out file.json]
 """
 import argparse
-import csv
-import glob
 import json
 import os
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from replay_filter import load, replayed  # noqa: E402
 
 FAMILIES = ('gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'graph_layer_kernel',
             'attn_fused_eval_kernel', 'attn_core', 'im2col', 'channel_att', 'layernorm_kernel')
@@ -30,19 +32,17 @@ def main():
     ap.add_argument('trace_dir')
     ap.add_argument('--out', default=None)
     a = ap.parse_args()
-    fn = glob.glob(os.path.join(a.mfma_dir, '**', '*counter_collection.csv'), recursive=True)[0]
     per = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
-    for r in csv.DictReader(open(fn, newline='')):
+    for r in replayed(load(a.mfma_dir, '*counter_collection.csv')):
         f = fam_of(r['Kernel_Name'])
         per[f][r['Counter_Name']] += float(r['Counter_Value'])
         disp[f].add(r.get('Dispatch_Id') or r.get('Correlation_Id'))
-    tfn = glob.glob(os.path.join(a.trace_dir, '**', '*kernel_stats.csv'), recursive=True)[0]
     dur = defaultdict(lambda: [0, 0.0])
-    for r in csv.DictReader(open(tfn, newline='')):
-        f = fam_of(r['Name'])
-        dur[f][0] += int(r['Calls'])
-        dur[f][1] += float(r['TotalDurationNs'])
+    for r in replayed(load(a.trace_dir, '*kernel_trace.csv')):
+        f = fam_of(r['Kernel_Name'])
+        dur[f][0] += 1
+        dur[f][1] += float(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
     out = {}
     for f, d in sorted(per.items()):
         n = len(disp[f])

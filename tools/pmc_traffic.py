@@ -7,15 +7,19 @@ for one pass on gfx950), with the MI355X_MICROARCH.md corrections:
 
     python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [--out profiles/traffic_latest.json]
 
-Each DIR is a rocprofv3 `-d` output directory holding a *counter_collection.csv.  Kernel
-families are matched by substring (gemm_kernel, logmel_kernel, graph_layer_kernel, ...).
+Each DIR is a rocprofv3 `-d` output directory holding a *counter_collection.csv of a
+tools/step_pmc.py run; only the replayed steps' dispatches (after the marker kernel,
+tools/replay_filter.py) are counted.  Kernel families are matched by substring (gemm_kernel,
+logmel_kernel, graph_layer_kernel, ...).
 """
 import argparse
-import csv
-import glob
 import json
 import os
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from replay_filter import load, replayed  # noqa: E402
 
 FAMILIES = ('gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'logmel_kernel',
             'graph_stack_kernel', 'graph_layer_kernel', 'graph_att_proj_kernel', 'attn_fused_eval_kernel',
@@ -24,25 +28,20 @@ FAMILIES = ('gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'logmel_
 
 
 def read_counter(d, name):
-    files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
-    if not files:
-        raise SystemExit(f'no counter_collection.csv under {d}')
     per = defaultdict(lambda: [0, 0.0])       # family -> [dispatches, KB]
     seen = set()
-    for fn in files:
-        with open(fn, newline='') as f:
-            for row in csv.DictReader(f):
-                if row.get('Counter_Name') != name:
-                    continue
-                kn = row.get('Kernel_Name', '')
-                fam = next((x for x in FAMILIES if x in kn), None)
-                if fam is None:
-                    continue
-                key = (fn, row.get('Dispatch_Id') or row.get('Correlation_Id'))
-                if key not in seen:
-                    seen.add(key)
-                    per[fam][0] += 1
-                per[fam][1] += float(row['Counter_Value'])
+    for row in replayed(load(d, '*counter_collection.csv')):
+        if row.get('Counter_Name') != name:
+            continue
+        kn = row.get('Kernel_Name', '')
+        fam = next((x for x in FAMILIES if x in kn), None)
+        if fam is None:
+            continue
+        key = row.get('Dispatch_Id') or row.get('Correlation_Id')
+        if key not in seen:
+            seen.add(key)
+            per[fam][0] += 1
+        per[fam][1] += float(row['Counter_Value'])
     return per
 
 
@@ -64,7 +63,7 @@ def main():
         wr = kw * 1024 / nw
         out[fam] = {'bytes_per_launch': round(rd + wr), 'read_bytes_per_launch': round(rd),
                     'write_bytes_per_launch': round(wr), 'dispatches': [nf, nw],
-                    'source': f'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes {a.tag}; FETCH x2 (gfx950), KB x1024'}
+                    'source': f'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes {a.tag}, replayed steps only; FETCH x2 (gfx950), KB x1024'}
     os.makedirs(os.path.dirname(a.out) or '.', exist_ok=True)
     with open(a.out, 'w') as f:
         json.dump(out, f, indent=1)

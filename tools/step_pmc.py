@@ -1,7 +1,9 @@
 """Runs exactly the bench step (bench.py configs[1]: HIP log-mel + SelfAttention_G eval over
 B synthetic clips, captured in one HIP graph) and nothing else, for PMC passes whose per-launch
-averages must describe the benched code: the two eager warm-up steps of bench.capture_step
-plus R graph replays, every dispatch a bench-step kernel.
+averages must describe the benched code: the two eager warm-up steps of bench.capture_step and
+the capture, then one marker kernel (torch.cuda._sleep), then R graph replays.  The tools that
+read the output (replay_filter.py) keep only the dispatches after the marker, i.e. the
+replayed steps: no first-call repacks, no eager-step copies.
 
     rocprofv3 --pmc FETCH_SIZE -d DIR -- python tools/step_pmc.py [R] [--dtype bf16]
 """
@@ -17,7 +19,13 @@ import bench  # noqa: E402
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    argv = sys.argv[1:]
+    ejson = None
+    if '--engine-json' in argv:
+        i = argv.index('--engine-json')
+        ejson = argv[i + 1]
+        del argv[i:i + 2]
+    args = [a for a in argv if not a.startswith('--') and a != 'bf16']
     reps = int(args[0]) if args else 3
     dev = torch.device('cuda:0')
     import a2m
@@ -33,10 +41,21 @@ def main():
     wave = bench.synth_wave(B, (T - 1) * bench.HOP + bench.WIN, seed=0, device=dev)
     with torch.no_grad():
         graph, out = bench.capture_step(dev, bench.infer_step(g, wave))
+        graph.replay()
+        torch.cuda.synchronize()
+        if ejson:
+            # the engine's algorithmic FLOPs per step (one eager step with the timing hook),
+            # for tools/replay_breakdown.py's roofline figure
+            gt = bench.gemm_engine_timing(bench.infer_step(g, wave))
+            import json
+            with open(ejson, 'w') as f:
+                json.dump({'launches': gt.launches, 'gflop': gt.flops / 1e9}, f)
+        torch.cuda._sleep(1000)             # the marker dispatch
+        torch.cuda.synchronize()
         for _ in range(reps):
             graph.replay()
     torch.cuda.synchronize()
-    print(f'step_pmc: 2 eager + {reps} graph steps, out {tuple(out.shape)}')
+    print(f'step_pmc: 2 eager + 1 graph step, marker, then {reps} replayed steps, out {tuple(out.shape)}')
 
 
 if __name__ == '__main__':
