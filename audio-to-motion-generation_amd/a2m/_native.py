@@ -125,6 +125,9 @@ SIGNATURES = {
     'a2m_gemm_timing_end': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
                                            ctypes.POINTER(F64), ctypes.POINTER(I64)]),
     'a2m_gemm_timing_stop': (ctypes.c_int, []),
+    'a2m_gemm_timing_clear': (ctypes.c_int, []),
+    'a2m_gemm_timing_read_spans': (ctypes.c_int, [I64, ctypes.POINTER(F64), ctypes.POINTER(F64),
+                                                  ctypes.POINTER(I64)]),
     'a2m_gemm_timing_read': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
                                             ctypes.POINTER(F64), ctypes.POINTER(I64)]),
     'a2m_timing_mark': (ctypes.c_int, [I32, ctypes.c_void_p]),

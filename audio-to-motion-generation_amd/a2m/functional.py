@@ -905,11 +905,11 @@ def adam_(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
 
 
 class gemm_timing:
-    """Context manager: HIP-event timing of every implicit-GEMM launch issued inside it
+    """Context manager: span-stamp timing of every implicit-GEMM launch issued inside it
     (a2m_gemm_timing_begin/_end).  After exit: .launches, .flops, .ms_tile, .ms_reduce,
-    .reduces.  With keep=True the events outlive the block: launches captured into a HIP graph
-    inside it carry event-record nodes, and read() after each replay of that graph returns the
-    latest replay's sums; release() frees them."""
+    .reduces.  With keep=True the records outlive the block: launches captured into a HIP graph
+    inside it keep their span stamps, and read() after each replay of that graph returns the
+    latest replay's sums (and re-arms the stamps); release() forgets the records."""
 
     def __init__(self, keep=False):
         self.keep = keep
@@ -930,14 +930,22 @@ class gemm_timing:
     def read(self):
         return self._sums(N.lib.a2m_gemm_timing_read)
 
+    def spans(self, cap=4096):
+        """[(start_us, end_us)] of every recorded launch's tile kernel in the latest execution
+        (re-arms the stamps like read())."""
+        import ctypes
+        s, e, n = (ctypes.c_double * cap)(), (ctypes.c_double * cap)(), ctypes.c_int64()
+        N.check(N.lib.a2m_gemm_timing_read_spans(cap, s, e, ctypes.byref(n)))
+        return [(s[i], e[i]) for i in range(n.value)]
+
     def release(self):
-        return self._sums(N.lib.a2m_gemm_timing_end)
+        N.check(N.lib.a2m_gemm_timing_clear())
 
     def __exit__(self, *exc):
         if self.keep:
             N.check(N.lib.a2m_gemm_timing_stop())
         else:
-            self.release()
+            self._sums(N.lib.a2m_gemm_timing_end)
         return False
 
 

@@ -20,6 +20,8 @@ batch statistics by default (PyTorch DDP default) or SyncBN.  The discriminator'
 are frozen during the G steps: the reference computes their gradients there and throws them
 away (optimizer_D.zero_grad() at :388).
 """
+import contextlib
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -140,11 +142,24 @@ class GradReducer:
     everything at finish()); afterwards a parameter arriving in an already launched bucket is an
     error, never a silent miss.  finish() gathers and reduces what is left, waits, and divides
     by the world size.  reduce_dtype=torch.bfloat16 halves the bytes on the wire (configs[4]).
+    force=True arms the reducer also for a one-rank group (the RCCL path exercised on one GPU,
+    tests/test_gpu_rccl.py).
+
+    Every rank also all-reduces a small error flag after its buckets, so that a plan violation
+    seen on one rank fails all of them together instead of deadlocking.  The flag is read back on
+    the host (a device sync) only on the first two steps; afterwards it is read at the start of
+    the next finish(), so the backward / optimizer step run ahead of the host as without it, and a
+    violation raises one step late on every rank at the same point.
     """
 
-    def __init__(self, opt, world, group=None, bucket_mb=25.0, reduce_dtype=None):
+    SYNC_CHECK_STEPS = 2
+
+    def __init__(self, opt, world, group=None, bucket_mb=25.0, reduce_dtype=None, force=False):
         self.opt, self.world, self.group = opt, world, group
+        self.force = force
         self.reduce_dtype = reduce_dtype
+        self.steps = 0
+        self._pending_flag = None
         spans = list(opt._spans())
         cap = max(int(bucket_mb * (1 << 20) / 4), 1)
         # buckets tile [0, numel) of the flat gradient (alignment padding included: it stays
@@ -180,7 +195,7 @@ class GradReducer:
     def begin(self):
         """Arm the hooks for one backward (call after zero_grad, before backward)."""
         self._reset()
-        self.active = self.world > 1
+        self.active = self.world > 1 or self.force
 
     def _make_hook(self, i):
         def hook(p):
@@ -251,13 +266,25 @@ class GradReducer:
         flag = torch.tensor([1.0 if self.error else 0.0, n, -n], dtype=torch.float64,
                             device=self.opt.flat_grad.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
-        if flag[0].item() > 0 or flag[1].item() != -flag[2].item():
-            self.active = False
-            raise RuntimeError(self.error or 'GradReducer: another rank received gradients outside '
-                                             'the learnt parameter set')
-        self.opt.flat_grad.div_(self.world)
+        prev, self._pending_flag = self._pending_flag, None
+        self.steps += 1
         self.active = False
+        if prev is not None:
+            self._check_flag(prev)
+        if self.steps <= self.SYNC_CHECK_STEPS:
+            self._check_flag(flag)
+        else:
+            self._pending_flag = flag
+        if self.world > 1:
+            self.opt.flat_grad.div_(self.world)
         return self.opt.flat_grad
+
+    def _check_flag(self, flag):
+        f = flag.tolist()
+        if f[0] > 0 or f[1] != -f[2]:
+            self._pending_flag = None
+            raise RuntimeError(self.error or 'GradReducer: a rank received gradients outside the '
+                                             'learnt parameter set')
 
 
 class GANTrainer:
@@ -265,7 +292,14 @@ class GANTrainer:
 
     def __init__(self, generator, discriminator, lr=10e-4, lambda_gan=1.0, lambda_d=1.0,
                  dynamic=None, fixed_labels=None, process_group=None, sync_bn=False,
-                 bucket_mb=25.0, grad_reduce_dtype=None, label_seed=None):
+                 bucket_mb=25.0, grad_reduce_dtype=None, label_seed=None, force_collectives=False):
+        """label_seed: seed of the generator the noisy GAN labels are drawn from; None (the
+        default) derives it from torch.initial_seed() of rank 0, so the labels follow the
+        caller's torch.manual_seed like the reference's global-RNG draw (an unseeded process
+        draws different labels each run, as the reference does).  With several ranks the seed
+        is broadcast here, at construction, not inside a step.  force_collectives: run the
+        data-parallel machinery (bucketed gradient all-reduce, SyncBN) also when the process
+        group has one rank -- the RCCL path on one GPU (tests/test_gpu_rccl.py)."""
         self.G, self.D = generator, discriminator
         self.opt_G = FlatAdam(generator.parameters(), lr=lr)
         self.opt_D = FlatAdam(discriminator.parameters(), lr=lr)
@@ -278,12 +312,17 @@ class GANTrainer:
         self.rank = dist.get_rank(process_group) if dp else 0
         # SyncBN: BatchNorm statistics all-reduced over the DP group, so the
         # ranks normalise over the whole batch like the single-device reference step
-        self.sync_bn = bool(sync_bn) and self.world > 1
-        self.red_G = GradReducer(self.opt_G, self.world, process_group, bucket_mb, grad_reduce_dtype)
-        self.red_D = GradReducer(self.opt_D, self.world, process_group, bucket_mb, grad_reduce_dtype)
+        force = bool(force_collectives) and dp
+        self.sync_bn = bool(sync_bn) and (self.world > 1 or force)
+        self.red_G = GradReducer(self.opt_G, self.world, process_group, bucket_mb, grad_reduce_dtype, force)
+        self.red_D = GradReducer(self.opt_D, self.world, process_group, bucket_mb, grad_reduce_dtype, force)
         self.label_seed = label_seed
         self._label_gen = None
         self.last_d_loss = None
+        if fixed_labels is None and label_seed is None and self.world > 1:
+            # agree on the label seed now (a collective), not lazily inside the first step
+            dev = next(generator.parameters()).device
+            self.label_seed = self._shared_label_seed(dev if dev.type == 'cuda' else torch.device('cpu'))
 
     def _allreduce_(self, t):
         if self.world > 1:
@@ -346,15 +385,23 @@ class GANTrainer:
         self.opt_D.step()
         return d_loss.detach()
 
-    def iteration(self, audio, real_pose, epoch=0, g_freq=None, d_freq=None, sync_losses=True):
-        """version5_model_train.py:330-414 for one batch; returns (D_loss, G_loss) tensors."""
+    @contextlib.contextmanager
+    def sync_bn_scope(self):
+        """BatchNorm statistics over the DP group inside the block when sync_bn is on (iteration()
+        enters it; g_step / d_step called directly need it for SyncBN)."""
         if not self.sync_bn:
-            return self._iteration(audio, real_pose, epoch, g_freq, d_freq, sync_losses)
+            yield
+            return
         prev = F.set_sync_bn_group(self.pg if self.pg is not None else dist.group.WORLD)
         try:
-            return self._iteration(audio, real_pose, epoch, g_freq, d_freq, sync_losses)
+            yield
         finally:
             F.set_sync_bn_group(prev)
+
+    def iteration(self, audio, real_pose, epoch=0, g_freq=None, d_freq=None, sync_losses=True):
+        """version5_model_train.py:330-414 for one batch; returns (D_loss, G_loss) tensors."""
+        with self.sync_bn_scope():
+            return self._iteration(audio, real_pose, epoch, g_freq, d_freq, sync_losses)
 
     def _iteration(self, audio, real_pose, epoch, g_freq, d_freq, sync_losses):
         dev = audio.device

@@ -1,5 +1,6 @@
 // Implicit-GEMM engine: host side (operand modes, planner, split-K reduce, launch, timing).
 // The kernels and their description are in gemm_kernel.h.
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -133,9 +134,9 @@ __device__ __forceinline__ void splitk_reduce(const GemmArgs& args, int batch) {
   }
 }
 
-// the reduce's span stamps go to slots 2, 3 of the launch's record
+// the reduce's span stamps follow the tile kernel's in the launch's record
 __device__ __forceinline__ unsigned long long* reduce_span(const GemmArgs& args) {
-  return args.ts ? args.ts + 2 : nullptr;
+  return args.ts ? args.ts + kSpanSlots : nullptr;
 }
 
 __global__ void splitk_reduce_kernel(GemmArgs args, int batch) {
@@ -418,18 +419,19 @@ struct GemmTiming {
   bool reduce;
   char desc[96];   // shape/plan, printed per launch by a2m_gemm_timing_read under A2M_GEMM_LOG=2
 };
-constexpr int kTimingRecs = 4096;   // launches per timing window
+constexpr int kTimingRecs = 1024;   // launches per timing window
 static std::mutex g_timing_mu;
 static bool g_timing = false;
 static bool g_timing_overflow = false;
 static std::vector<GemmTiming> g_timing_recs;
-static unsigned long long* g_ts = nullptr;   // [kTimingRecs][4] + [A2M_TIMING_MARKS] mark slots
+constexpr int kRecSlots = 2 * kSpanSlots;   // tile + reduce
+static unsigned long long* g_ts = nullptr;   // [kTimingRecs][kRecSlots] + [A2M_TIMING_MARKS] mark slots
 static double g_wall_mhz = 0.0;
 
 // (re)arm the stamps: start slots at the maximum, end slots at 0
 static int timing_reset_stamps() {
-  std::vector<unsigned long long> init((size_t)kTimingRecs * 4, 0ull);
-  for (int i = 0; i < kTimingRecs; ++i) init[(size_t)i * 4] = init[(size_t)i * 4 + 2] = ~0ull;
+  std::vector<unsigned long long> init((size_t)kTimingRecs * kRecSlots, 0ull);
+  for (size_t i = 0; i < init.size(); i += 2) init[i] = ~0ull;
   return hipMemcpy(g_ts, init.data(), init.size() * sizeof(unsigned long long), hipMemcpyHostToDevice) ==
          hipSuccess ? A2M_OK : A2M_EHIP;
 }
@@ -443,13 +445,13 @@ static int timing_alloc() {
   int dev = 0, khz = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0 ||
-      hipMalloc(&g_ts, ((size_t)kTimingRecs * 4 + A2M_TIMING_MARKS) * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&g_ts, ((size_t)kTimingRecs * kRecSlots + A2M_TIMING_MARKS) * sizeof(unsigned long long)) != hipSuccess) {
     set_error("gemm timing: device stamp buffer / wall clock rate unavailable");
     g_ts = nullptr;
     return A2M_EHIP;
   }
   g_wall_mhz = khz / 1e3;
-  return hipMemset(g_ts, 0, ((size_t)kTimingRecs * 4 + A2M_TIMING_MARKS) * sizeof(unsigned long long)) ==
+  return hipMemset(g_ts, 0, ((size_t)kTimingRecs * kRecSlots + A2M_TIMING_MARKS) * sizeof(unsigned long long)) ==
          hipSuccess ? A2M_OK : A2M_EHIP;
 }
 
@@ -464,7 +466,7 @@ static unsigned long long* timing_open(double flops, const char* desc) {
   t.flops = flops;
   std::snprintf(t.desc, sizeof(t.desc), "%s", desc);
   g_timing_recs.push_back(t);
-  return g_ts + 4 * (g_timing_recs.size() - 1);
+  return g_ts + kRecSlots * (g_timing_recs.size() - 1);
 }
 
 int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int K, int batch,
@@ -623,32 +625,55 @@ int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, doub
   A2M_CHECK_ARG(!a2m::g_timing_overflow, "gemm_timing_read: more than %d launches in the window",
                 a2m::kTimingRecs);
   const size_t nrec = a2m::g_timing_recs.size();
-  std::vector<unsigned long long> st(nrec * 4 + 1);
+  const int R = a2m::kRecSlots, S = a2m::kSpanSlots;
+  std::vector<unsigned long long> st(nrec * R + 1);
   if (hipDeviceSynchronize() != hipSuccess ||
-      (nrec && hipMemcpy(st.data(), a2m::g_ts, nrec * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
+      (nrec && hipMemcpy(st.data(), a2m::g_ts, nrec * R * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
                    hipSuccess)) {
     a2m::set_error("gemm timing: stamp read failed");
     return A2M_EHIP;
   }
+  // a kernel's duration: its longest per-XCD span (-1: no XCD stamped, i.e. it did not run since
+  // the last reset); *global: last end - first start over all XCDs (diagnostic)
+  auto span = [](const unsigned long long* s, double* global) {
+    double best = -1.0;
+    unsigned long long glo = ~0ull, ghi = 0;
+    for (int x = 0; x < 8; ++x) {
+      unsigned long long lo = ~0ull, hi = 0;
+      for (int l = 0; l < a2m::kSpanLanes; ++l) {
+        const unsigned long long* q = s + 2 * (x * a2m::kSpanLanes + l);
+        if (q[0] == ~0ull || q[1] < q[0]) continue;
+        lo = std::min(lo, q[0]);
+        hi = std::max(hi, q[1]);
+      }
+      if (lo == ~0ull) continue;
+      best = std::max(best, (double)(hi - lo));
+      glo = std::min(glo, lo);
+      ghi = std::max(ghi, hi);
+    }
+    *global = ghi >= glo ? (double)(ghi - glo) : -1.0;
+    return best;
+  };
   int64_t n = 0, nr = 0;
   double f = 0, mt = 0, mr = 0;
   int rc = A2M_OK;
   const double tick_ms = 1.0 / (a2m::g_wall_mhz * 1e3);
   for (size_t i = 0; i < nrec; ++i) {
     const a2m::GemmTiming& t = a2m::g_timing_recs[i];
-    const unsigned long long* s = &st[i * 4];
-    if (s[1] < s[0] || (t.reduce && s[3] < s[2])) {   // a launch that did not run since the reset
+    double ga = 0, gb = 0;
+    const double sa = span(&st[i * R], &ga), sb = t.reduce ? span(&st[i * R + S], &gb) : 0.0;
+    if (sa < 0 || sb < 0) {
       a2m::set_error("gemm timing: launch %zu (%s) has no stamps", i, t.desc);
       rc = A2M_EHIP;
       continue;
     }
-    const double a = (double)(s[1] - s[0]) * tick_ms, b = t.reduce ? (double)(s[3] - s[2]) * tick_ms : 0.0;
+    const double a = sa * tick_ms, b = sb * tick_ms;
     ++n;
     f += t.flops;
     static const int log_launches = a2m::env_int("A2M_GEMM_LOG", 0);
     if (log_launches >= 2)
-      std::fprintf(stderr, "a2m gemm-time %s tile %.1f us reduce %.1f us %.1f TF\n", t.desc,
-                   1e3 * a, 1e3 * b, a > 0 ? t.flops / (1e9 * a) : 0.0);
+      std::fprintf(stderr, "a2m gemm-time %s tile %.1f us (all-XCD span %.1f) reduce %.1f us %.1f TF\n", t.desc,
+                   1e3 * a, 1e3 * ga * tick_ms, 1e3 * b, a > 0 ? t.flops / (1e9 * a) : 0.0);
     mt += a;
     if (t.reduce) { mr += b; ++nr; }
   }
@@ -665,6 +690,34 @@ int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, doub
   return rc;
 }
 
+int a2m_gemm_timing_read_spans(int64_t cap, double* start_us, double* end_us, int64_t* n) {
+  std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+  A2M_CHECK_ARG(a2m::g_ts != nullptr && start_us && end_us && n && cap >= 0,
+                "gemm_timing_read_spans: bad arguments (or timing never begun)");
+  const size_t nrec = std::min<size_t>(a2m::g_timing_recs.size(), (size_t)cap);
+  const int R = a2m::kRecSlots;
+  std::vector<unsigned long long> st(nrec * R + 1);
+  if (hipDeviceSynchronize() != hipSuccess ||
+      (nrec && hipMemcpy(st.data(), a2m::g_ts, nrec * R * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
+                   hipSuccess)) {
+    a2m::set_error("gemm timing: stamp read failed");
+    return A2M_EHIP;
+  }
+  for (size_t i = 0; i < nrec; ++i) {
+    unsigned long long lo = ~0ull, hi = 0;
+    for (int s = 0; s < a2m::kSpanSlots; s += 2) {
+      const unsigned long long* q = &st[i * R + s];
+      if (q[0] == ~0ull || q[1] < q[0]) continue;
+      lo = std::min(lo, q[0]);
+      hi = std::max(hi, q[1]);
+    }
+    start_us[i] = lo == ~0ull ? -1.0 : (double)lo / a2m::g_wall_mhz;
+    end_us[i] = lo == ~0ull ? -1.0 : (double)hi / a2m::g_wall_mhz;
+  }
+  *n = (int64_t)nrec;
+  return a2m::timing_reset_stamps() == A2M_OK ? A2M_OK : A2M_EHIP;
+}
+
 int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                         int64_t* reduces) {
   a2m_gemm_timing_stop();
@@ -674,6 +727,13 @@ int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, doubl
   return rc;
 }
 
+int a2m_gemm_timing_clear(void) {
+  std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+  a2m::g_timing = false;
+  a2m::g_timing_recs.clear();
+  return A2M_OK;
+}
+
 // Named wall-clock marks (bench.py's in-step phase split: step start, log-mel done, encoder
 // done): a one-thread kernel stores the clock into the mark's slot, so a mark captured into a
 // graph re-stamps on every replay.  Its own dispatch is ~1-2 us of the interval it opens.
@@ -681,7 +741,7 @@ int a2m_timing_mark(int32_t slot, void* stream) {
   A2M_CHECK_ARG(slot >= 0 && slot < A2M_TIMING_MARKS, "timing_mark: slot %d", slot);
   A2M_CHECK_ARG(a2m::g_ts != nullptr, "timing_mark: call a2m_gemm_timing_begin first (stamp buffer)");
   hipLaunchKernelGGL(a2m::timing_mark_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
-                     a2m::g_ts + (size_t)a2m::kTimingRecs * 4 + slot);
+                     a2m::g_ts + (size_t)a2m::kTimingRecs * a2m::kRecSlots + slot);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }
@@ -691,7 +751,7 @@ int a2m_timing_mark_elapsed(int32_t a, int32_t b, float* ms) {
                 "timing_mark_elapsed: slots %d, %d", a, b);
   unsigned long long m[A2M_TIMING_MARKS];
   if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(m, a2m::g_ts + (size_t)a2m::kTimingRecs * 4, sizeof(m), hipMemcpyDeviceToHost) != hipSuccess) {
+      hipMemcpy(m, a2m::g_ts + (size_t)a2m::kTimingRecs * a2m::kRecSlots, sizeof(m), hipMemcpyDeviceToHost) != hipSuccess) {
     a2m::set_error("timing_mark_elapsed: stamp read failed");
     return A2M_EHIP;
   }

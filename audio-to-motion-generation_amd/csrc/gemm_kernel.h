@@ -42,19 +42,33 @@ struct GemmArgs {
                    // along m (split-K slabs then are [N][M])
   int skew;        // KS = 3: wave group 1 runs its k-steps half a step after group 0's
   unsigned long long* ts;   // measurement only (a2m_gemm_timing_*; null otherwise): this launch's
-                            // [tile first start, tile last end, reduce first start, reduce last
-                            // end] on the GPU wall clock
+                            // span stamps, [tile | reduce][XCD][first start, last end]
 };
 
-// Launch-span stamps (bench.py's in-step roofline): the earliest block start and the latest
-// wave end of a launch, from the constant-rate wall clock, by vector atomics into the launch's
-// slots.  They work identically eagerly and inside a replayed HIP graph (where event records
-// between kernels are not timestamps of the kernel: DESIGN.md 6).
+// Launch-span stamps (bench.py's in-step roofline): per XCD, the earliest block start and the
+// latest block end of a launch on the constant-rate wall clock, by vector atomics into the
+// launch's slots.  Each block stamps once at its start and once after a final barrier, into
+// one of kSpanLanes slot pairs of its XCD chosen by its linear block id, so a short launch of
+// thousands of blocks does not serialise on a handful of addresses (one pair per XCD inflated
+// a 7 us split-K reduce to 40 us).  Kept per XCD because the XCDs' clocks need not agree: a
+// launch's duration is taken as its longest per-XCD span (every XCD receives blocks from the
+// dispatch's first moment).  They work identically eagerly and inside a replayed HIP graph
+// (where event records between kernels are not timestamps of the kernel: DESIGN.md 6).
+constexpr int kSpanLanes = 32;
+constexpr int kSpanSlots = 8 * kSpanLanes * 2;   // XCD x lane x (start, end) per kernel
+__device__ __forceinline__ unsigned long long* span_slot(unsigned long long* p) {
+  const unsigned xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;   // hwreg(HW_REG_XCC_ID, 0, 4)
+  const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  return p + 2 * (xcd * kSpanLanes + lin % kSpanLanes);
+}
 __device__ __forceinline__ void span_begin(unsigned long long* p) {
-  if (p && threadIdx.x == 0) atomicMin(p, (unsigned long long)wall_clock64());
+  if (p && threadIdx.x == 0) atomicMin(span_slot(p), (unsigned long long)wall_clock64());
 }
 __device__ __forceinline__ void span_end(unsigned long long* p) {
-  if (p && (threadIdx.x & 63) == 0) atomicMax(p + 1, (unsigned long long)wall_clock64());
+  if (p) {   // uniform: the whole block takes the barrier
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(span_slot(p) + 1, (unsigned long long)wall_clock64());
+  }
 }
 
 struct RowInfo {

@@ -508,6 +508,12 @@ int32_t a2m_get_gemm_precision(void);
 int a2m_gemm_timing_end(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                         int64_t* reduces);
 int a2m_gemm_timing_stop(void);
+/* Per-launch tile-kernel spans of the latest execution instead of their sums: the first block
+ * start and last block end (us on the GPU wall clock, -1 for a launch that did not run) of the
+ * first min(cap, launches) records; re-arms the stamps like _read. */
+int a2m_gemm_timing_read_spans(int64_t cap, double* start_us, double* end_us, int64_t* n);
+/* _stop + forget the records without reading them (after the last _read of a kept window) */
+int a2m_gemm_timing_clear(void);
 int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                          int64_t* reduces);
 /* Named wall-clock marks (measurement only; after a2m_gemm_timing_begin has allocated the stamp
