@@ -445,8 +445,11 @@ static int conv2d_nhwc_gemm(const float* x, int B, int Ci, int H, int W, const f
                             int kh, int kw, int stride, int pad_h, int pad_w, int Hout, int w_lo, int Wn,
                             const Epilogue& E, void* ws, size_t ws_bytes, hipStream_t st) {
   Gather A = dense_rk(packed, Ci * kh * kw);
-  if (Ci % gemm_k_tile() == 0) {
-    // every k-tile is one tap's slice of Ci channels: channels-last conv rows (loader mode 6)
+  if (Ci % gemm_k_tile() == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    // every k-tile is one tap's slice of Ci channels: channels-last conv rows (loader mode 6,
+    // float4 loads: x 16-byte aligned, and every row's channel run starts at a multiple of Ci
+    // floats; a 4-byte-aligned x takes the mode-4 k-run loader below, whose float4u loads need
+    // only 4-byte alignment)
     Gather Bc{};
     Bc.base = x; Bc.sr0 = H * W * Ci; Bc.R1 = Hout; Bc.R2 = Wn; Bc.ar1 = stride; Bc.ar2 = stride;
     Bc.ch = -pad_h; Bc.cw = w_lo * stride - pad_w; Bc.Lh = H; Bc.Lw = W; Bc.K1 = kh; Bc.K2 = kw;

@@ -38,36 +38,34 @@ __device__ __forceinline__ double bsum(double v, double* red) {
   return s;
 }
 
-// angle a = atan2(cross(u,v), dot(u,v)), u = p_j - p_a, v = p_c - p_j; dL/da = g
-__device__ __forceinline__ void angle_grad(const float* p, int a, int j, int c, float g, float* d) {
+// angle a = atan2(cross(u,v), dot(u,v)), u = p_j - p_a, v = p_c - p_j; dL/da = g.  Returns the
+// adjoints of u and v (gux, guy, gvx, gvy): joint j receives (gux - gvx, guy - gvy), joint a
+// (-gux, -guy), joint c (gvx, gvy).
+__device__ __forceinline__ float4 angle_grad(const float* p, int a, int j, int c, float g) {
   const float ux = p[2 * j] - p[2 * a], uy = p[2 * j + 1] - p[2 * a + 1];
   const float vx = p[2 * c] - p[2 * j], vy = p[2 * c + 1] - p[2 * j + 1];
   const float cr = ux * vy - uy * vx, dt = ux * vx + uy * vy;
   const float den = cr * cr + dt * dt;
-  if (den == 0.f || g == 0.f) return;
+  if (den == 0.f || g == 0.f) return make_float4(0.f, 0.f, 0.f, 0.f);
   const float gcr = g * dt / den, gdt = -g * cr / den;  // d atan2(y,x)/dy = x/r^2, /dx = -y/r^2
   // cross = ux vy - uy vx ; dot = ux vx + uy vy
-  const float gux = gcr * vy + gdt * vx, guy = -gcr * vx + gdt * vy;
-  const float gvx = -gcr * uy + gdt * ux, gvy = gcr * ux + gdt * uy;
-  atomicAdd(&d[2 * j], gux - gvx);
-  atomicAdd(&d[2 * j + 1], guy - gvy);
-  atomicAdd(&d[2 * a], -gux);
-  atomicAdd(&d[2 * a + 1], -guy);
-  atomicAdd(&d[2 * c], gvx);
-  atomicAdd(&d[2 * c + 1], gvy);
+  return make_float4(gcr * vy + gdt * vx, -gcr * vx + gdt * vy, -gcr * uy + gdt * ux, gcr * ux + gdt * uy);
 }
 
-// One workgroup per clip.  LDS accumulation (atomics on LDS within one workgroup): the
-// order of float additions into one pose coordinate varies with thread timing, within
-// ~1 ulp per term.
+// One workgroup per clip, kTC time steps per pass.  Phase 1: every bone's and every angle
+// triple's adjoint, each written by one thread into its own LDS slot; phase 2: one thread per
+// (time step, joint) adds the slots that touch its joint in a fixed order (its own bone, its
+// children's bones ascending, the hand triples ascending, the body triples ascending).  No
+// atomics: the gradient is bitwise reproducible (the LDS float atomics used before summed in
+// thread-timing order and moved the G-step's gradients by ~1 ulp run to run).
 __global__ __launch_bounds__(256) void pose_loss_bwd_kernel(const float* gen, int64_t gs_b,
                                                             int64_t gs_t, const float* real,
                                                             int64_t rs_b, int64_t rs_t, int B, int T,
                                                             float hand_w, float body_w,
                                                             const float* grad_out, float* dgen) {
   __shared__ float lg[51], lr[51], coef[51];
-  __shared__ float acc[kTC * 104];
-  __shared__ double red[4];
+  __shared__ float2 bone_g[kTC][51];    // (s dx, s dy) of bone k (joint k+1 from its parent)
+  __shared__ float4 tri_g[kTC][35];     // angle adjoints: 30 hand triples, then 5 body triples
   const int b = blockIdx.x;
   const float gbone = real ? grad_out[0] : 0.f, gang = grad_out[1];
   // mean bone lengths over time (as in the forward)
@@ -92,25 +90,17 @@ __global__ __launch_bounds__(256) void pose_loss_bwd_kernel(const float* gen, in
   const float gh = gang * hand_w / (float)(B * T * 30), gb = gang * body_w / (float)(B * T * 5);
   for (int t0 = 0; t0 < T; t0 += kTC) {
     const int nt = min(kTC, T - t0);
-    for (int i = threadIdx.x; i < kTC * 104; i += blockDim.x) acc[i] = 0.f;
-    __syncthreads();
     for (int i = threadIdx.x; i < nt * 51; i += blockDim.x) {  // bones
       const int tt = i / 51, k = i % 51, jb = k + 1, pj = kPar[jb];
       const float* p = gen + b * gs_b + (t0 + tt) * gs_t;
       const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
       const float n = sqrtf(dx * dx + dy * dy);
-      if (n == 0.f || coef[k] == 0.f) continue;
-      const float s = coef[k] / n;
-      float* a = acc + tt * 104;
-      atomicAdd(&a[2 * jb], s * dx);
-      atomicAdd(&a[2 * jb + 1], s * dy);
-      atomicAdd(&a[2 * pj], -s * dx);
-      atomicAdd(&a[2 * pj + 1], -s * dy);
+      const float s = (n == 0.f || coef[k] == 0.f) ? 0.f : coef[k] / n;
+      bone_g[tt][k] = make_float2(s * dx, s * dy);
     }
     for (int i = threadIdx.x; i < nt * 35; i += blockDim.x) {  // angle triples
       const int tt = i / 35, q = i % 35;
       const float* p = gen + b * gs_b + (t0 + tt) * gs_t;
-      float* a = acc + tt * 104;
       if (q < 30) {
         const int* tr = kHT[q];
         const float* ph = p + 20;
@@ -118,22 +108,37 @@ __global__ __launch_bounds__(256) void pose_loss_bwd_kernel(const float* gen, in
         const float vx = ph[2 * tr[2]] - ph[2 * tr[1]], vy = ph[2 * tr[2] + 1] - ph[2 * tr[1] + 1];
         const float ang = atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
         const float g = (ang < 0.f ? -gh : 0.f) + (ang > kPi ? gh : 0.f);
-        angle_grad(ph, tr[0], tr[1], tr[2], g, a + 20);
+        tri_g[tt][q] = angle_grad(ph, tr[0], tr[1], tr[2], g);
       } else {
         const int* tr = kBT[q - 30];
         const float ux = p[2 * tr[1]] - p[2 * tr[0]], uy = p[2 * tr[1] + 1] - p[2 * tr[0] + 1];
         const float vx = p[2 * tr[2]] - p[2 * tr[1]], vy = p[2 * tr[2] + 1] - p[2 * tr[1] + 1];
         const float ang = atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
         const float g = (ang < -0.5f * kPi ? -gb : 0.f) + (ang > kPi ? gb : 0.f);
-        angle_grad(p, tr[0], tr[1], tr[2], g, a);
+        tri_g[tt][q] = angle_grad(p, tr[0], tr[1], tr[2], g);
       }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nt * 104; i += blockDim.x)
-      dgen[((int64_t)b * T + t0) * 104 + i] += acc[i];
+    for (int i = threadIdx.x; i < nt * 52; i += blockDim.x) {
+      const int tt = i / 52, j = i % 52;
+      float sx = 0.f, sy = 0.f;
+      if (j >= 1) { sx += bone_g[tt][j - 1].x; sy += bone_g[tt][j - 1].y; }
+      for (int c = 1; c < 52; ++c)
+        if (kPar[c] == j) { sx -= bone_g[tt][c - 1].x; sy -= bone_g[tt][c - 1].y; }
+      for (int q = 0; q < 35; ++q) {
+        const int* tr = q < 30 ? kHT[q] : kBT[q - 30];
+        const int off = q < 30 ? 10 : 0;   // the hand triples index joints from 10 (p + 20)
+        const float4 v = tri_g[tt][q];
+        if (tr[1] + off == j) { sx += v.x - v.z; sy += v.y - v.w; }
+        if (tr[0] + off == j) { sx -= v.x; sy -= v.y; }
+        if (tr[2] + off == j) { sx += v.z; sy += v.w; }
+      }
+      float* d = dgen + ((int64_t)b * T + t0 + tt) * 104 + 2 * j;
+      d[0] += sx;
+      d[1] += sy;
+    }
     __syncthreads();
   }
-  (void)red;
 }
 
 // motion terms on [B][T][F]; one workgroup per clip, partials to part[b][3]; dfake written

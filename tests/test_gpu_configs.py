@@ -206,10 +206,18 @@ def test_bf16_train_step_b32():
     losses, and gradient agreement (global cosine over the parameters whose true gradient is
     not identically zero -- conv biases ahead of train-mode BatchNorm and key biases under the
     softmax carry pure rounding noise -- and the median per-weight cosine); then one full
-    iteration with dropout in bf16: finite losses, parameters move."""
+    iteration with dropout in bf16: finite losses, parameters move.
+
+    Bounds (tools/bf16_grad_probe.py, profiles/r04_bf16_grad_probe.jsonl): bf16
+    GEMMs in the BACKWARD alone leave the G gradient at cosine 0.9999 (asserted >= 0.999).  In
+    the FORWARD every layer adds ~2^-8 of relative error (encoder 4e-3 per layer, 1.3e-2 after
+    the UNet's down path, 0.14 at the pose), and this G-step is ill-conditioned in the pose:
+    the fp32 step with the pose perturbed by 1e-3 of its magnitude already has cosine 0.973.
+    So the all-bf16 step sits at cosine ~0.51 (median ~0.56) -- asserted as a regression bound
+    (>= 0.45 / 0.50), not as agreement."""
     import a2m
     from a2m import autograd as AG
-    from a2m.training import GANTrainer
+    from a2m.training import GANTrainer, compute_temporal_smoothness_loss_and_jerk
     from oracle import synth
     from test_gpu_train import _bn_cancelled
     gen = torch.Generator().manual_seed(21)
@@ -231,6 +239,21 @@ def test_bf16_train_step_b32():
             dg = {n: p_.grad.detach().double().flatten().clone() for n, p_ in d.named_parameters()}
         assert torch.isfinite(gl) and torch.isfinite(dl)
         res[prec] = (gg, dg, gl.item(), dl.item(), {n: p_.dim() for n, p_ in list(g.named_parameters()) + list(d.named_parameters())})
+    # the G-step with an fp32 forward and a bf16 backward
+    g, d = _models(DEV)
+    tr = GANTrainer(g, d, lr=0.0, fixed_labels=(0.93, 0.07))
+    valid, _ = tr._labels(0, 32, DEV)
+    for p_ in d.parameters():
+        p_.requires_grad_(False)
+    fake_pose, internal = g(audio, real_pose=pose)
+    fake_d, _ = d(AG.pos_to_motion(fake_pose))
+    terms = compute_temporal_smoothness_loss_and_jerk(fake_pose, pose)
+    loss = terms[0] + tr.lambda_gan * AG.mse_loss(fake_d, valid) + 0.1 * terms[1] + 0.05 * terms[2]
+    for t in internal:
+        loss = loss + t
+    with a2m.gemm_precision('bf16'):
+        loss.backward()
+    gbw = {n: p_.grad.detach().double().flatten().clone() for n, p_ in g.named_parameters()}
 
     def agree(a, b, dims):
         names = [n for n in a if not _bn_cancelled(n) and a[n].norm() > 0]
@@ -241,11 +264,14 @@ def test_bf16_train_step_b32():
         return glob, med
     cg = agree(res['fp32'][0], res['bf16'][0], res['fp32'][4])
     cd = agree(res['fp32'][1], res['bf16'][1], res['fp32'][4])
-    print(f'B=32 bf16 vs fp32: G grad cosine global {cg[0]:.5f} weight-median {cg[1]:.5f}; D global '
-          f'{cd[0]:.5f} median {cd[1]:.5f}; G_loss {res["bf16"][2]:.5f} vs {res["fp32"][2]:.5f}, '
-          f'D_loss {res["bf16"][3]:.5f} vs {res["fp32"][3]:.5f}')
+    cb = agree(res['fp32'][0], gbw, res['fp32'][4])
+    print(f'B=32 bf16 vs fp32: G grad cosine global {cg[0]:.5f} weight-median {cg[1]:.5f}; bf16 backward '
+          f'only {cb[0]:.6f} / {cb[1]:.6f}; D global {cd[0]:.5f} median {cd[1]:.5f}; G_loss '
+          f'{res["bf16"][2]:.5f} vs {res["fp32"][2]:.5f}, D_loss {res["bf16"][3]:.5f} vs {res["fp32"][3]:.5f}')
     assert abs(res['bf16'][2] - res['fp32'][2]) < 1e-2 * abs(res['fp32'][2])
     assert abs(res['bf16'][3] - res['fp32'][3]) < 2e-2 * abs(res['fp32'][3])
+    assert cb[0] >= 0.999 and cb[1] >= 0.999, cb
+    assert cg[0] >= 0.45 and cg[1] >= 0.50, cg
     assert cd[0] > 0.99
     torch.manual_seed(0)
     from a2m.real_motion_model import SelfAttention_D, SelfAttention_G

@@ -7,6 +7,8 @@ agree with an fp64 convolution at fp32 accuracy, wrap nothing across clip bounda
 match the im2col path it replaces.  bf16x6 (three-way bf16 operand split, six products) must
 be fp32-class against fp64.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -153,6 +155,73 @@ def test_conv2d_nhwc_matches_fp64(B, Ci, Co, H, W, k, s, p, cols, out_nhwc):
     y = (y.permute(0, 3, 1, 2) if out_nhwc else y).cpu().double()
     e = rel_err(y[..., lo:hi], ref[..., lo:hi])
     assert e < TOL32, e
+
+
+def _bn_ref(y, bn, act, slope=0.2):
+    w, b_, rm, rv, eps = bn
+    sh = (1, -1, 1, 1)
+    z = (y - rm.double().view(sh)) / torch.sqrt(rv.double().view(sh) + eps) * w.double().view(sh) + b_.double().view(sh)
+    return torch.where(z > 0, z, slope * z) if act else z
+
+
+def test_conv2d_nhwc_unaligned_input_takes_run_loader():
+    """An input that is 4- but not 16-byte aligned (a view one float into a buffer) with Ci a
+    multiple of the k-tile: the float4 channel-run loader (mode 6) needs 16-byte alignment, so
+    the conv takes the k-run loader (mode 4) and still matches fp64."""
+    from a2m import functional as F
+    g = torch.Generator().manual_seed(7)
+    B, Ci, Co, H, W = 2, 64, 128, 16, 20
+    x = torch.randn(B, Ci, H, W, generator=g)
+    w = torch.randn(Co, Ci, 4, 4, generator=g) / np.sqrt(Ci * 16)
+    b = torch.randn(Co, generator=g)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride=2, padding=1)
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    buf = torch.empty(xn.numel() + 1, device=DEV)
+    xv = buf[1:].view(xn.shape)
+    xv.copy_(xn.to(DEV))
+    assert xv.data_ptr() % 16 == 4
+    y = F.conv2d_nhwc(xv, w.to(DEV), b.to(DEV), 2, (1, 1), cache={})
+    assert rel_err(y.permute(0, 3, 1, 2).cpu().double(), ref) < TOL32
+
+
+@pytest.mark.parametrize('Co,stride,act,mfma', [(64, 1, True, 1), (1024, 2, True, 1), (64, 2, False, 0),
+                                                (1024, 1, True, 0), (96, 2, True, 1)])
+def test_conv2d_c1_bn_act_stride(Co, stride, act, mfma):
+    """The encoder's Ci = 1 first conv (4 x 4) in its direct kernels -- the MFMA one
+    (conv2d_c1_mfma_kernel, default for channels-last outputs) and, with A2M_C1_MFMA=0, the VALU
+    one -- at stride 1 and 2, with the BatchNorm-eval affine and LeakyReLU epilogue, and at
+    Co = 1024, against fp64."""
+    import subprocess
+    import sys
+    import json
+    env = dict(os.environ, A2M_C1_MFMA=str(mfma))
+    code = (
+        'import sys, json, torch, numpy as np; sys.path[:0] = %r\n'
+        'from test_gpu_tapconv import _c1_case\n'
+        'print(json.dumps(_c1_case(%d, %d, %r)))\n' % ([os.path.dirname(os.path.abspath(__file__))], Co, stride, act))
+    p = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-3000:]
+    e = json.loads(p.stdout.strip().splitlines()[-1])
+    assert e < TOL32, e
+
+
+def _c1_case(Co, stride, act):
+    """(child process: A2M_C1_MFMA is read once per process) conv0-shaped conv vs fp64."""
+    import conftest  # noqa: F401  (sys.path for the package)
+    from a2m import functional as F
+    g = torch.Generator().manual_seed(Co + stride)
+    B, H, W = 3, 64, 128
+    x = torch.randn(B, 1, H, W, generator=g) * 2 - 3
+    w = torch.randn(Co, 1, 4, 4, generator=g) / 4
+    b = torch.randn(Co, generator=g)
+    bn = (torch.rand(Co, generator=g) + 0.5, torch.randn(Co, generator=g), torch.randn(Co, generator=g) * 0.1,
+          torch.rand(Co, generator=g) + 0.5, 1e-5)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=1)
+    ref = _bn_ref(ref, bn, act)
+    y = F.conv2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), w.to(DEV), b.to(DEV), stride, (1, 1),
+                      bn=tuple(t.to(DEV) for t in bn[:4]) + (bn[4],), act=F.ACT_LRELU if act else F.ACT_NONE,
+                      cache={})
+    return rel_err(y.permute(0, 3, 1, 2).cpu().double(), ref)
 
 
 @pytest.mark.parametrize('B,T,split', [(64, 64, 0), (3, 64, 1), (2, 480, 0), (1, 33, 0), (5, 100, 3)])
