@@ -124,6 +124,7 @@ SIGNATURES = {
     'a2m_get_gemm_precision': (I32, []),
     'a2m_gemm_timing_end': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
                                            ctypes.POINTER(F64), ctypes.POINTER(I64)]),
+    'a2m_bct_to_btc_f32': (ctypes.c_int, [P, I64, I32, I32, I32, P, P]),
     'a2m_gemm_timing_stop': (ctypes.c_int, []),
     'a2m_gemm_timing_clear': (ctypes.c_int, []),
     'a2m_gemm_timing_read_spans': (ctypes.c_int, [I64, ctypes.POINTER(F64), ctypes.POINTER(F64),

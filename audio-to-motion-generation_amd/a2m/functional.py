@@ -308,6 +308,18 @@ def conv2d_nhwc_interp(x, w, b, stride, pad, T, col, bn=None, act=ACT_NONE, slop
     return out
 
 
+def bct_to_btc(x, out=None):
+    """[B, C, T] (channel stride T) -> [B, T, C] contiguous (a2m_bct_to_btc_f32, T <= 64)."""
+    _check_dev(x, out)
+    B, C, T = x.shape
+    assert x.stride(2) == 1 and x.stride(1) == T
+    if out is None:
+        out = torch.empty(B, T, C, device=x.device, dtype=x.dtype)
+    assert out.is_contiguous() and tuple(out.shape) == (B, T, C)
+    N.check(N.lib.a2m_bct_to_btc_f32(_p(x), x.stride(0), B, C, T, _p(out), _stream()))
+    return out
+
+
 def interp_time(x, T, out=None):
     _check_dev(x)
     assert x.is_contiguous()

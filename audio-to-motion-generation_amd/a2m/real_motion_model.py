@@ -100,7 +100,14 @@ class SelfAttention_G(_GraphTopology):
         nj = getattr(self, f'num_{part}_joints')
         pin, pout = getattr(self, f'{part}_proj_in'), getattr(self, f'{part}_proj_out')
         h = torch.empty(B, T, nj * 64, device=x.device)
-        F.conv1d(x, pin.weight, pin.bias, out=h.permute(0, 2, 1))
+        if _PROJ_DENSE and x.stride(2) == 1 and x.stride(1) == T and T <= 64:
+            # A2M_PROJ_DENSE: x first copied to [B*T][C] rows, so the projection's activation
+            # operand is dense k-contiguous rows (loader mode 0) instead of t-runs (mode 3);
+            # the output is the node layout [B, T, J*64] either way
+            xt = F.bct_to_btc(x)
+            F.gemm(nj * 64, B * T, C, pin.weight, C, 1, xt, C, 1, h, 1, nj * 64, bias=pin.bias)
+        else:
+            F.conv1d(x, pin.weight, pin.bias, out=h.permute(0, 2, 1))
         a, b = h.view(B * T * nj, 64), torch.empty(B * T * nj, 64, device=x.device)
         ptr, idx = self.topology(part)
         lns = getattr(self, f'{part}_layer_norms')
@@ -270,7 +277,18 @@ class SelfAttention_G(_GraphTopology):
             main = torch.cuda.current_stream(audio.device)
             side = _side_stream(audio.device)
             side.wait_stream(main)
-            if _HAND_FIRST:
+            if _TWO_SIDES:
+                # A2M_TWO_SIDES: each branch on its own side stream, both forked from and joined
+                # to the caller's (experiment: how the graph executor places the branches)
+                side2 = _side_stream(audio.device, 1)
+                side2.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._branch('hand', feats, out, self.body_feats)
+                with torch.cuda.stream(side2):
+                    self._branch('body', feats, out, 0)
+                main.wait_stream(side)
+                main.wait_stream(side2)
+            elif _HAND_FIRST:
                 # the hand branch (42-joint graph stack) is the longer one; forked first, on the
                 # side stream (measured 2.96 vs 3.00 ms a step; a high-priority side stream
                 # (A2M_SIDE_PRIO=1) measured 4.8 ms)
@@ -281,7 +299,8 @@ class SelfAttention_G(_GraphTopology):
                 with torch.cuda.stream(side):
                     self._branch('body', feats, out, 0)
                 self._branch('hand', feats, out, self.body_feats)
-            main.wait_stream(side)
+            if not _TWO_SIDES:
+                main.wait_stream(side)
         else:
             self._branch('body', feats, out, 0)
             self._branch('hand', feats, out, self.body_feats)
@@ -331,15 +350,17 @@ def _group_sources(m):
         return (m.conv.weight, m.conv.bias, n.weight, n.bias, n.running_mean, n.running_var)
     return m.weights()   # SelfAttention
 _FUSED_STACK = os.environ.get('A2M_GRAPH_STACK', '1') != '0'   # one launch for the 5 graph layers
+_PROJ_DENSE = os.environ.get('A2M_PROJ_DENSE', '0') != '0'
 _SIDE_STREAMS = {}
 
 
 _HAND_FIRST = os.environ.get('A2M_HAND_FIRST', '1') != '0'
 _SIDE_PRIO = os.environ.get('A2M_SIDE_PRIO', '0') != '0'
+_TWO_SIDES = os.environ.get('A2M_TWO_SIDES', '0') != '0'
 
 
-def _side_stream(device):
-    key = device.index or 0
+def _side_stream(device, which=0):
+    key = (device.index or 0, which)
     s = _SIDE_STREAMS.get(key)
     if s is None:
         prio = torch.cuda.Stream.priority_range()[1] if _SIDE_PRIO else 0   # highest

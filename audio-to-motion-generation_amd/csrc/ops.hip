@@ -1342,6 +1342,17 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
   return gemm(Av, Ba, Eo, C, T, T, B, ws, ws_bytes, st);
 }
 
+int a2m_bct_to_btc_f32(const float* x, int64_t xs_b, int32_t B, int32_t C, int32_t T, float* y,
+                       void* stream) {
+  A2M_CHECK_ARG(x && y && B > 0 && C > 0 && T > 0 && T <= TR_MAXT && xs_b >= (int64_t)C * T,
+                "bct_to_btc: bad shape (T <= %d)", TR_MAXT);
+  A2M_CHECK_ARG(fits32((int64_t)B * xs_b) && fits32((int64_t)B * T * C), "bct_to_btc: too large");
+  hipLaunchKernelGGL(bct_to_btc_kernel, dim3((unsigned)cdiv(C, TR_C), (unsigned)B), dim3(256), 0,
+                     as_stream(stream), x, xs_b, C, T, y);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
 int32_t a2m_self_attention_eval_fits(int32_t C, int32_t T) { return attn_fused_eval_fits(C, T) ? 1 : 0; }
 
 int a2m_self_attention_eval_group_f32(const float* x, int64_t x_gs, int64_t x_bs, int32_t G, int32_t B,

@@ -180,6 +180,12 @@ int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t
 
 /* F.interpolate(x, size=(T,1), mode='bilinear', align_corners=False).squeeze(-1)
  * (model_layers.py:277-279) on x [B][C][H][W] -> y [B][C][T]. */
+/* y[b][t][c] = x[b][c][t] (x channel stride T, batch stride xs_b; T <= 64): the [B*T][C]
+ * row layout of an activation for GEMMs that want it as dense k-contiguous rows (the UNet's
+ * wide attentions do this internally; the decoders' graph-stack input projection,
+ * real_motion_model.py:173-176).  No reference counterpart: a layout change. */
+int a2m_bct_to_btc_f32(const float* x, int64_t xs_b, int32_t B, int32_t C, int32_t T, float* y,
+                       void* stream);
 int a2m_interp_time_f32(const float* x, int32_t B, int32_t C, int32_t H, int32_t W,
                         float* y, int32_t T, void* stream);
 
