@@ -65,9 +65,10 @@ __device__ __forceinline__ float interp_time_at(const float* p, int H, int W, in
   return v;
 }
 
-// One thread per four consecutive t of a (b, c) row (T % 4 == 0, 32-bit indexing): float4
-// stores; otherwise one output per thread.
-__global__ void interp_time_kernel(const float* x, int B, int C, int H, int W, float* y, int T) {
+// vec: one thread per four consecutive t of a (b, c) row (host: T % 4 == 0, y 16-byte aligned,
+// B*C*T < 2^31 for the 32-bit indexing): float4 stores; otherwise one output per thread with
+// 64-bit indexing and no alignment requirement.
+__global__ void interp_time_kernel(const float* x, int B, int C, int H, int W, float* y, int T, int vec) {
   const float sh = (float)H / (float)T;
   const float sw = (float)W / 1.0f;
   float srcw = sw * 0.5f - 0.5f;
@@ -75,7 +76,7 @@ __global__ void interp_time_kernel(const float* x, int B, int C, int H, int W, f
   const int w0 = (int)srcw;
   const int w1 = w0 + (w0 < W - 1 ? 1 : 0);
   const float lw1 = srcw - (float)w0, lw0 = 1.f - lw1;
-  if ((T & 3) == 0) {
+  if (vec) {
     const int T4 = T >> 2;
     const int total4 = B * C * T4;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
@@ -1249,12 +1250,12 @@ int a2m_repeat_time_f32(const float* x, int32_t B, int32_t C, int32_t T, float s
 int a2m_interp_time_f32(const float* x, int32_t B, int32_t C, int32_t H, int32_t W, float* y,
                         int32_t T, void* stream) {
   A2M_CHECK_ARG(x && y && B > 0 && C > 0 && H > 0 && W > 0 && T > 0, "interp: bad args");
-  A2M_CHECK_ARG((int64_t)B * C * T < (1LL << 31) && (reinterpret_cast<uintptr_t>(y) & 15) == 0,
-                "interp: too large or y not 16-byte aligned");
-  const int64_t total = (int64_t)B * C * T / ((T & 3) == 0 ? 4 : 1);
+  const int vec = (T & 3) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0 &&
+                  (int64_t)B * C * T < (1LL << 31);
+  const int64_t total = (int64_t)B * C * T / (vec ? 4 : 1);
   const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
   hipLaunchKernelGGL(interp_time_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, B, C,
-                     H, W, y, T);
+                     H, W, y, T, vec);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

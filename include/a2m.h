@@ -320,7 +320,9 @@ int a2m_pose_losses_w_f32(const float* gen, int64_t gs_b, int64_t gs_t, const fl
  * drop_mode: 0 none, 1 element dropout before BN (ConvNormRelu 1-d, model_layers.py:118),
  * 2 channel dropout before BN (Dropout2d, 2-d ConvNormRelu), 3 element dropout after the
  * activation (discriminator blocks, real_motion_model.py:504-551).  Masks are a hash of
- * (seed, element index) and are regenerated by the backward pass. */
+ * (seed, element index) and are regenerated by the backward pass.  Limit: B * L < 2^31
+ * elements per channel (32-bit slice indexing; A2M_EINVAL beyond -- such a channel alone
+ * would be 8 GB, more than any tensor of this model at any batch that fits one GPU). */
 int a2m_bn_train_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C,
                          int32_t L, const float* gamma, const float* beta, float* running_mean,
                          float* running_var, float momentum, float eps, float drop_p,
