@@ -741,7 +741,15 @@ int a2m_gemm_timing_clear(void) {
 // graph re-stamps on every replay.  Its own dispatch is ~1-2 us of the interval it opens.
 int a2m_timing_mark(int32_t slot, void* stream) {
   A2M_CHECK_ARG(slot >= 0 && slot < A2M_TIMING_MARKS, "timing_mark: slot %d", slot);
-  A2M_CHECK_ARG(a2m::g_ts != nullptr, "timing_mark: call a2m_gemm_timing_begin first (stamp buffer)");
+  if (!a2m::g_ts) {   // allocate the stamp buffer here unless the stream is being captured
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    A2M_CHECK_ARG(hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cs) == hipSuccess &&
+                      cs == hipStreamCaptureStatusNone,
+                  "timing_mark: first mark inside a stream capture (call a2m_gemm_timing_begin first)");
+    std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+    const int rc = a2m::timing_alloc();
+    if (rc != A2M_OK) return rc;
+  }
   hipLaunchKernelGGL(a2m::timing_mark_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
                      a2m::g_ts + (size_t)a2m::kTimingRecs * a2m::kRecSlots + slot);
   A2M_LAUNCH_CHECK();

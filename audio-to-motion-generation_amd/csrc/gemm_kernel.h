@@ -225,6 +225,9 @@ struct TileLoader {
   static constexpr int T5 = 3;
   int o5[MODE == 5 && !H ? T5 : 1][4];
   int ok5;
+  // mode 6: the tap (i6, j6) and channel offset c6 of k-tile k6 (the next load's, normally):
+  // advanced by whole k-tiles instead of dividing k0 by Ci and the tap by kw every k-step
+  int k6, i6, j6, c6;
   KPos kp[NKP];   // k position of each of this thread's k groups at the next load (modes 1-3)
   KPos kstep;     // BK in (k0, k1, k2) digits
   float r[NREG];
@@ -287,6 +290,13 @@ struct TileLoader {
         if (MODE == 6) ri[p].base += (ri[p].h * gg.Lw + ri[p].w) * gg.nhwc;
       }
       kq = (tid % QPR) * 4;
+      if (MODE == 6) {
+        const int tap = kbeg / gg.nhwc;
+        k6 = kbeg;
+        c6 = kbeg - tap * gg.nhwc;
+        i6 = tap / gg.K2;
+        j6 = tap - i6 * gg.K2;
+      }
     }
     if (MODE != 0 && MODE != 6) {
       kstep = kpos(gg, kstride);
@@ -326,9 +336,17 @@ struct TileLoader {
       }
     } else if (MODE == 6) {
       const int Ci = g->nhwc;
-      const int tap = k0 / Ci, ci0 = k0 - tap * Ci;   // uniform: scalar arithmetic
-      const int i = tap / g->K2, j = tap - i * g->K2;
-      const int toff = (i * g->Lw + j) * Ci + ci0 + kq;
+      // k0 comes in whole k-tiles after k6 (one for the one-group tile); Ci % BK == 0 (host)
+      while (k6 < k0) {
+        k6 += BK;
+        c6 += BK;
+        if (c6 == Ci) {
+          c6 = 0;
+          if (++j6 == g->K2) { j6 = 0; ++i6; }
+        }
+      }
+      const int i = i6, j = j6;
+      const int toff = (i * g->Lw + j) * Ci + c6 + kq;
 #pragma unroll
       for (int p = 0; p < NPASS; ++p) {
         const int h = ri[p].h + i, w = ri[p].w + j;
@@ -966,7 +984,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
+        read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
       }
     } else
     for (int i = 0; i < nk; ++i) {
@@ -1005,7 +1023,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       if (args.prio) __builtin_amdgcn_s_setprio(1);
       if (A2M_ABLATE != 1) mfma_part<0, SPLIT>(f1, acc);
       __builtin_amdgcn_sched_barrier(0);
-      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
+      // unconditional (after the last k-step the stale stage is read and never used): behind a
+      // branch the compiler split these reads (b96 / b32 / read2 + moves, a wait inside the
+      // MFMA cluster) and, not knowing how many were in flight after the join, waited for all
+      // of them (lgkmcnt(0)) before this half's remaining MFMAs
+      read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
       __builtin_amdgcn_sched_barrier(0);
       if (A2M_ABLATE != 1) mfma_part<SPLIT, NSUB>(f1, acc);
       else ablate_touch(f1, acc);
@@ -1075,7 +1097,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       else ablate_touch(f, acc);
       if (args.prio) __builtin_amdgcn_s_setprio(0);
       if (A2M_ABLATE != 3) __syncthreads();
-      if (i + 1 < nk) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, grp, wm, wn, li, lh, f);
+      read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, grp, wm, wn, li, lh, f);
     }
     // sum the two groups' partial accumulators (group 1 -> LDS -> group 0)
     __syncthreads();
