@@ -510,8 +510,6 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   a.xcd_group = gemm_xcd_group();
   static const int skew = env_int("A2M_GEMM_KS3_SKEW", 1);
   a.skew = skew;
-  static const int prio = env_int("A2M_GEMM_PRIO", 0);
-  a.prio = prio;
   static const int stage_m = env_int("A2M_GEMM_MCONTIG", 1);
   // fused resample (E.interp_T): the tile always writes raw slabs (also at one split) and the
   // reduce kernel runs epilogue + resample

@@ -41,8 +41,6 @@ struct GemmArgs {
   int mcontig;     // output has unit m stride: the tile is staged through LDS and written
                    // along m (split-K slabs then are [N][M])
   int skew;        // KS = 3: wave group 1 runs its k-steps half a step after group 0's
-  int prio;        // A2M_GEMM_PRIO (experiment): 1 = s_setprio 1 around each k-step's MFMA
-                   // clusters (the arbiter favours a wave about to feed the matrix pipe)
   unsigned long long* ts;   // measurement only (a2m_gemm_timing_*; null otherwise): this launch's
                             // span stamps, [tile | reduce][XCD][first start, last end]
 };
@@ -914,6 +912,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
     by = first_m + in % gsz;
     bx = in / gsz;
   }
+  // block-uniform values kept in SGPRs (readfirstlane): the k-loop's tile-count branches then
+  // compile to scalar branches instead of exec-masked regions
+  bx = __builtin_amdgcn_readfirstlane(bx);
+  by = __builtin_amdgcn_readfirstlane(by);
+  bz = __builtin_amdgcn_readfirstlane(bz);
   const int zz = bz;
   const int batch = zz / args.splits, split = zz % args.splits;
   const int m0 = by * BM, n0 = bx * BN;
@@ -943,7 +946,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 
-  const int nk = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
+  const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
   if constexpr (KS == 1 || KS == 3) {
     Frags<TM, TN, P, NS> f0, f1;
     if (nk > 0) {
@@ -1000,10 +1003,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
         lb.load(kbeg + (i + 2) * BK);
       }
       read_frags<BM, BN, TM, TN, P, NS, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
-      if (args.prio) __builtin_amdgcn_s_setprio(1);
       if (A2M_ABLATE != 1) mfma_half(f0, acc);
       else ablate_touch(f0, acc);
-      if (args.prio) __builtin_amdgcn_s_setprio(0);
       // The step's barrier, pinned after the first half's MFMAs (left to itself the compiler
       // hoists it above them, and __syncthreads' fence would also wait for the second half's
       // fragment reads).  Only this wave's tile stores must have landed: LDS ops retire in
@@ -1020,7 +1021,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       // cannot tell them apart from the second half's own reads in the LDS counter)
       constexpr int SPLIT = P == 1 ? 1 : 2;
       constexpr int NSUB = P == 0 ? 8 * NS : (P == 1 ? 2 : 6);
-      if (args.prio) __builtin_amdgcn_s_setprio(1);
       if (A2M_ABLATE != 1) mfma_part<0, SPLIT>(f1, acc);
       __builtin_amdgcn_sched_barrier(0);
       // unconditional (after the last k-step the stale stage is read and never used): behind a
@@ -1031,7 +1031,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       __builtin_amdgcn_sched_barrier(0);
       if (A2M_ABLATE != 1) mfma_part<SPLIT, NSUB>(f1, acc);
       else ablate_touch(f1, acc);
-      if (args.prio) __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();  // the m-contiguous epilogue reuses the stages
     if constexpr (KS == 3) {   // group 1's partial accumulators -> LDS -> group 0
@@ -1092,10 +1091,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
           lb.load(kbeg + (i + 3) * BK);
         }
       }
-      if (args.prio) __builtin_amdgcn_s_setprio(1);
       if (A2M_ABLATE != 1) mfma_half(f, acc);
       else ablate_touch(f, acc);
-      if (args.prio) __builtin_amdgcn_s_setprio(0);
       if (A2M_ABLATE != 3) __syncthreads();
       read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, grp, wm, wn, li, lh, f);
     }

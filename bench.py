@@ -165,12 +165,15 @@ def gemm_engine_timing(step):
     return t
 
 
-def instep_timing(dev, g, wave, reps=20):
+def instep_timing(dev, g, wave, reps=20, warm=None):
     """The bench step captured once more with the engine's span stamps on (every implicit-GEMM
     launch stamps its own first-block start / last-wave end; nothing is added between kernels,
     so the two decoder branches overlap exactly as in the timed graph) and three wall-clock
     mark kernels (step start, after the log-mel, after the encoder); the graph is replayed
-    `reps` times and each replay read back.  Returns per-step means: the engine's launches /
+    `reps` times and each replay read back; `warm` (three replays of the timed bench graph) runs
+    right before each of those replays, so that each timed replay follows back-to-back work as
+    in the timed loop instead of an idle, clocked-down GPU after the previous read's sync.
+    Returns per-step means: the engine's launches /
     FLOPs / tile ms / reduce ms, and the step's log-mel and log-mel + encoder phases (ms).
     This is the basis of `roofline` and of `mel_encoder_roofline.path_frac_instep`;
     tools/step_pmc.sh's rocprof kernel trace of the replayed bench graph is its cross-check
@@ -201,6 +204,8 @@ def instep_timing(dev, g, wave, reps=20):
         torch.cuda.synchronize()
         t.read()                     # discard the warm-up replay's stamps (re-arms them)
         for _ in range(reps):
+            if warm is not None:
+                warm()
             graph.replay()
             torch.cuda.synchronize()
             t.read()
@@ -481,7 +486,8 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0):
             'traffic': tr['bytes_per_launch'] if tr else None,
             'traffic_source': tr['source'] if tr else None,
             'basis': 'in-step: the bench graph re-captured with the engine launches stamping their own '
-                     'spans (first block start .. last block end, GPU wall clock), replayed 20 times, '
+                     'spans (first block start .. last block end, GPU wall clock), replayed 20 times '
+                     '(each after three back-to-back replays of the timed graph), '
                      'plus the measured per-launch dispatch overhead (dispatch_ms_per_launch) that a '
                      'kernel trace counts in each kernel; cross-check: rocprof kernel trace of replayed '
                      'steps only (tools/step_pmc.sh, profiles/)',
@@ -612,7 +618,8 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         value = world * B * T / (elapsed / args.steps)
         gt = gemm_engine_timing(step)
-        it = instep_timing(dev, g, wave)
+        warm = None if graph is None else (lambda: [run() for _ in range(3)])
+        it = instep_timing(dev, g, wave, warm=warm)
         disp_ms = dispatch_overhead_ms(dev)
         mel_ms, mel_bytes = run_mel_kernel(dev, wave)
         mel_enc = mel_encoder_roofline(dev, g, wave, mel_ms, mel_bytes, mfma_peak(args.dtype))
