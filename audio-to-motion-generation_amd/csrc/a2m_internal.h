@@ -69,6 +69,9 @@ struct Gather {
                 // (chunk, tap, ci) with BK-channel chunks, rows n = b*R2 + t; the chunk's
                 // x[b][c][t] window is loaded once and re-stored shifted for each of the
                 // `tapconv` taps (sr0 = batch stride, sk0 = channel stride, cw = -pad)
+  int halo;     // set by the engine (not the caller): mode 5 with 3 taps, pad 1, R2 >= 16 on the
+                // fp32 64x64 one-group tile stores the window once with zero rows around each
+                // clip and reads each tap at a row shift (gemm_kernel.h, TileLoader::store_h)
 };
 
 inline Gather dense_rk(const float* p, int ld, int64_t bstride = 0) {  // [R][K] row-major, ld >= K

@@ -504,6 +504,10 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                   (ks3 >= 2 && p.splits == 2 && force_split <= 0 && g_override_split == 0 &&
                    (mb == 0 || mb == 3 || mb == 5)));
   if (use_ks3) { p.splits = 1; p.kchunk = nt_all * p.bk; }
+  // A2M_GEMM_HALO=0: mode 5 re-stores the window shifted for every tap (the round-3 loader)
+  static const int halo_on = env_int("A2M_GEMM_HALO", 1);
+  a.B.halo = halo_on && mb == 5 && prec == 0 && p.bm == 64 && !use_ks3 && B.tapconv == 3 &&
+             B.cw == -1 && B.R2 >= 16 && 64 % B.R2 == 0;
   a.splits = p.splits;
   a.kchunk = p.kchunk;
   a.partial = nullptr;

@@ -223,6 +223,12 @@ struct TileLoader {
   static constexpr int T5 = 3;
   int o5[MODE == 5 && !H ? T5 : 1][4];
   int ok5;
+  // halo layout (Gather::halo; fp32, 3 taps, pad 1, clips T >= 16): the chunk's x window is
+  // stored ONCE, at rows hrow(n) = (n / T) (T + 2) + 1 + n % T of its own LDS stage, with a zero
+  // row before and after every clip; tap j reads it shifted by j - 1 rows
+  static constexpr int HR = BR + 2 * (BR / 16);   // rows of a halo stage (T >= 16)
+  static constexpr int TILE_H = HR * LDK;
+  int h5[MODE == 5 && !H ? 4 : 1];
   // mode 6: the tap (i6, j6) and channel offset c6 of k-tile k6 (the next load's, normally):
   // advanced by whole k-tiles instead of dividing k0 by Ci and the tap by kw every k-step
   int k6, i6, j6, c6;
@@ -250,6 +256,14 @@ struct TileLoader {
       st_tap = ld_tap = st_j % gg.tapconv;
       ld_cc = st_j / gg.tapconv;
       if constexpr (!H) {
+        if (gg.halo) {
+          const int T = gg.R2;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int n = lrow[0] + e;   // tile row (whole clips per tile: n / T is the clip)
+            h5[e] = ((n / T) * (T + 2) + 1 + n % T) * LDK + kq;
+          }
+        }
         ok5 = 0;
 #pragma unroll
         for (int t = 0; t < T5; ++t)
@@ -443,6 +457,16 @@ struct TileLoader {
         }
         r[p * 4 + 0] = v.x; r[p * 4 + 1] = v.y; r[p * 4 + 2] = v.z; r[p * 4 + 3] = v.w;
       }
+    }
+  }
+
+  // halo layout: the tap-0 registers of the chunk to their unshifted rows (rows past R hold 0)
+  __device__ __forceinline__ void store_h(float* lds) {
+    if constexpr (MODE == 5 && !H) {
+#pragma unroll
+      for (int p = 0; p < NP3; ++p)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) lds[h5[e] + p * KPP] = r[p * 4 + e];
     }
   }
 
@@ -881,7 +905,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
   using LA = TileLoader<BM, BK, MA, P>;
   using LB = TileLoader<BN, BK, MB, P>;
   constexpr int STAGE = LA::TILE + LB::TILE;
-  __shared__ __attribute__((aligned(16))) float lds_all[(KS == 3 ? 4 : 2) * STAGE];
+  // mode-5 halo layout: two A stages + two chunk-wide B stages (tile_halo below)
+  constexpr bool HALO = MB == 5 && P == 0 && KS == 1 && BN == 64;
+  constexpr int LDS_F = (KS == 3 ? 4 : 2) * STAGE;
+  constexpr int LDS_H = HALO ? 2 * LA::TILE + 2 * LB::TILE_H : 0;
+  __shared__ __attribute__((aligned(16))) float lds_all[LDS_F > LDS_H ? LDS_F : LDS_H];
   __shared__ EpiRow epr[BM];   // the block's per-row epilogue constants (final-output launches)
   static_assert(KS == 1 || (TM * TN * 16 * 256 <= 2 * STAGE), "KS = 2 partials must fit the stages");
   const int grp = KS == 1 ? 0 : (int)(threadIdx.x >> 8);
@@ -947,7 +975,78 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
+  bool halo_done = false;
+  if constexpr (HALO) {
+    if (args.B.halo) {
+      // Tap-chunked conv1d with the halo B layout (LB::store_h): per channel chunk the x window
+      // is loaded AND stored once; the chunk's three k-tiles (taps) read it at row shifts -1, 0,
+      // +1 (a lane's B rows move by its clip's halo offset too), so taps 1 and 2 store only A.
+      // A keeps its k-tile-parity stages; B has chunk-parity stages after them.
+      const int T = args.B.R2;
+      float* const bst0 = lds + 2 * LA::TILE;
+      // zero rows of both B stages: rows c (T + 2) and c (T + 2) + T + 1 of every clip c
+      {
+        const int nclip = BN / T;
+        for (int idx = tid; idx < 2 * nclip * 2 * LB::LDK; idx += 256) {
+          const int col = idx % LB::LDK, q = idx / LB::LDK;
+          const int which = q & 1, clip = (q >> 1) % nclip, stage = (q >> 1) / nclip;
+          bst0[stage * LB::TILE_H + (clip * (T + 2) + (which ? T + 1 : 0)) * LB::LDK + col] = 0.f;
+        }
+      }
+      const int brow = wn * (BN / 2) + li;          // this lane's B fragment row (TN = 1)
+      const int bsh = 2 * (brow / T) + 1;           // its halo row offset at tap shift 0
+      const int ntap = args.B.tapconv;              // 3 (host)
+      int tap_i = (kbeg / BK) % ntap;               // tap / chunk parity of k-tile i
+      int cpar = 0;
+      auto bfrag = [&](int tap, int par) { return bst0 + par * LB::TILE_H + (bsh + tap - 1) * LB::LDK; };
+      Frags<TM, TN, P, NS> f0, f1;
+      if (nk > 0) {
+        la.load(kbeg);
+        lb.load(kbeg);
+        la.store(lds);
+        lb.store_h(bst0);
+        if (nk > 1) {
+          la.load(kbeg + BK);
+          lb.load(kbeg + BK);
+        }
+      }
+      __syncthreads();
+      if (nk > 0) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(lds, bfrag(tap_i, 0), 0, wm, wn, li, lh, f0);
+      for (int i = 0; i < nk; ++i) {
+        const float* cur = lds + (i & 1) * LA::TILE;
+        float* nxt = lds + ((i + 1) & 1) * LA::TILE;
+        const int tap_n = tap_i + 1 == ntap ? 0 : tap_i + 1;   // tile i + 1
+        const int cpar_n = tap_n == 0 ? cpar ^ 1 : cpar;
+        if (i + 1 < nk) {
+          la.store(nxt);
+          if (tap_n == 0) lb.store_h(bst0 + cpar_n * LB::TILE_H);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (i + 2 < nk) {
+          la.load(kbeg + (i + 2) * BK);
+          lb.load(kbeg + (i + 2) * BK);
+        }
+        read_frags<BM, BN, TM, TN, P, NS, LA, LB>(cur, bfrag(tap_i, cpar), 1, wm, wn, li, lh, f1);
+        mfma_half(f0, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int RD = 2 * NS * (TM + TN);
+        __builtin_amdgcn_s_waitcnt(0xC07F | ((RD < 15 ? RD : 15) << 8));
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_part<0, 2>(f1, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, bfrag(tap_n, cpar_n), 0, wm, wn, li, lh, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_part<2, 8 * NS>(f1, acc);
+        tap_i = tap_n;
+        cpar = cpar_n;
+      }
+      __syncthreads();  // the m-contiguous epilogue reuses the stages
+      halo_done = true;
+    }
+  }
   if constexpr (KS == 1 || KS == 3) {
+   if (!halo_done) {
     Frags<TM, TN, P, NS> f0, f1;
     if (nk > 0) {
       la.load(kbeg);
@@ -1057,6 +1156,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
         return;
       }
     }
+   }
   } else {
     // The groups take turns staging: group j % 2 loads k-tile j three steps ahead and stores it
     // one step ahead, so a tile's global loads have two k-steps to land (one with a single

@@ -52,6 +52,54 @@ def test_tap_conv1d_matches_fp64(prec, B, Ci, Co, T, k):
     assert e < TOL32, e
 
 
+_HALO_CASES = [(64, 256, 256, 64), (8, 512, 1024, 32), (5, 1024, 2048, 16), (1, 256, 512, 16),
+               (3, 128, 64, 16), (16, 256, 128, 64)]
+
+
+def _tap_cases():
+    """(both processes) the tap-path outputs of _HALO_CASES (the last with the BN + LeakyReLU
+    epilogue), on seeded inputs."""
+    from a2m import functional as F
+    outs = []
+    for i, (B, Ci, Co, T) in enumerate(_HALO_CASES):
+        g = torch.Generator().manual_seed(100 + i)
+        x = torch.randn(B, Ci, T, generator=g).to(DEV)
+        w = (torch.randn(Co, Ci, 3, generator=g) / np.sqrt(3 * Ci)).to(DEV)
+        b = torch.randn(Co, generator=g).to(DEV)
+        kw = {}
+        if i == len(_HALO_CASES) - 1:
+            kw = dict(bn=tuple(t.to(DEV) for t in (torch.rand(Co, generator=g) + 0.5, torch.randn(Co, generator=g),
+                                                   torch.randn(Co, generator=g) * 0.1,
+                                                   torch.rand(Co, generator=g) + 0.5)) + (1e-5,),
+                      act=F.ACT_LRELU, slope=0.2)
+        cache = {}
+        outs.append(F.conv1d(x, w, b, 1, 1, cache=cache, **kw).cpu())
+        assert 'w' in cache, 'tap path not taken'
+    return outs
+
+
+def test_tap_conv1d_halo_layout_bitwise(tmp_path):
+    """The halo B layout (3 taps, pad 1, clips of T >= 16: the window stored once with a zero row
+    around every clip, each tap read at a row shift; the default) feeds the MFMAs the same
+    operands in the same order as the per-tap re-stored window (A2M_GEMM_HALO=0, computed in a
+    child process since the switch is read once): bit-identical outputs, including ragged
+    batches (B = 5 clips of 16 leave a partial tile), split-K plans and the BN epilogue."""
+    import subprocess
+    import sys
+    out = str(tmp_path / 'nohalo.pt')
+    code = ('import sys, torch; sys.path[:0] = %r\n'
+            'import conftest\n'
+            'from test_gpu_tapconv import _tap_cases\n'
+            'torch.save(_tap_cases(), %r)\n' % ([os.path.dirname(os.path.abspath(__file__))], out))
+    p = subprocess.run([sys.executable, '-c', code], env=dict(os.environ, A2M_GEMM_HALO='0'),
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-3000:]
+    ref = torch.load(out, weights_only=True)
+    got = _tap_cases()
+    for case, a, r in zip(_HALO_CASES, got, ref):
+        assert torch.equal(a, r), (case, (a - r).abs().max().item())
+
+
 def test_tap_conv1d_epilogue_views_and_cache():
     """BN-eval + LeakyReLU epilogue, x a channel slice of a concat buffer, out a strided view;
     the packed weights are rebuilt when the weight changes in place."""

@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 120 python tools/instep_spans.py 10 > gpurun_out/r04_instep_spans.txt 2>&1 || exit 1
+timeout -k 10 200 python bench.py --steps 100 --no-cpu-baseline > gpurun_out/r04f_bench.json 2> gpurun_out/r04f_bench.err || exit 1
 timeout -k 10 120 python tools/branch_probe.py 100 > gpurun_out/r04_branch_probe.txt 2>&1 || exit 2
 A2M_TWO_SIDES=1 timeout -k 10 120 python tools/branch_probe.py 100 >> gpurun_out/r04_branch_probe.txt 2>&1 || exit 3
 timeout -k 10 120 python tools/proj_probe.py > gpurun_out/r04_proj_probe.txt 2>&1 || exit 4
@@ -14,5 +14,4 @@ timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $PWD/gpurun_ou
 A2M_TWO_SIDES=1 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $PWD/gpurun_out/r04_bp2_trace -o run -- python tools/branch_probe.py 30 >> gpurun_out/r04_branch_probe.txt 2>&1 || exit 8
 bash tools/ab_env.sh "A2M_PROJ_DENSE=1" 3 > gpurun_out/r04_ab_projdense.txt 2>&1 || exit 6
 bash tools/ab_env.sh "A2M_TWO_SIDES=1" 3 > gpurun_out/r04_ab_twosides.txt 2>&1 || exit 9
-bash tools/ab_env.sh "A2M_GEMM_PRIO=1" 3 > gpurun_out/r04_ab_prio.txt 2>&1 || exit 10
 exit 0
