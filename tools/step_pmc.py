@@ -6,6 +6,10 @@ read the output (replay_filter.py) keep only the dispatches after the marker, i.
 replayed steps: no first-call repacks, no eager-step copies.
 
     rocprofv3 --pmc FETCH_SIZE -d DIR -- python tools/step_pmc.py [R] [--dtype bf16]
+        [--engine-json F] [--stamps F]
+--stamps also records the engine launches' own span stamps in every replay (a device sync after
+each replay), so the kernel trace and the stamps describe the same dispatches
+(tools/stamp_vs_trace.py).
 """
 import os
 import sys
@@ -25,6 +29,11 @@ def main():
         i = argv.index('--engine-json')
         ejson = argv[i + 1]
         del argv[i:i + 2]
+    sjson = None
+    if '--stamps' in argv:   # also record the engine's span stamps of every replay (tools/stamp_vs_trace.py)
+        i = argv.index('--stamps')
+        sjson = argv[i + 1]
+        del argv[i:i + 2]
     args = [a for a in argv if not a.startswith('--') and a != 'bf16']
     reps = int(args[0]) if args else 3
     dev = torch.device('cuda:0')
@@ -39,8 +48,11 @@ def main():
             torch.nn.init.constant_(m.gamma, 0.3)
     g = g.to(dev).eval()
     wave = bench.synth_wave(B, (T - 1) * bench.HOP + bench.WIN, seed=0, device=dev)
+    import contextlib
+    from a2m import functional as F
     with torch.no_grad():
-        graph, out = bench.capture_step(dev, bench.infer_step(g, wave))
+        with (F.gemm_timing(keep=True) if sjson else contextlib.nullcontext()) as tm:
+            graph, out = bench.capture_step(dev, bench.infer_step(g, wave))
         graph.replay()
         torch.cuda.synchronize()
         if ejson:
@@ -52,9 +64,19 @@ def main():
                 json.dump({'launches': gt.launches, 'gflop': gt.flops / 1e9}, f)
         torch.cuda._sleep(1000)             # the marker dispatch
         torch.cuda.synchronize()
+        stamps = []
+        if sjson:
+            tm.spans()   # re-arm after the pre-marker replay
         for _ in range(reps):
             graph.replay()
+            if sjson:
+                stamps.append([sp for sp in tm.spans() if sp[0] >= 0])
     torch.cuda.synchronize()
+    if sjson:
+        tm.release()
+        import json
+        with open(sjson, 'w') as f:
+            json.dump({'replays': stamps}, f)
     print(f'step_pmc: 2 eager + 1 graph step, marker, then {reps} replayed steps, out {tuple(out.shape)}')
 
 
