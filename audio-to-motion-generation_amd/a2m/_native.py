@@ -131,6 +131,10 @@ SIGNATURES = {
                                                   ctypes.POINTER(I64)]),
     'a2m_gemm_timing_read': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
                                             ctypes.POINTER(F64), ctypes.POINTER(I64)]),
+    'a2m_gemm_timing_read_spans_ex': (ctypes.c_int, [I64, ctypes.POINTER(F64), ctypes.POINTER(F64),
+                                                     ctypes.POINTER(F64), ctypes.POINTER(I64)]),
+    'a2m_gemm_timing_read_ex': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
+                                               ctypes.POINTER(F64), ctypes.POINTER(I64), ctypes.POINTER(F64)]),
     'a2m_timing_mark': (ctypes.c_int, [I32, ctypes.c_void_p]),
     'a2m_timing_mark_elapsed': (ctypes.c_int, [I32, I32, ctypes.POINTER(ctypes.c_float)]),
 }

@@ -940,14 +940,22 @@ class gemm_timing:
         return self
 
     def read(self):
-        return self._sums(N.lib.a2m_gemm_timing_read)
-
-    def spans(self, cap=4096):
-        """[(start_us, end_us)] of every recorded launch's tile kernel in the latest execution
-        (re-arms the stamps like read())."""
+        """The latest execution's sums (re-arms the stamps); also .ms_queued: the launches'
+        times from their ready marks (their stream reaching them) to their last block end."""
         import ctypes
-        s, e, n = (ctypes.c_double * cap)(), (ctypes.c_double * cap)(), ctypes.c_int64()
-        N.check(N.lib.a2m_gemm_timing_read_spans(cap, s, e, ctypes.byref(n)))
+        q = ctypes.c_double()
+        self._sums(lambda *a: N.lib.a2m_gemm_timing_read_ex(*a, ctypes.byref(q)))
+        self.ms_queued = q.value
+        return self
+
+    def spans(self, cap=4096, ready=False):
+        """[(start_us, end_us)] of every recorded launch's tile kernel in the latest execution
+        ([(ready_us, start_us, end_us)] with ready=True; re-arms the stamps like read())."""
+        import ctypes
+        r, s, e, n = (ctypes.c_double * cap)(), (ctypes.c_double * cap)(), (ctypes.c_double * cap)(), ctypes.c_int64()
+        N.check(N.lib.a2m_gemm_timing_read_spans_ex(cap, r, s, e, ctypes.byref(n)))
+        if ready:
+            return [(r[i], s[i], e[i]) for i in range(n.value)]
         return [(s[i], e[i]) for i in range(n.value)]
 
     def release(self):

@@ -424,7 +424,14 @@ static std::mutex g_timing_mu;
 static bool g_timing = false;
 static bool g_timing_overflow = false;
 static std::vector<GemmTiming> g_timing_recs;
-constexpr int kRecSlots = 2 * kSpanSlots;   // tile + reduce
+// tile spans + reduce spans + the launch's ready mark (and a pad slot; A2M_GEMM_TIMING_READY=1):
+// the wall clock at which a one-thread mark kernel, enqueued right before the tile kernel on its
+// stream, ran -- i.e.
+// when the stream reached the launch (its previous kernel done), so last end - ready counts the
+// launch's dispatch and any wait for free CUs behind the other decoder branch, as a kernel
+// trace's duration does
+constexpr int kRecSlots = 2 * kSpanSlots + 2;
+constexpr int kReadySlot = 2 * kSpanSlots;
 static unsigned long long* g_ts = nullptr;   // [kTimingRecs][kRecSlots] + [A2M_TIMING_MARKS] mark slots
 static double g_wall_mhz = 0.0;
 
@@ -540,7 +547,13 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     std::snprintf(desc, sizeof(desc), "M=%d N=%d K=%d b=%d tile=%d split=%d modes=%d,%d", M, N, K,
                   batch, p.bm, p.splits, ma, mb);
     a.ts = timing_open(2.0 * M * N * (double)K * batch, desc);
-    if (a.ts) g_timing_recs.back().reduce = p.splits > 1 || interp;
+    if (a.ts) {
+      g_timing_recs.back().reduce = p.splits > 1 || interp;
+      // A2M_GEMM_TIMING_READY=1 (diagnostic): the ready mark.  Off by default: the extra kernel
+      // per launch shifts how the two decoder branches share the CUs (tools/stamp_vs_trace.py)
+      static const int ready = env_int("A2M_GEMM_TIMING_READY", 0);
+      if (ready) hipLaunchKernelGGL(timing_mark_kernel, dim3(1), dim3(64), 0, stream, a.ts + kReadySlot);
+    }
   }
   if (prec == 1) {
     if (p.bm == 128) launch_tile<128, 128, 64, 1>(a, ma, mb, batch, stream);
@@ -624,6 +637,11 @@ int a2m_gemm_timing_stop(void) {
 
 int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                          int64_t* reduces) {
+  return a2m_gemm_timing_read_ex(launches, flops, ms_tile, ms_reduce, reduces, nullptr);
+}
+
+int a2m_gemm_timing_read_ex(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
+                            int64_t* reduces, double* ms_queued) {
   std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
   A2M_CHECK_ARG(a2m::g_ts != nullptr, "gemm_timing_read: timing was never begun");
   A2M_CHECK_ARG(!a2m::g_timing_overflow, "gemm_timing_read: more than %d launches in the window",
@@ -659,7 +677,7 @@ int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, doub
     return best;
   };
   int64_t n = 0, nr = 0;
-  double f = 0, mt = 0, mr = 0;
+  double f = 0, mt = 0, mr = 0, mq = 0;
   int rc = A2M_OK;
   const double tick_ms = 1.0 / (a2m::g_wall_mhz * 1e3);
   for (size_t i = 0; i < nrec; ++i) {
@@ -672,6 +690,14 @@ int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, doub
       continue;
     }
     const double a = sa * tick_ms, b = sb * tick_ms;
+    // ready mark .. last block end over all XCDs (the constant-rate clock is common to them)
+    const unsigned long long rdy = st[i * R + a2m::kReadySlot];
+    if (ms_queued && rdy != ~0ull && ga >= 0) {
+      unsigned long long hi = 0;
+      for (int q = 1; q < S; q += 2)
+        if (st[i * R + q - 1] != ~0ull && st[i * R + q] >= st[i * R + q - 1]) hi = std::max(hi, st[i * R + q]);
+      mq += hi > rdy ? (double)(hi - rdy) * tick_ms : a;
+    }
     ++n;
     f += t.flops;
     static const int log_launches = a2m::env_int("A2M_GEMM_LOG", 0);
@@ -686,6 +712,7 @@ int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, doub
   if (ms_tile) *ms_tile = mt;
   if (ms_reduce) *ms_reduce = mr;
   if (reduces) *reduces = nr;
+  if (ms_queued) *ms_queued = mq;
   // re-arm for the next replay of a graph that carries these launches
   if (a2m::timing_reset_stamps() != A2M_OK) {
     a2m::set_error("gemm timing: stamp reset failed");
@@ -695,6 +722,11 @@ int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, doub
 }
 
 int a2m_gemm_timing_read_spans(int64_t cap, double* start_us, double* end_us, int64_t* n) {
+  return a2m_gemm_timing_read_spans_ex(cap, nullptr, start_us, end_us, n);
+}
+
+int a2m_gemm_timing_read_spans_ex(int64_t cap, double* ready_us, double* start_us, double* end_us,
+                                  int64_t* n) {
   std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
   A2M_CHECK_ARG(a2m::g_ts != nullptr && start_us && end_us && n && cap >= 0,
                 "gemm_timing_read_spans: bad arguments (or timing never begun)");
@@ -717,6 +749,10 @@ int a2m_gemm_timing_read_spans(int64_t cap, double* start_us, double* end_us, in
     }
     start_us[i] = lo == ~0ull ? -1.0 : (double)lo / a2m::g_wall_mhz;
     end_us[i] = lo == ~0ull ? -1.0 : (double)hi / a2m::g_wall_mhz;
+    if (ready_us) {
+      const unsigned long long r = st[i * R + a2m::kReadySlot];
+      ready_us[i] = r == ~0ull ? -1.0 : (double)r / a2m::g_wall_mhz;
+    }
   }
   *n = (int64_t)nrec;
   return a2m::timing_reset_stamps() == A2M_OK ? A2M_OK : A2M_EHIP;

@@ -174,7 +174,10 @@ def instep_timing(dev, g, wave, reps=20, warm=None):
     right before each of those replays, so that each timed replay follows back-to-back work as
     in the timed loop instead of an idle, clocked-down GPU after the previous read's sync.
     Returns per-step means: the engine's launches /
-    FLOPs / tile ms / reduce ms, and the step's log-mel and log-mel + encoder phases (ms).
+    FLOPs / tile ms / reduce ms / queued ms (each launch from its ready mark -- a one-thread
+    kernel the engine enqueues right before the tile kernel while timing -- to its last block
+    end: its dispatch plus any wait for free CUs behind the other decoder branch, the extent a
+    kernel trace gives a kernel), and the step's log-mel and log-mel + encoder phases (ms).
     This is the basis of `roofline` and of `mel_encoder_roofline.path_frac_instep`;
     tools/step_pmc.sh's rocprof kernel trace of the replayed bench graph is its cross-check
     (profiles/)."""
@@ -198,7 +201,8 @@ def instep_timing(dev, g, wave, reps=20, warm=None):
         torch.cuda.current_stream(dev).wait_stream(s)
     finally:
         hook.remove()
-    acc = {'launches': 0, 'flops': 0.0, 'ms_tile': 0.0, 'ms_reduce': 0.0, 'mel_ms': 0.0, 'mel_enc_ms': 0.0}
+    acc = {'launches': 0, 'flops': 0.0, 'ms_tile': 0.0, 'ms_reduce': 0.0, 'ms_queued': 0.0, 'mel_ms': 0.0,
+           'mel_enc_ms': 0.0}
     try:
         graph.replay()
         torch.cuda.synchronize()
@@ -213,6 +217,7 @@ def instep_timing(dev, g, wave, reps=20, warm=None):
             acc['flops'] += t.flops
             acc['ms_tile'] += t.ms_tile
             acc['ms_reduce'] += t.ms_reduce
+            acc['ms_queued'] += t.ms_queued
             acc['mel_ms'] += F.timing_mark_elapsed(0, 1)
             acc['mel_enc_ms'] += F.timing_mark_elapsed(0, 2)
     finally:
@@ -478,6 +483,7 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0):
     ms_disp = it['ms_tile'] + n * dispatch_ms     # as a kernel trace accounts each launch
     tf = it['flops'] / (ms_disp * 1e-3) / 1e12
     tf_exec = it['flops'] / (it['ms_tile'] * 1e-3) / 1e12
+    tf_q = it['flops'] / (it['ms_queued'] * 1e-3) / 1e12 if it['ms_queued'] > 0 else None
     tf_ser = gt.flops / (gt.ms_tile * 1e-3) / 1e12
     tr = load_traffic('gemm_kernel') if peak == FP32_MFMA_PEAK_TFLOPS else None
     return {'bound': 'mfma', 'kernel': 'gemm_kernel (implicit-GEMM engine: every launch of one step)',
@@ -487,13 +493,17 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0):
             'traffic_source': tr['source'] if tr else None,
             'basis': 'in-step: the bench graph re-captured with the engine launches stamping their own '
                      'spans (first block start .. last block end, GPU wall clock), replayed 20 times '
-                     '(each after three back-to-back replays of the timed graph), '
-                     'plus the measured per-launch dispatch overhead (dispatch_ms_per_launch) that a '
-                     'kernel trace counts in each kernel; cross-check: rocprof kernel trace of replayed '
-                     'steps only (tools/step_pmc.sh, profiles/)',
+                     '(each after three back-to-back replays of the timed graph), plus the measured '
+                     'per-launch dispatch overhead (dispatch_ms_per_launch) that a kernel trace counts '
+                     'in each kernel; cross-check: rocprof kernel trace of replayed steps only '
+                     '(tools/step_pmc.sh; per launch tools/stamp_vs_trace.py, profiles/)',
             'launches_per_step': it['launches'], 'ms_per_launch': round(ms_disp / n, 4),
             'dispatch_ms_per_launch': round(dispatch_ms, 4),
             'frac_execution': round(tf_exec / peak, 4),
+            **({'frac_queued': round(tf_q / peak, 4),
+                'frac_queued_basis': 'A2M_GEMM_TIMING_READY=1: each launch from a ready mark (a one-thread '
+                                     'kernel enqueued just before it on its stream) to its last block end'}
+               if tf_q else {}),
             'gflop_per_launch': round(it['flops'] / n / 1e9, 3),
             'ms_tile_per_step': round(it['ms_tile'], 4),
             'splitk_reduce_ms_per_step': round(it['ms_reduce'], 4),

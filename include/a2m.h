@@ -520,10 +520,20 @@ int a2m_gemm_timing_stop(void);
  * start and last block end (us on the GPU wall clock, -1 for a launch that did not run) of the
  * first min(cap, launches) records; re-arms the stamps like _read. */
 int a2m_gemm_timing_read_spans(int64_t cap, double* start_us, double* end_us, int64_t* n);
+/* _read_spans plus each launch's ready mark (us; -1 unless A2M_GEMM_TIMING_READY=1 was set when
+ * the launch was recorded: the wall clock at which a one-thread mark kernel enqueued right before
+ * the tile kernel ran, i.e. when its stream reached the launch) */
+int a2m_gemm_timing_read_spans_ex(int64_t cap, double* ready_us, double* start_us, double* end_us,
+                                  int64_t* n);
 /* _stop + forget the records without reading them (after the last _read of a kept window) */
 int a2m_gemm_timing_clear(void);
 int a2m_gemm_timing_read(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
                          int64_t* reduces);
+/* _read plus ms_queued: the sum over launches of (last block end - ready mark), the launch's time
+ * from the moment its stream reached it, i.e. including its dispatch and any wait for free CUs
+ * (0 without A2M_GEMM_TIMING_READY=1) */
+int a2m_gemm_timing_read_ex(int64_t* launches, double* flops, double* ms_tile, double* ms_reduce,
+                            int64_t* reduces, double* ms_queued);
 /* Named wall-clock marks (measurement only; after a2m_gemm_timing_begin has allocated the stamp
  * buffer): a one-thread kernel on the stream stores the GPU wall clock into mark `slot`
  * (0 .. A2M_TIMING_MARKS-1), also as a node of a graph being captured; _elapsed synchronises the

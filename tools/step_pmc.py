@@ -6,7 +6,7 @@ read the output (replay_filter.py) keep only the dispatches after the marker, i.
 replayed steps: no first-call repacks, no eager-step copies.
 
     rocprofv3 --pmc FETCH_SIZE -d DIR -- python tools/step_pmc.py [R] [--dtype bf16]
-        [--engine-json F] [--stamps F]
+        [--engine-json F] [--stamps F] [--sync]
 --stamps also records the engine launches' own span stamps in every replay (a device sync after
 each replay), so the kernel trace and the stamps describe the same dispatches
 (tools/stamp_vs_trace.py).
@@ -34,6 +34,12 @@ def main():
         i = argv.index('--stamps')
         sjson = argv[i + 1]
         del argv[i:i + 2]
+    # --sync: a device sync after every replay.  Free-running replays under --kernel-trace ran the
+    # step 11 % slower than unprofiled (2.97 vs 2.67 ms, r04j) and lengthened every traced kernel
+    # with it (engine 2628 us/step against 2345 us with a sync per replay, the stamps' 2265 us of
+    # spans + 2.2 us per launch); unprofiled, synced and free-running replays take the same time
+    # (tools/branch_probe.py: 2.672 vs 2.661 ms)
+    sync = '--sync' in argv
     args = [a for a in argv if not a.startswith('--') and a != 'bf16']
     reps = int(args[0]) if args else 3
     dev = torch.device('cuda:0')
@@ -69,8 +75,10 @@ def main():
             tm.spans()   # re-arm after the pre-marker replay
         for _ in range(reps):
             graph.replay()
+            if sync:
+                torch.cuda.synchronize()
             if sjson:
-                stamps.append([sp for sp in tm.spans() if sp[0] >= 0])
+                stamps.append([sp for sp in tm.spans(ready=True) if sp[1] >= 0])
     torch.cuda.synchronize()
     if sjson:
         tm.release()

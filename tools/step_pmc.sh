@@ -1,7 +1,9 @@
 #!/bin/bash
 # rocprof passes over exactly the bench step (tools/step_pmc.py), counting only the graph-replayed
-# steps after its marker kernel (tools/replay_filter.py): a kernel-trace/stats pass (per-step
-# breakdown + the GEMM engine's in-step roofline, tools/replay_breakdown.py), FETCH_SIZE,
+# steps after its marker kernel (tools/replay_filter.py): a kernel-trace/stats pass over replays
+# each followed by a device sync (step_pmc.py --sync: free-running replays slow down under the
+# trace) for the per-step breakdown and the GEMM engine's in-step roofline
+# (tools/replay_breakdown.py), FETCH_SIZE,
 # WRITE_SIZE, MFMA busy + GRBM cycles; then per-launch HBM traffic and MFMA utilisation per
 # kernel family (tools/pmc_traffic.py, tools/pmc_mfma.py).   tools/step_pmc.sh TAG [--dtype bf16]
 set -u
@@ -12,7 +14,7 @@ R=${STEP_PMC_REPS:-10}
 OUT=gpurun_out/steppmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $REPO/$OUT/trace -o run -- python tools/step_pmc.py $R --engine-json $OUT/engine.json "$@" > $OUT/trace.log 2>&1 || { echo trace failed; tail -5 $OUT/trace.log; exit 2; }
+timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $REPO/$OUT/trace -o run -- python tools/step_pmc.py $R --sync --engine-json $OUT/engine.json "$@" > $OUT/trace.log 2>&1 || { echo trace failed; tail -5 $OUT/trace.log; exit 2; }
 GF=$(python -c "import json; print(json.load(open('$OUT/engine.json'))['gflop'])")
 python tools/replay_breakdown.py $OUT/trace $R --gflop $GF --out $OUT/breakdown.txt > /dev/null || exit 8
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $REPO/$OUT/fetch -o run -- python tools/step_pmc.py 3 "$@" > $OUT/fetch.log 2>&1 || { echo fetch failed; tail -5 $OUT/fetch.log; exit 3; }
