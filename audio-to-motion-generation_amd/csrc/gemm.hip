@@ -391,6 +391,13 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, in
   return p;
 }
 
+// slab workspace of a split plan: [splits][batch][M][N] for the reduce kernel, or whole padded
+// tiles [batch * tiles][splits][BM * BN] for the in-launch combine (the larger is reserved)
+static size_t split_ws_bytes(const Plan& p, int M, int N, int batch) {
+  const size_t padded = (size_t)cdiv(M, p.bm) * p.bm * cdiv(N, p.bm) * p.bm;
+  return (size_t)p.splits * batch * std::max((size_t)M * N, padded) * sizeof(float);
+}
+
 size_t gemm_ws_bytes(int M, int N, int K, int batch) {
   // either operand orientation (the plan depends on whether an operand is row-gathered) and
   // either precision
@@ -399,9 +406,34 @@ size_t gemm_ws_bytes(int M, int N, int K, int batch) {
     for (int prec : {0, 1, 2})
       for (bool rows6 : {false, true}) {
         const Plan p = plan_for(M, N, K, batch, gathered, prec, 1, rows6);
-        if (p.splits > 1) need = std::max(need, (size_t)p.splits * batch * M * N * sizeof(float));
+        if (p.splits > 1) need = std::max(need, split_ws_bytes(p, M, N, batch));
       }
   return need;
+}
+
+// Arrival counters of the in-launch split-K combine: one int per output tile of a launch, taken
+// from a ring so that launches that may run concurrently (the decoder branches' streams, graph
+// replays) use disjoint counters; every counter is 0 between launches (zeroed once here, reset
+// by each tile's last arriver).  Allocated outside graph capture (the eager warm-up launches);
+// a launch captured before then keeps the reduce kernel.
+constexpr size_t kCntRing = 1 << 20;
+static int* g_cnt = nullptr;
+static size_t g_cnt_next = 0;
+static std::mutex g_cnt_mu;
+
+static int* fixup_counters(size_t tiles, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_cnt_mu);
+  if (!g_cnt) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    if (hipMalloc(&g_cnt, kCntRing * sizeof(int)) != hipSuccess) { g_cnt = nullptr; return nullptr; }
+    if (hipMemset(g_cnt, 0, kCntRing * sizeof(int)) != hipSuccess) return nullptr;
+  }
+  if (tiles > kCntRing / 4) return nullptr;
+  if (g_cnt_next + tiles > kCntRing) g_cnt_next = 0;
+  int* c = g_cnt + g_cnt_next;
+  g_cnt_next += (tiles + 63) / 64 * 64;
+  return c;
 }
 
 // Optional per-launch timing of the engine (bench.py's live roofline).  While enabled, every
@@ -529,8 +561,23 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                             (size_t)E.interp_H * sizeof(float) <= 32768),
                 "gemm: fused resample needs batch 1, N a multiple of H = %d <= 8192", E.interp_H);
   a.mcontig = stage_m && E.som == 1 && M > 1 && !interp;
+  // in-launch split-K combine (A2M_GEMM_FIXUP=1; default: the reduce kernel): the one-group tiles
+  // (not the two-group KS = 2 / 3 variants), up to 16 splits (more: the wide reduce kernel)
+  // Off by default: with the 16 KB limit it measured neutral (2.719 vs 2.720 ms, three pairs, r04k)
+  static const int fix_on = env_int("A2M_GEMM_FIXUP", 0);
+  static const int ks2 = env_int("A2M_GEMM_KS2", 1);
+  const bool ks2_launch = prec == 0 && p.bm == 64 && !use_ks3 && ks2 && ma == 0 &&
+                          (mb == 0 || (ks2 == 2 && mb == 6));
+  // the last arriver reads the other S - 1 slabs serially (sc1, from memory): measured a net loss
+  // where that exceeds a few tens of KB (128x128 tiles at 4-8 splits: step 2.86 vs 2.76 ms with
+  // every launch combined in-kernel, r04k), so only up to A2M_GEMM_FIXUP_KB (default 16) of slabs
+  static const int fix_kb = env_int("A2M_GEMM_FIXUP_KB", 16);
+  a.cnt = nullptr;
+  if (fix_on && p.splits > 1 && p.splits <= 16 && !interp && !use_ks3 && !ks2_launch &&
+      (p.splits - 1) * p.bm * p.bm * 4 <= fix_kb * 1024)
+    a.cnt = fixup_counters((size_t)cdiv(M, p.bm) * cdiv(N, p.bm) * batch, stream);
   if (p.splits > 1 || interp) {
-    const size_t need = (size_t)p.splits * batch * M * N * sizeof(float);
+    const size_t need = a.cnt ? split_ws_bytes(p, M, N, batch) : (size_t)p.splits * batch * M * N * sizeof(float);
     if (ws == nullptr || ws_bytes < need) {
       set_error("gemm: workspace too small (%zu < %zu bytes)", ws_bytes, need);
       return A2M_EWS;
@@ -539,8 +586,9 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   }
   static const int log_launches = env_int("A2M_GEMM_LOG", 0);
   if (log_launches)
-    std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
-                 M, N, K, batch, p.bm, p.bk, p.splits, ma, mb, E.som, E.so0, E.so1, E.so2, E.N1, E.N2);
+    std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d%s modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
+                 M, N, K, batch, p.bm, p.bk, p.splits, a.cnt ? " (in-launch)" : "", ma, mb, E.som, E.so0, E.so1,
+                 E.so2, E.N1, E.N2);
   a.ts = nullptr;
   if (g_timing) {
     char desc[96];
@@ -548,7 +596,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                   batch, p.bm, p.splits, ma, mb);
     a.ts = timing_open(2.0 * M * N * (double)K * batch, desc);
     if (a.ts) {
-      g_timing_recs.back().reduce = p.splits > 1 || interp;
+      g_timing_recs.back().reduce = (p.splits > 1 && !a.cnt) || interp;
       // A2M_GEMM_TIMING_READY=1 (diagnostic): the ready mark.  Off by default: the extra kernel
       // per launch shifts how the two decoder branches share the CUs (tools/stamp_vs_trace.py)
       static const int ready = env_int("A2M_GEMM_TIMING_READY", 0);
@@ -562,7 +610,6 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     if (p.bm == 128) launch_tile<128, 128, 32, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
   } else {
-    static const int ks2 = env_int("A2M_GEMM_KS2", 1);
     if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
     else if (use_ks3) launch_tile<64, 64, 32, 0, 3>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
@@ -582,7 +629,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     hipLaunchKernelGGL(splitk_reduce_interp_kernel, dim3((unsigned)cdiv((int64_t)M * nb, RB)), dim3(256),
                        (size_t)RB * H * sizeof(float), stream, a, nb, RB, wide);
     A2M_LAUNCH_CHECK();
-  } else if (p.splits > 1) {
+  } else if (p.splits > 1 && !a.cnt) {
     const int inner = a.mcontig ? M : N;
     const int64_t total = (int64_t)M * N * batch / ((inner & 3) == 0 ? 4 : 1);
     static const int wide_on = env_int("A2M_GEMM_WIDE_REDUCE", 1);

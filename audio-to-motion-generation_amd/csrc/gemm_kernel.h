@@ -26,6 +26,7 @@
 namespace a2m {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned v4u32_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // K-tile depth BK = 32 (the kernels are templated on it).  LDS row pitch BK+4 floats keeps the
@@ -43,6 +44,8 @@ struct GemmArgs {
   int skew;        // KS = 3: wave group 1 runs its k-steps half a step after group 0's
   unsigned long long* ts;   // measurement only (a2m_gemm_timing_*; null otherwise): this launch's
                             // span stamps, [tile | reduce][XCD][first start, last end]
+  int* cnt;        // split-K combined in the launch (gemm_tile's epilogue): one arrival counter
+                   // per output tile (0 between launches); null: slabs for the reduce kernel
 };
 
 // Launch-span stamps (bench.py's in-step roofline): per XCD, the earliest block start and the
@@ -958,7 +961,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
   }
 
   // epilogue constants of the block's rows, visible after the k loop's first barrier
-  if (!args.partial && grp == 0 && tid < BM && m0 + tid < args.M)
+  if ((!args.partial || args.cnt) && grp == 0 && tid < BM && m0 + tid < args.M)
     epr[tid] = epi_row(args.E, m0 + tid + batch * args.E.pstride);
 
   LA la;
@@ -1224,6 +1227,81 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
     }
   }
 
+  // In-launch split-K combine (args.cnt; KS = 1 tiles only, host): every split block stores its
+  // partial accumulators as a slab in fragment order (thread-linear float4s: one coalesced
+  // 4 KB row per instruction) with write-through (sc1) stores, drains them, and takes a ticket
+  // on the tile's arrival counter (one relaxed agent-scope add by one lane after the block's
+  // barrier); the block that draws the last ticket resets the counter for the next launch,
+  // reads the other slabs back with sc1 loads (no L2 write-back fence on the producers, no
+  // stale L1 / other-XCD L2 lines on the reader: the guide's split-K seam) and sums all S
+  // partials in the order s = 0, 1, ..., S - 1 from 0 (its own from registers) -- the reduce
+  // kernel's order, so the sums are bitwise those of splitk_reduce_kernel -- then runs the
+  // normal epilogue.  No block waits for another: the combine costs the last arriver S - 1
+  // slab reads instead of a second launch and its slab round trip.
+  bool slab_out = args.partial != nullptr;
+  if constexpr (KS == 1) {
+    if (args.cnt) {
+      constexpr int NQ4 = TM * TN * 4;   // float4s per thread
+      constexpr int SLAB = BM * BN;      // floats per slab
+      const int S = args.splits;
+      const int tile = (batch * (int)gridDim.y + by) * (int)gridDim.x + bx;
+      float* tb = args.partial + (int64_t)tile * S * SLAB;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          tb, (short)0, __builtin_amdgcn_readfirstlane(S * SLAB * 4), 0x00020000);
+#pragma unroll
+      for (int c = 0; c < NQ4; ++c) {
+        const int t = c / (4 * TN), u = (c / 4) % TN, q = 4 * (c % 4);
+        const float4 v = make_float4(acc[t][u][q], acc[t][u][q + 1], acc[t][u][q + 2], acc[t][u][q + 3]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, v), rs,
+                                               ((split * NQ4 + c) * 256 + tid) * 16, 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(lds_all);
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(args.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == S - 1;
+        if (last) __hip_atomic_store(args.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = last;
+      }
+      __syncthreads();
+      const int last = flag[0];
+      __syncthreads();   // the flag word is read before the epilogue may reuse the stages
+      if (!last) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the slab loads below
+      floatx16 own[TM][TN];
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u) {
+          own[t][u] = acc[t][u];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
+        }
+      for (int sl = 0; sl < S; ++sl) {
+        if (sl == split) {
+#pragma unroll
+          for (int t = 0; t < TM; ++t)
+#pragma unroll
+            for (int u = 0; u < TN; ++u)
+#pragma unroll
+              for (int q = 0; q < 16; ++q) acc[t][u][q] += own[t][u][q];
+          continue;
+        }
+        float4 v[NQ4];
+#pragma unroll
+        for (int c = 0; c < NQ4; ++c)
+          v[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((sl * NQ4 + c) * 256 + tid) * 16, 0, 16));
+#pragma unroll
+        for (int c = 0; c < NQ4; ++c) {
+          const int t = c / (4 * TN), u = (c / 4) % TN, q = 4 * (c % 4);
+          acc[t][u][q] += v[c].x; acc[t][u][q + 1] += v[c].y; acc[t][u][q + 2] += v[c].z; acc[t][u][q + 3] += v[c].w;
+        }
+      }
+      slab_out = false;
+    }
+  }
+
   // epilogue
   if (args.mcontig) {
     // m-contiguous output (node-feature layouts [.., J*64]): a direct store would put the 32
@@ -1243,7 +1321,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
     const int ml = tid % BM;
     const int m = m0 + ml;
     if (m < args.M) {
-      if (args.partial) {
+      if (slab_out) {
         for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
           const int n = n0 + nl;
           if (n >= args.N) break;
@@ -1267,7 +1345,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
   for (int u = 0; u < TN; ++u) {
     const int n = n0 + wn * (BN / 2) + u * 32 + li;
     if (n >= args.N) continue;
-    if (args.partial) {
+    if (slab_out) {
       float* dst = args.partial + (int64_t)zz * args.M * args.N + n;
 #pragma unroll
       for (int t = 0; t < TM; ++t)
