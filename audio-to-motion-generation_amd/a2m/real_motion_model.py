@@ -115,12 +115,13 @@ class SelfAttention_G(_GraphTopology):
             layers = []
             for L in range(5):
                 g = getattr(self, f'{part}_gcn{L + 1}')
+                planes = g.__dict__.setdefault('_planes', {})   # bf16x6 weight planes
                 if L % 2 == 0:
                     U = F.graph_att_proj(g.lin.weight, g.att_src, g.att_dst, cache=g._U)
-                    layers.append((0, g.lin.weight, None, U, g.bias, lns[L].weight, lns[L].bias))
+                    layers.append((0, g.lin.weight, None, U, g.bias, lns[L].weight, lns[L].bias, planes))
                 else:
                     layers.append((1, g.lin_rel.weight, g.lin_root.weight, None, g.lin_rel.bias,
-                                   lns[L].weight, lns[L].bias))
+                                   lns[L].weight, lns[L].bias, planes))
             a = F.graph_stack(a, nj, ptr, idx, layers, out=b)
         else:
             for L in range(5):
@@ -136,6 +137,29 @@ class SelfAttention_G(_GraphTopology):
         F.conv1d(a.view(B, T, nj * 64).permute(0, 2, 1), pout.weight, pout.bias, out=rows.permute(0, 2, 1))
         nrm = getattr(self, f'{part}_norm')
         return F.layernorm_to_bct(rows.view(B * T, C), nrm.weight, nrm.bias, T, eps=nrm.eps, out=out_bct)
+
+    def _branches_interleaved(self, feats, out, main, side):
+        parts = (('hand', side, self.body_feats), ('body', main, 0))
+        xs = {'hand': feats, 'body': feats}
+
+        def run(stage):
+            mods = {p: list(getattr(self, f'{p}_{stage}')) for p, _, _ in parts}
+            for i in range(max(len(m) for m in mods.values())):
+                for p, st, _ in parts:
+                    if i < len(mods[p]):
+                        with torch.cuda.stream(st):
+                            xs[p] = mods[p][i](xs[p])
+        run('decoder_pre')
+        for p, st, _ in parts:
+            with torch.cuda.stream(st):
+                xs[p] = self._graph_stack(p, xs[p], None)
+        run('decoder_post')
+        for p, st, f0 in parts:
+            with torch.cuda.stream(st):
+                lg = getattr(self, f'{p}_logits')
+                nf = lg.weight.shape[0]
+                F.conv1d(xs[p], lg.weight, lg.bias, out=out[:, :, f0:f0 + nf].permute(0, 2, 1))
+        main.wait_stream(side)
 
     def _branch(self, part, feats, pose_out, f0):
         self._branch_tail(part, getattr(self, f'{part}_decoder_pre')(feats), pose_out, f0)
@@ -277,7 +301,11 @@ class SelfAttention_G(_GraphTopology):
             main = torch.cuda.current_stream(audio.device)
             side = _side_stream(audio.device)
             side.wait_stream(main)
-            if _TWO_SIDES:
+            if _INTERLEAVE:
+                # A2M_INTERLEAVE: the two branches captured layer by layer in alternation (hand on
+                # the side stream), so the graph's node order interleaves them
+                self._branches_interleaved(feats, out, main, side)
+            elif _TWO_SIDES:
                 # A2M_TWO_SIDES: each branch on its own side stream, both forked from and joined
                 # to the caller's (experiment: how the graph executor places the branches)
                 side2 = _side_stream(audio.device, 1)
@@ -299,7 +327,7 @@ class SelfAttention_G(_GraphTopology):
                 with torch.cuda.stream(side):
                     self._branch('body', feats, out, 0)
                 self._branch('hand', feats, out, self.body_feats)
-            if not _TWO_SIDES:
+            if not _TWO_SIDES and not _INTERLEAVE:
                 main.wait_stream(side)
         else:
             self._branch('body', feats, out, 0)
@@ -357,6 +385,7 @@ _SIDE_STREAMS = {}
 _HAND_FIRST = os.environ.get('A2M_HAND_FIRST', '1') != '0'
 _SIDE_PRIO = os.environ.get('A2M_SIDE_PRIO', '0') != '0'
 _TWO_SIDES = os.environ.get('A2M_TWO_SIDES', '0') != '0'
+_INTERLEAVE = os.environ.get('A2M_INTERLEAVE', '0') != '0'
 
 
 def _side_stream(device, which=0):

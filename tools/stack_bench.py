@@ -1,5 +1,6 @@
 """Times the fused eval graph stack (a2m_graph_stack_fwd_f32: GAT, GraphConv, GAT, GraphConv,
-GAT) at the bench shapes: hand (J=42) and body (J=10) over B*T = 4096 frames.
+GAT) at the bench shapes: hand (J=42) and body (J=10) over B*T = 4096 frames (the kernel
+A2M_STACK_X6 selects; weight planes cached outside the timed loop).
     python tools/stack_bench.py [hand|body] [iters]"""
 import os
 import sys
@@ -33,9 +34,9 @@ for name, J, lo in (('hand', 42, 10), ('body', 10, 0)):
         if L % 2 == 0:
             lw = rnd(256, 64, scale=0.15)
             U = F.graph_att_proj(lw, rnd(1, 4, 64, scale=0.3), rnd(1, 4, 64, scale=0.3))
-            layers.append((0, lw, None, U, rnd(64, scale=0.1), lnw, lnb))
+            layers.append((0, lw, None, U, rnd(64, scale=0.1), lnw, lnb, {}))
         else:
-            layers.append((1, rnd(64, 64, scale=0.12), rnd(64, 64, scale=0.12), None, rnd(64, scale=0.1), lnw, lnb))
+            layers.append((1, rnd(64, 64, scale=0.12), rnd(64, 64, scale=0.12), None, rnd(64, scale=0.1), lnw, lnb, {}))
     out = torch.empty_like(x)
     for _ in range(3):
         F.graph_stack(x, J, ptr, idx, layers, out=out)
