@@ -572,8 +572,14 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   // where that exceeds a few tens of KB (128x128 tiles at 4-8 splits: step 2.86 vs 2.76 ms with
   // every launch combined in-kernel, r04k), so only up to A2M_GEMM_FIXUP_KB (default 16) of slabs
   static const int fix_kb = env_int("A2M_GEMM_FIXUP_KB", 16);
+  // LDS-DMA operand staging (KS = 4, A2M_GEMM_GLDS: 1 = 64x64 tiles, 2 = also 128x128): fp32,
+  // dense weights x dense / channels-last conv rows (modes 0 / 6 over 16-byte aligned rows)
+  static const int glds_on = env_int("A2M_GEMM_GLDS", 0);
+  const bool rows_ok = mb == 6 || (B.sr0 % 4 == 0 && B.bstride % 4 == 0);
+  const bool glds_launch = glds_on && prec == 0 && !use_ks3 && ma == 0 && (mb == 0 || mb == 6) &&
+                           rows_ok && (p.bm == 64 || glds_on >= 2);
   a.cnt = nullptr;
-  if (fix_on && p.splits > 1 && p.splits <= 16 && !interp && !use_ks3 && !ks2_launch &&
+  if (fix_on && p.splits > 1 && p.splits <= 16 && !interp && !use_ks3 && !ks2_launch && !glds_launch &&
       (p.splits - 1) * p.bm * p.bm * 4 <= fix_kb * 1024)
     a.cnt = fixup_counters((size_t)cdiv(M, p.bm) * cdiv(N, p.bm) * batch, stream);
   if (p.splits > 1 || interp) {
@@ -610,7 +616,9 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     if (p.bm == 128) launch_tile<128, 128, 32, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
   } else {
-    if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
+    if (glds_launch && p.bm == 128) launch_tile<128, 128, 32, 0, 4>(a, ma, mb, batch, stream);
+    else if (glds_launch) launch_tile<64, 64, 32, 0, 4>(a, ma, mb, batch, stream);
+    else if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
     else if (use_ks3) launch_tile<64, 64, 32, 0, 3>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
     // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end

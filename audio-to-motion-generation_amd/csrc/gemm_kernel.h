@@ -679,6 +679,106 @@ struct TileLoader {
   }
 };
 
+// LDS-DMA operand staging (KS = 4; fp32, BK = 32; dense rows, mode 0, or channels-last conv
+// rows, mode 6): every k-tile row's 32 floats (128 B) go global -> LDS with
+// global_load_lds_dwordx4, no register round trip, into an unpadded [row][32] image whose 16-B
+// quads are XOR-swizzled by row (slot s of row r holds quad s ^ (r & 7)): one wave-instruction
+// fills 8 whole rows (its LDS destination is lane-linear), the swizzle is applied to the global
+// source addresses, and the fragment reads un-swizzle it, which keeps their ds_read_b128s
+// spread over the banks.  Rows / k outside the operand (and mode 6's padding pixels) read a
+// 16-B zero block instead.
+static __device__ __attribute__((aligned(16))) float g_glds_zero[4];
+template <int BR, int MODE>
+struct GldsLoader {
+  static_assert(MODE == 0 || MODE == 6, "LDS-DMA staging: k-contiguous rows only");
+  static constexpr int BK = 32;
+  static constexpr int TILE = BR * BK;     // floats
+  static constexpr int RPW = BR / 4;       // rows per wave
+  static constexpr int NI = RPW / 8;       // wave-instructions per k-tile
+  const Gather* g;
+  const float* base;
+  int K;
+  int rbase[NI];
+  int rh[NI], rw[NI];
+  bool rval[NI];
+  int qo;                                  // this lane's source quad offset (floats)
+  int lrow0;                               // the wave's first tile row
+  int k6, i6, j6, c6;
+  __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid, int kbeg) {
+    g = &gg;
+    base = gg.base + (int64_t)z * gg.bstride;
+    K = KK;
+    const int wave = tid >> 6, lane = tid & 63;
+    lrow0 = wave * RPW;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = lrow0 + 8 * j + (lane >> 3);
+      RowInfo ri = row_info(gg, row0 + row, R);
+      if (MODE == 6) ri.base += (ri.h * gg.Lw + ri.w) * gg.nhwc;
+      rbase[j] = ri.base;
+      rh[j] = ri.h;
+      rw[j] = ri.w;
+      rval[j] = ri.valid;
+    }
+    // the lane's row & 7 is (lane >> 3) & 7 for every instruction (rows 8j + lane / 8)
+    qo = 4 * ((lane & 7) ^ ((lane >> 3) & 7));
+    if (MODE == 6) {
+      const int tap = kbeg / gg.nhwc;
+      k6 = kbeg;
+      c6 = kbeg - tap * gg.nhwc;
+      i6 = tap / gg.K2;
+      j6 = tap - i6 * gg.K2;
+    }
+  }
+  // k-tile k0 into the stage image lds (all waves; completion counted by vmcnt)
+  __device__ __forceinline__ void issue(int k0, float* lds) {
+    int toff = 0, ti = 0, tj = 0;
+    if (MODE == 6) {
+      const int Ci = g->nhwc;
+      while (k6 < k0) {
+        k6 += BK;
+        c6 += BK;
+        if (c6 == Ci) {
+          c6 = 0;
+          if (++j6 == g->K2) { j6 = 0; ++i6; }
+        }
+      }
+      ti = i6;
+      tj = j6;
+      toff = (ti * g->Lw + tj) * Ci + c6;
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const float* src;
+      if (MODE == 0) {
+        const int k = k0 + qo;
+        src = rval[j] && k < K ? base + rbase[j] + k : g_glds_zero;
+      } else {
+        const int h = rh[j] + ti, w = rw[j] + tj;
+        const bool ok = rval[j] && k0 < K && (unsigned)h < (unsigned)g->Lh && (unsigned)w < (unsigned)g->Lw;
+        src = ok ? base + rbase[j] + toff + qo : g_glds_zero;
+      }
+      // inline asm, not the builtin: the compiler cannot tell the builtin's LDS writes from the
+      // fragment reads of the other stages and waits vmcnt(0) before every k-step's reads, which
+      // drains the DMAs meant to stay in flight; the k loop counts them itself (s_waitcnt vmcnt)
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)(lds + (lrow0 + 8 * j) * BK));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    }
+  }
+  // the 8 k-values (k = 16 half + 8 lh + s) of tile row `row`
+  __device__ __forceinline__ static void frag(const float* lds, int row, int half, int lh, float* f) {
+    const float* rp = lds + row * BK;
+    const int q0 = 4 * half + 2 * lh, sw = row & 7;
+    const float4 v0 = *reinterpret_cast<const float4*>(rp + 4 * (q0 ^ sw));
+    const float4 v1 = *reinterpret_cast<const float4*>(rp + 4 * ((q0 + 1) ^ sw));
+    f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w;
+    f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
+  }
+};
+
 __device__ __forceinline__ int64_t epi_addr(const Epilogue& E, int m, int n) {
   int n2 = n % E.N2;
   int t = n / E.N2;
@@ -903,19 +1003,32 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
   static_assert(P == 0 ? (BK == 32 || BK == 64) : BK == (P == 1 ? 64 : 32),
                 "the k-step pipeline assumes two halves per k-tile");
   constexpr int NS = P == 0 ? BK / 32 : 1;   // fp32: 16-k fragment chunks per half
-  static_assert(KS == 1 || P == 0, "two wave groups: fp32 tiles only");
+  static_assert(KS == 1 || P == 0, "two wave groups / LDS-DMA staging: fp32 tiles only");
   constexpr int TM = BM / 64, TN = BN / 64;
   using LA = TileLoader<BM, BK, MA, P>;
   using LB = TileLoader<BN, BK, MB, P>;
   constexpr int STAGE = LA::TILE + LB::TILE;
   // mode-5 halo layout: two A stages + two chunk-wide B stages (tile_halo below)
   constexpr bool HALO = MB == 5 && P == 0 && KS == 1 && BN == 64;
-  constexpr int LDS_F = (KS == 3 ? 4 : 2) * STAGE;
+  // KS = 4: three LDS-DMA stages of unpadded [row][32] images
+  constexpr int GSTAGE = (BM + BN) * 32;
+  constexpr int LDS_F = KS == 4 ? (3 * GSTAGE > 2 * STAGE ? 3 * GSTAGE : 2 * STAGE) : (KS == 3 ? 4 : 2) * STAGE;
   constexpr int LDS_H = HALO ? 2 * LA::TILE + 2 * LB::TILE_H : 0;
-  __shared__ __attribute__((aligned(16))) float lds_all[LDS_F > LDS_H ? LDS_F : LDS_H];
-  __shared__ EpiRow epr[BM];   // the block's per-row epilogue constants (final-output launches)
+  constexpr int LDS_T = LDS_F > LDS_H ? LDS_F : LDS_H;
+  // KS = 4 keeps the epilogue constants inside the one staging array: with a second __shared__
+  // object the compiler cannot tell the LDS-DMA writes from the fragment reads and waits
+  // vmcnt(0) before every k-step's reads
+  constexpr int EPR_F = KS == 4 ? (int)((BM * sizeof(EpiRow) + 15) / 16 * 4) : 0;
+  __shared__ __attribute__((aligned(16))) float lds_all[LDS_T + EPR_F];
+  EpiRow* epr;   // the block's per-row epilogue constants (final-output launches)
+  if constexpr (KS == 4) {
+    epr = reinterpret_cast<EpiRow*>(lds_all + LDS_T);
+  } else {
+    __shared__ EpiRow epr_arr[BM];
+    epr = epr_arr;
+  }
   static_assert(KS == 1 || (TM * TN * 16 * 256 <= 2 * STAGE), "KS = 2 partials must fit the stages");
-  const int grp = KS == 1 ? 0 : (int)(threadIdx.x >> 8);
+  const int grp = (KS == 1 || KS == 4) ? 0 : (int)(threadIdx.x >> 8);
   float* lds = KS == 3 ? lds_all + grp * 2 * STAGE : lds_all;
   const int tid = threadIdx.x & 255;
   const int lane = tid & 63, wave = tid >> 6;
@@ -966,8 +1079,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
 
   LA la;
   LB lb;
-  la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
-  lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
+  if constexpr (KS != 4) {
+    la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
+    lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
+  }
 
   floatx16 acc[TM][TN];
 #pragma unroll
@@ -978,7 +1093,65 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
-  bool halo_done = false;
+  if constexpr (KS == 4) {
+    // LDS-DMA pipeline (GldsLoader): tiles land in a ring of three LDS stages two k-steps ahead
+    // of the MFMAs, with no register staging.  Step i: issue tile i + 2 into the stage tile i - 1
+    // used (every wave is past step i - 1's barrier, after its last reads of it), read the second
+    // half's fragments, first-half MFMAs, then wait for this wave's tile i + 1 (vmcnt counted:
+    // tile i + 2's NIW DMAs may stay in flight) and its fragment reads, a raw barrier (no
+    // __syncthreads: its fence would drain the in-flight DMAs), next tile's first fragments
+    // behind the second half's first MFMAs.
+    using GA = GldsLoader<BM, MA>;
+    using GB = GldsLoader<BN, MB>;
+    constexpr int GST = GA::TILE + GB::TILE;
+    constexpr int NIW = GA::NI + GB::NI;   // DMAs per wave per k-tile
+    static_assert(NIW < 16, "vmcnt immediate");
+    GA ga;
+    GB gb;
+    ga.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
+    gb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
+    auto issue = [&](int t, int stage) {
+      float* st = lds_all + stage * GST;
+      ga.issue(kbeg + t * BK, st);
+      gb.issue(kbeg + t * BK, st + GA::TILE);
+    };
+    Frags<TM, TN, P, NS> f0, f1;
+    if (nk > 0) issue(0, 0);
+    if (nk > 1) {
+      issue(1, 1);
+      __builtin_amdgcn_s_waitcnt(0x0070 | NIW);   // vmcnt(NIW) lgkmcnt(0): tile 0 landed
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0070);
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags<BM, BN, TM, TN, P, NS, GA, GB>(lds_all, lds_all + GA::TILE, 0, wm, wn, li, lh, f0);
+    int cs = 0;
+    for (int i = 0; i < nk; ++i) {
+      const float* cur = lds_all + cs * GST;
+      const int ns = cs == 2 ? 0 : cs + 1;
+      const float* nxt = lds_all + ns * GST;
+      const bool more = i + 2 < nk;
+      if (more) issue(i + 2, ns == 2 ? 0 : ns + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      read_frags<BM, BN, TM, TN, P, NS, GA, GB>(cur, cur + GA::TILE, 1, wm, wn, li, lh, f1);
+      mfma_half(f0, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) __builtin_amdgcn_s_waitcnt(0x0070 | NIW);
+      else __builtin_amdgcn_s_waitcnt(0x0070);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_part<0, 2>(f1, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      read_frags<BM, BN, TM, TN, P, NS, GA, GB>(nxt, nxt + GA::TILE, 0, wm, wn, li, lh, f0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_part<2, 8 * NS>(f1, acc);
+      cs = ns;
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);
+    __syncthreads();  // the m-contiguous epilogue reuses the stages
+  }
+  bool halo_done = KS == 4;
   if constexpr (HALO) {
     if (args.B.halo) {
       // Tap-chunked conv1d with the halo B layout (LB::store_h): per channel chunk the x window
@@ -1160,7 +1333,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       }
     }
    }
-  } else {
+  } else if constexpr (KS == 2) {
     // The groups take turns staging: group j % 2 loads k-tile j three steps ahead and stores it
     // one step ahead, so a tile's global loads have two k-steps to land (one with a single
     // staging group) at no extra registers.
@@ -1369,7 +1542,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
 }
 
 template <int BM, int BN, int BK, int MA, int MB, int P, int KS = 1>
-__global__ __launch_bounds__(256 * (KS == 1 ? 1 : 2)) void gemm_kernel(GemmArgs args) {
+__global__ __launch_bounds__(256 * ((KS == 1 || KS == 4) ? 1 : 2)) void gemm_kernel(GemmArgs args) {
   span_begin(args.ts);
   gemm_tile<BM, BN, BK, MA, MB, P, KS>(args);
   span_end(args.ts);
@@ -1382,12 +1555,14 @@ template <int BM, int BN, int BK, int P, int KS = 1>
 void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
-  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3(KS == 1 ? 256 : 512), 0, st, a); return; }
+  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3((KS == 1 || KS == 4) ? 256 : 512), 0, st, a); return; }
   // (else-chained, so a wave-group variant instantiates only the mode pairs it serves)
   if constexpr (KS == 2) {  // dense (or channels-last conv, mode 6) operands only (gemm.hip)
     A2M_L(0, 0) A2M_L(0, 6)
   } else if constexpr (KS == 3) {  // dense / gathered weights x tap-chunked conv1d operands (gemm.hip)
     A2M_L(0, 5) A2M_L(0, 3) A2M_L(0, 0)
+  } else if constexpr (KS == 4) {  // LDS-DMA staging: dense weights x dense / channels-last rows
+    A2M_L(0, 0) A2M_L(0, 6)
   } else {
     A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3) A2M_L(0, 4)
     A2M_L(1, 0) A2M_L(1, 1) A2M_L(1, 2) A2M_L(1, 3) A2M_L(1, 4)
@@ -1402,6 +1577,8 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
 extern template void launch_tile<64, 64, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 32, 0, 2>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 32, 0, 3>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<64, 64, 32, 0, 4>(const GemmArgs&, int, int, int, hipStream_t);
+extern template void launch_tile<128, 128, 32, 0, 4>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
