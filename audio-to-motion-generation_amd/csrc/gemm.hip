@@ -537,11 +537,16 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   static const int ks3_maxb = env_int("A2M_GEMM_KS3_MAXB", 256);
   const int64_t blocks64 = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
   const int nt_all = (int)cdiv(K, p.bk);
-  bool use_ks3 = prec == 0 && ks3 && p.bm == 64 && ma == 0 && blocks64 <= ks3_maxb &&
+  // A2M_GEMM_KS3_ROWS=1: the same for one-split channels-last conv rows (mode 6; the encoder's
+  // conv3 is the one such launch, 512 blocks: with A2M_GEMM_KS3_MAXB=512 encoder 0.2988-0.3009
+  // vs 0.2982-0.3011 ms, four rounds, r04p -- neutral, off)
+  static const int ks3_rows = env_int("A2M_GEMM_KS3_ROWS", 0);
+  bool use_ks3 = prec == 0 && p.bm == 64 && ma == 0 && blocks64 <= ks3_maxb &&
                  nt_all % (2 * kquant) == 0 && nt_all >= 8 &&
-                 ((p.splits == 1 && (mb == 5 || mb == 3)) ||
-                  (ks3 >= 2 && p.splits == 2 && force_split <= 0 && g_override_split == 0 &&
-                   (mb == 0 || mb == 3 || mb == 5)));
+                 ((ks3 && ((p.splits == 1 && (mb == 5 || mb == 3)) ||
+                           (ks3 >= 2 && p.splits == 2 && force_split <= 0 && g_override_split == 0 &&
+                            (mb == 0 || mb == 3 || mb == 5)))) ||
+                  (ks3_rows && p.splits == 1 && mb == 6));
   if (use_ks3) { p.splits = 1; p.kchunk = nt_all * p.bk; }
   // A2M_GEMM_HALO=0: mode 5 re-stores the window shifted for every tap (the round-3 loader)
   static const int halo_on = env_int("A2M_GEMM_HALO", 1);

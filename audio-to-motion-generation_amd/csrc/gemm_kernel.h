@@ -1560,7 +1560,7 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   if constexpr (KS == 2) {  // dense (or channels-last conv, mode 6) operands only (gemm.hip)
     A2M_L(0, 0) A2M_L(0, 6)
   } else if constexpr (KS == 3) {  // dense / gathered weights x tap-chunked conv1d operands (gemm.hip)
-    A2M_L(0, 5) A2M_L(0, 3) A2M_L(0, 0)
+    A2M_L(0, 5) A2M_L(0, 3) A2M_L(0, 0) A2M_L(0, 6)
   } else if constexpr (KS == 4) {  // LDS-DMA staging: dense weights x dense / channels-last rows
     A2M_L(0, 0) A2M_L(0, 6)
   } else {
