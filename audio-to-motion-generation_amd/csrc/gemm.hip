@@ -351,7 +351,14 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   double t = per_cu * block_flops / thr + cdiv(per_cu, occ) * fixed + 4.0;
   // A2M_GEMM_SPLIT_COST (percent, experiments): scales the reduce term
   static const double red_scale = env_int("A2M_GEMM_SPLIT_COST", 100) / 100.0;
-  if (splits > 1) t += red_scale * ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0);
+  // channels-last conv rows (the encoder): the reduce priced at A2M_GEMM_SPLIT_COST_ROWS
+  // (default 200 %), so its launches take fewer splits (conv2: 3 instead of 4).  With every
+  // launch's reduce at 200 % the encoder measured 0.2906-0.2937 vs 0.2951-0.2971 ms but the step
+  // neutral to slightly slower (three rounds); on the encoder's launches only: in-step
+  // path_frac 0.480-0.484 vs 0.473-0.476, step 2.718-2.727 vs 2.721-2.737 ms (four rounds, r04s)
+  static const double red_scale_rows = env_int("A2M_GEMM_SPLIT_COST_ROWS", 200) / 100.0;
+  if (splits > 1)
+    t += (conv_rows ? red_scale_rows : red_scale) * ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0);
   return t;
 }
 

@@ -26,18 +26,20 @@ static PhaseTaps phase_taps_h(int r, int k, int s, int pad) {
 }
 
 // P_(rh,rw)[ci][(co*nth + th)*ntw + tw] = W[co][ci][kh0 + s*th][kw0 + s*tw]
+// One block row per ci (blockIdx.y) and 32-bit index math: the flat 64-bit form spent four
+// 64-bit divisions per element, which made the large UNet weights' packs VALU-bound.
 __global__ void dgrad_pack_kernel(const float* w, int Co, int Ci, int kh, int kw, int nth, int ntw,
                                   int kh0, int kw0, int sh, int sw, float* out) {
-  const int64_t total = (int64_t)Ci * Co * nth * ntw;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int tw = (int)(i % ntw);
-    int64_t t = i / ntw;
-    const int th = (int)(t % nth);
-    t /= nth;
-    const int co = (int)(t % Co);
-    const int ci = (int)(t / Co);
-    out[i] = w[(((int64_t)co * Ci + ci) * kh + kh0 + sh * th) * kw + kw0 + sw * tw];
+  const int ci = blockIdx.y;
+  const int per = Co * nth * ntw;   // packed row length (< 2^31: host)
+  const int ntap = nth * ntw;
+  float* orow = out + (int64_t)ci * per;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < per; j += gridDim.x * blockDim.x) {
+    const int co = j / ntap;
+    const int t = j - co * ntap;
+    const int th = ntw == 1 ? t : t / ntw;
+    const int tw = t - th * ntw;
+    orow[j] = w[(((int64_t)co * Ci + ci) * kh + kh0 + sh * th) * kw + kw0 + sw * tw];
   }
 }
 
@@ -59,6 +61,7 @@ int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
                 "conv_dgrad: output geometry mismatch");
   A2M_CHECK_ARG((int64_t)B * Co * Ho * Wo < (1LL << 31) && (int64_t)B * dxs_b < (1LL << 31),
                 "conv_dgrad: too large");
+  A2M_CHECK_ARG(Ci <= 65535 && (int64_t)Co * kh * kw < (1LL << 31), "conv_dgrad: Ci %d > 65535 (pack grid)", Ci);
   const size_t pack_bytes = ((size_t)Ci * Co * kh * kw * sizeof(float) + 255) & ~size_t(255);
   if (!ws || ws_bytes < pack_bytes) {
     set_error("conv_dgrad: workspace too small (%zu < %zu bytes)", ws_bytes, pack_bytes);
@@ -86,8 +89,7 @@ int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
       Bg.cw = K ? (rw + pad_w - tw.k0) / stride_w : 0;
       Bg.divh = Bg.divw = 1; Bg.Lh = Ho; Bg.Lw = Wo; Bg.sh = Wo; Bg.sw = 1; Bg.kcontig = 0;
       if (K > 0) {
-        hipLaunchKernelGGL(dgrad_pack_kernel,
-                           dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Ci * K, 256), 8192)),
+        hipLaunchKernelGGL(dgrad_pack_kernel, dim3((unsigned)std::min<int64_t>(cdiv(K, 256), 64), (unsigned)Ci),
                            dim3(256), 0, st, w, Co, Ci, kh, kw, th.n, tw.n, th.k0, tw.k0, stride_h,
                            stride_w, packed);
         A2M_LAUNCH_CHECK();
