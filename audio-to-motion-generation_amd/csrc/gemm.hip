@@ -321,6 +321,28 @@ static int gemm_xcd_group() {
 
 static int g_override_tile = 0, g_override_split = 0;   // a2m_gemm_plan_override (tuning)
 
+struct PlanRule {
+  int M, N, K, tile, splits;
+};
+static const PlanRule* plan_rule(int M, int N, int K) {
+  static const std::vector<PlanRule> rules = [] {
+    std::vector<PlanRule> v;
+    const char* e = std::getenv("A2M_GEMM_PLAN_RULES");
+    while (e && *e) {
+      PlanRule r{};
+      int used = 0;
+      if (std::sscanf(e, "%d,%d,%d:%d:%d%n", &r.M, &r.N, &r.K, &r.tile, &r.splits, &used) != 5) break;
+      v.push_back(r);
+      e += used;
+      while (*e == ';' || *e == ' ') ++e;
+    }
+    return v;
+  }();
+  for (const PlanRule& r : rules)
+    if (r.M == M && r.N == N && r.K == K) return &r;
+  return nullptr;
+}
+
 static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int tile, int kchunk,
                            int splits, int prec, bool conv_rows = false) {
   static const double thr64[4] = {340e3, 428e3, 435e3, 440e3};   // flop / us per CU
@@ -531,6 +553,15 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   if (force_split > 0) {
     p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk * kquant) * p.bk * kquant);
     p.splits = (int)cdiv(K, p.kchunk);
+  }
+  // A2M_GEMM_PLAN_RULES="M,N,K:tile:splits;..." (tuning experiments): a fixed plan for the
+  // launches of exactly that shape, everything else keeps the planner's
+  if (const PlanRule* r = plan_rule(M, N, K)) {
+    if (r->tile) p.bm = r->tile;
+    if (r->splits > 0) {
+      p.kchunk = (int)(cdiv(cdiv(K, r->splits), p.bk * kquant) * p.bk * kquant);
+      p.splits = (int)cdiv(K, p.kchunk);
+    }
   }
   if (K == 0) { p.splits = 1; p.kchunk = p.bk; }
   // A2M_GEMM_KS3=1: few-block launches (one 64x64 block per CU or less) with a tap-chunked or
