@@ -165,14 +165,17 @@ def gemm_engine_timing(step):
     return t
 
 
-def instep_timing(dev, g, wave, reps=20, warm=None):
+def instep_timing(dev, g, wave, reps=20, warm=None, marks=(0, 2), gemm=True):
     """The bench step captured once more with the engine's span stamps on (every implicit-GEMM
     launch stamps its own first-block start / last-wave end; nothing is added between kernels,
-    so the two decoder branches overlap exactly as in the timed graph) and three wall-clock
-    mark kernels (step start, after the log-mel, after the encoder); the graph is replayed
+    so the two decoder branches overlap exactly as in the timed graph) and wall-clock mark
+    kernels (step start, after the encoder); the graph is replayed
     `reps` times and each replay read back; `warm` (three replays of the timed bench graph) runs
     right before each of those replays, so that each timed replay follows back-to-back work as
     in the timed loop instead of an idle, clocked-down GPU after the previous read's sync.
+    `marks` selects the mark kernels (0 before the log-mel, 1 after it, 2 after the encoder): the
+    mel + encoder interval (0 -> 2) is measured without mark 1 between its kernels, the in-step
+    log-mel (0 -> 1) in a second capture (`gemm=False`: no engine stamps).
     Returns per-step means: the engine's launches /
     FLOPs / tile ms / reduce ms / queued ms (each launch from its ready mark -- a one-thread
     kernel the engine enqueues right before the tile kernel while timing -- to its last block
@@ -181,47 +184,59 @@ def instep_timing(dev, g, wave, reps=20, warm=None):
     This is the basis of `roofline` and of `mel_encoder_roofline.path_frac_instep`;
     tools/step_pmc.sh's rocprof kernel trace of the replayed bench graph is its cross-check
     (profiles/)."""
+    import contextlib
     from a2m import functional as F
     from a2m.mel_features import log_mel_batch
-    hook = g.audio_encoder.register_forward_hook(lambda m, i, o: F.timing_mark(2))
+    hook = (g.audio_encoder.register_forward_hook(lambda m, i, o: F.timing_mark(2))
+            if 2 in marks else None)
 
     def step():
         F.timing_mark(0)
         mel = log_mel_batch(wave)
-        F.timing_mark(1)
+        if 1 in marks:
+            F.timing_mark(1)
         return g(mel)[0]
+    if not gemm:   # the mark buffer lives with the engine's stamp buffer: allocate it
+        with F.gemm_timing():
+            pass
     try:
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             graph = torch.cuda.CUDAGraph()
-            with F.gemm_timing(keep=True) as t:
+            with (F.gemm_timing(keep=True) if gemm else contextlib.nullcontext()) as t:
                 with torch.cuda.graph(graph, stream=s):
                     step()
         torch.cuda.current_stream(dev).wait_stream(s)
     finally:
-        hook.remove()
+        if hook is not None:
+            hook.remove()
     acc = {'launches': 0, 'flops': 0.0, 'ms_tile': 0.0, 'ms_reduce': 0.0, 'ms_queued': 0.0, 'mel_ms': 0.0,
            'mel_enc_ms': 0.0}
     try:
         graph.replay()
         torch.cuda.synchronize()
-        t.read()                     # discard the warm-up replay's stamps (re-arms them)
+        if gemm:
+            t.read()                 # discard the warm-up replay's stamps (re-arms them)
         for _ in range(reps):
             if warm is not None:
                 warm()
             graph.replay()
             torch.cuda.synchronize()
-            t.read()
-            acc['launches'] += t.launches
-            acc['flops'] += t.flops
-            acc['ms_tile'] += t.ms_tile
-            acc['ms_reduce'] += t.ms_reduce
-            acc['ms_queued'] += t.ms_queued
-            acc['mel_ms'] += F.timing_mark_elapsed(0, 1)
-            acc['mel_enc_ms'] += F.timing_mark_elapsed(0, 2)
+            if gemm:
+                t.read()
+                acc['launches'] += t.launches
+                acc['flops'] += t.flops
+                acc['ms_tile'] += t.ms_tile
+                acc['ms_reduce'] += t.ms_reduce
+                acc['ms_queued'] += t.ms_queued
+            if 1 in marks:
+                acc['mel_ms'] += F.timing_mark_elapsed(0, 1)
+            if 2 in marks:
+                acc['mel_enc_ms'] += F.timing_mark_elapsed(0, 2)
     finally:
-        t.release()
+        if gemm:
+            t.release()
         del graph
     out = {k: v / reps for k, v in acc.items()}
     out['launches'] = int(round(out['launches']))
@@ -630,6 +645,7 @@ def main():
         gt = gemm_engine_timing(step)
         warm = None if graph is None else (lambda: [run() for _ in range(3)])
         it = instep_timing(dev, g, wave, warm=warm)
+        it['mel_ms'] = instep_timing(dev, g, wave, warm=warm, marks=(0, 1), gemm=False)['mel_ms']
         disp_ms = dispatch_overhead_ms(dev)
         mel_ms, mel_bytes = run_mel_kernel(dev, wave)
         mel_enc = mel_encoder_roofline(dev, g, wave, mel_ms, mel_bytes, mfma_peak(args.dtype))
