@@ -1006,6 +1006,15 @@ class gemm_timing:
         return False
 
 
+def timing_mark_to_launch_end(slot, rec):
+    """ms from mark `slot` to the last block end of engine launch record `rec` (its tile kernel
+    or split-K reduce) in the latest execution of the kept timing window (no re-arm)."""
+    import ctypes
+    ms = ctypes.c_float()
+    N.check(N.lib.a2m_timing_mark_to_launch_end(int(slot), int(rec), ctypes.byref(ms)))
+    return ms.value
+
+
 def timing_mark(slot):
     """Store the GPU wall clock into mark `slot` from a one-thread kernel on the current stream
     (a node of the graph when capturing; needs gemm_timing to have been entered once)."""

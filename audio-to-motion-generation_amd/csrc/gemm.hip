@@ -905,8 +905,26 @@ int a2m_timing_mark_elapsed(int32_t a, int32_t b, float* ms) {
   return A2M_OK;
 }
 
+int a2m_timing_mark_to_launch_end(int32_t slot, int64_t rec, float* ms) {
+  std::lock_guard<std::mutex> lk(a2m::g_timing_mu);
+  A2M_CHECK_ARG(slot >= 0 && slot < A2M_TIMING_MARKS && a2m::g_ts && ms && rec >= 0 &&
+                    rec < (int64_t)a2m::g_timing_recs.size(),
+                "timing_mark_to_launch_end: slot %d, record %lld", slot, (long long)rec);
+  const int R = a2m::kRecSlots;
+  std::vector<unsigned long long> st(R);
+  unsigned long long m[A2M_TIMING_MARKS];
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(st.data(), a2m::g_ts + (size_t)rec * R, R * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(m, a2m::g_ts + (size_t)a2m::kTimingRecs * R, sizeof(m), hipMemcpyDeviceToHost) != hipSuccess) {
+    a2m::set_error("timing_mark_to_launch_end: stamp read failed");
+    return A2M_EHIP;
+  }
+  unsigned long long hi = 0;
+  for (int q = 0; q < 2 * a2m::kSpanSlots; q += 2)   // tile and reduce slots
+    if (st[q] != ~0ull && st[q + 1] >= st[q]) hi = std::max(hi, st[q + 1]);
+  A2M_CHECK_ARG(hi > 0, "timing_mark_to_launch_end: record %lld has no stamps", (long long)rec);
+  *ms = (float)((double)((long long)(hi - m[slot])) / (a2m::g_wall_mhz * 1e3));
+  return A2M_OK;
+}
+
 }  // extern "C"
-
-namespace a2m {
-
-}  // namespace a2m

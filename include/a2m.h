@@ -553,6 +553,9 @@ int a2m_gemm_timing_read_ex(int64_t* launches, double* flops, double* ms_tile, d
 #define A2M_TIMING_MARKS 16
 int a2m_timing_mark(int32_t slot, void* stream);
 int a2m_timing_mark_elapsed(int32_t a, int32_t b, float* ms);
+/* ms from mark `slot` to the last block end (tile kernel or its split-K reduce) of engine
+ * launch record `rec` of the current timing window, in the latest execution (does not re-arm) */
+int a2m_timing_mark_to_launch_end(int32_t slot, int64_t rec, float* ms);
 
 #ifdef __cplusplus
 }
