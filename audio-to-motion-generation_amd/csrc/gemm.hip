@@ -343,6 +343,25 @@ static const PlanRule* plan_rule(int M, int N, int K) {
   return nullptr;
 }
 
+// Plans tuned in the replayed bench step (fp32; A2M_GEMM_TUNED=0 turns the table off): the
+// UNet's large tap-chunked convs, where the planner's isolated fit prefers 128x128 tiles with 4
+// or 8 splits but the step runs faster on 64x64 tiles with 2 (r04: in-step sweeps with
+// A2M_GEMM_PLAN_RULES, three rounds each, 2.698-2.707 vs 2.716 ms for the first entry;
+// DESIGN.md 6 Round 4)
+static const PlanRule kTunedPlans[] = {
+    {1024, 2048, 6144, 64, 2},   // UNet up conv, T 32
+    {512, 4096, 3072, 64, 2},    // UNet up conv, T 64
+    {512, 2048, 1024, 64, 2},
+    {1024, 1024, 4096, 128, 4},  // the 128 tile kept, 4 splits instead of 8
+};
+static const PlanRule* tuned_plan(int M, int N, int K, int prec) {
+  static const int on = env_int("A2M_GEMM_TUNED", 1);
+  if (!on || prec != 0) return nullptr;
+  for (const PlanRule& r : kTunedPlans)
+    if (r.M == M && r.N == N && r.K == K) return &r;
+  return nullptr;
+}
+
 static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int tile, int kchunk,
                            int splits, int prec, bool conv_rows = false) {
   static const double thr64[4] = {340e3, 428e3, 435e3, 440e3};   // flop / us per CU
@@ -556,7 +575,9 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   }
   // A2M_GEMM_PLAN_RULES="M,N,K:tile:splits;..." (tuning experiments): a fixed plan for the
   // launches of exactly that shape, everything else keeps the planner's
-  if (const PlanRule* r = plan_rule(M, N, K)) {
+  const PlanRule* rule = plan_rule(M, N, K);
+  if (!rule && force_split <= 0 && g_override_split == 0 && g_override_tile == 0) rule = tuned_plan(M, N, K, prec);
+  if (const PlanRule* r = rule) {
     if (r->tile) p.bm = r->tile;
     if (r->splits > 0) {
       p.kchunk = (int)(cdiv(cdiv(K, r->splits), p.bk * kquant) * p.bk * kquant);
