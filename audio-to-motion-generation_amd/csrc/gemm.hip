@@ -354,6 +354,9 @@ static const PlanRule kTunedPlans[] = {
     {512, 2048, 1024, 64, 2},
     {1024, 1024, 4096, 128, 4},  // the 128 tile kept, 4 splits instead of 8
     {2048, 1024, 3072, 128, 2},  // UNet convT phase: 2 splits instead of 4 (2.675-2.698 vs 2.703-2.723 ms)
+    {256, 4096, 2688, 64, 1},    // hand graph-stack output projection: 1 split instead of 2 (weaker
+                                 // evidence: mean 2.694 vs 2.705 ms and 2.719 vs 2.753 ms on two noisy
+                                 // boxes, seven of ten rounds lower)
 };
 static const PlanRule* tuned_plan(int M, int N, int K, int prec) {
   static const int on = env_int("A2M_GEMM_TUNED", 1);
