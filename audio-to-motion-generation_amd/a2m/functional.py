@@ -985,7 +985,7 @@ class gemm_timing:
         self.ms_queued = q.value
         return self
 
-    def spans(self, cap=4096, ready=False):
+    def spans(self, cap=1024, ready=False):
         """[(start_us, end_us)] of every recorded launch's tile kernel in the latest execution
         ([(ready_us, start_us, end_us)] with ready=True; re-arms the stamps like read())."""
         import ctypes

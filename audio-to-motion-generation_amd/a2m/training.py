@@ -145,14 +145,18 @@ class GradReducer:
     force=True arms the reducer also for a one-rank group (the RCCL path exercised on one GPU,
     tests/test_gpu_rccl.py).
 
-    Every rank also all-reduces a small error flag after its buckets, so that a plan violation
-    seen on one rank fails all of them together instead of deadlocking.  The flag is read back on
-    the host (a device sync) only on the first two steps; afterwards it is read at the start of
-    the next finish(), so the backward / optimizer step run ahead of the host as without it, and a
-    violation raises one step late on every rank at the same point.
+    Plan checks: the ranks agree, through a small MAX all-reduce of an error flag, that no rank
+    saw a gradient outside the plan and that all learnt the same parameter set, so a violation
+    fails every rank together instead of leaving one blocked in a bucket all-reduce.  That
+    collective runs on the first SYNC_CHECK_STEPS steps (read back at once: a device sync) and
+    then only every CHECK_EVERY steps, read back at the next finish() so the host keeps running
+    ahead; a violation seen in between is kept (sticky) and raised at the next check on every
+    rank.  flush() runs a check now and reads it -- call it where the ranks must agree that
+    training was sound (end of training, before a checkpoint: GANTrainer.flush()).
     """
 
     SYNC_CHECK_STEPS = 2
+    CHECK_EVERY = 50
 
     def __init__(self, opt, world, group=None, bucket_mb=25.0, reduce_dtype=None, force=False):
         self.opt, self.world, self.group = opt, world, group
@@ -160,6 +164,7 @@ class GradReducer:
         self.reduce_dtype = reduce_dtype
         self.steps = 0
         self._pending_flag = None
+        self._sticky_error = None  # a violation seen since the last check
         spans = list(opt._spans())
         cap = max(int(bucket_mb * (1 << 20) / 4), 1)
         # buckets tile [0, numel) of the flat gradient (alignment padding included: it stays
@@ -260,31 +265,49 @@ class GradReducer:
             work.wait()
             if buf is not sl:
                 sl.copy_(buf)
-        # every rank has issued the same bucket sequence; now agree on whether any rank saw a
-        # gradient outside the plan (or learnt a different parameter set), and fail together
-        n = len(self.expected)
-        flag = torch.tensor([1.0 if self.error else 0.0, n, -n], dtype=torch.float64,
-                            device=self.opt.flat_grad.device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
-        prev, self._pending_flag = self._pending_flag, None
+        if self.error and self._sticky_error is None:
+            self._sticky_error = self.error
         self.steps += 1
         self.active = False
+        # every rank has issued the same bucket sequence; on check steps, agree on whether any
+        # rank saw a gradient outside the plan (or learnt a different parameter set)
+        prev, self._pending_flag = self._pending_flag, None
         if prev is not None:
             self._check_flag(prev)
         if self.steps <= self.SYNC_CHECK_STEPS:
-            self._check_flag(flag)
-        else:
-            self._pending_flag = flag
+            self._check_flag(self._flag())
+        elif self.steps % self.CHECK_EVERY == 0:
+            self._pending_flag = self._flag()
         if self.world > 1:
             self.opt.flat_grad.div_(self.world)
         return self.opt.flat_grad
+
+    def _flag(self):
+        n = len(self.expected) if self.expected is not None else 0
+        flag = torch.tensor([1.0 if self._sticky_error else 0.0, n, -n], dtype=torch.float64,
+                            device=self.opt.flat_grad.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        return flag
+
+    @torch.no_grad()
+    def flush(self):
+        """Collective (every rank at the same point): read any outstanding check, run one now,
+        raise on every rank if any saw a violation since the last check."""
+        if not (self.world > 1 or self.force) or self.expected is None:
+            return
+        prev, self._pending_flag = self._pending_flag, None
+        if prev is not None:
+            self._check_flag(prev)
+        self._check_flag(self._flag())
 
     def _check_flag(self, flag):
         f = flag.tolist()
         if f[0] > 0 or f[1] != -f[2]:
             self._pending_flag = None
-            raise RuntimeError(self.error or 'GradReducer: a rank received gradients outside the '
-                                             'learnt parameter set')
+            msg = self._sticky_error or self.error
+            self._sticky_error = None
+            raise RuntimeError(msg or 'GradReducer: a rank received gradients outside the '
+                                      'learnt parameter set')
 
 
 class GANTrainer:
@@ -397,6 +420,12 @@ class GANTrainer:
             yield
         finally:
             F.set_sync_bn_group(prev)
+
+    def flush(self):
+        """Collective: both gradient reducers' plan checks, now (end of training, before a
+        checkpoint); raises on every rank if any rank's gradients left the learnt plan."""
+        self.red_G.flush()
+        self.red_D.flush()
 
     def iteration(self, audio, real_pose, epoch=0, g_freq=None, d_freq=None, sync_losses=True):
         """version5_model_train.py:330-414 for one batch; returns (D_loss, G_loss) tensors."""

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "gemm_kernel.h"
+#include "gemm_pipe.h"
 
 namespace a2m {
 
@@ -332,7 +333,9 @@ static const PlanRule* plan_rule(int M, int N, int K) {
       PlanRule r{};
       int used = 0;
       if (std::sscanf(e, "%d,%d,%d:%d:%d%n", &r.M, &r.N, &r.K, &r.tile, &r.splits, &used) != 5) break;
-      v.push_back(r);
+      if ((r.tile == 0 || r.tile == 64 || r.tile == 128) && r.splits >= 0 && r.splits <= 256) v.push_back(r);
+      else std::fprintf(stderr, "a2m: A2M_GEMM_PLAN_RULES entry %d,%d,%d:%d:%d ignored (tile 0/64/128, splits 0..256)\n",
+                        r.M, r.N, r.K, r.tile, r.splits);
       e += used;
       while (*e == ';' || *e == ' ') ++e;
     }
@@ -443,49 +446,46 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, in
   return p;
 }
 
-// slab workspace of a split plan: [splits][batch][M][N] for the reduce kernel, or whole padded
-// tiles [batch * tiles][splits][BM * BN] for the in-launch combine (the larger is reserved)
+// slab workspace of a split plan: [splits][batch][M][N] for the reduce kernel
 static size_t split_ws_bytes(const Plan& p, int M, int N, int batch) {
-  const size_t padded = (size_t)cdiv(M, p.bm) * p.bm * cdiv(N, p.bm) * p.bm;
-  return (size_t)p.splits * batch * std::max((size_t)M * N, padded) * sizeof(float);
+  return (size_t)p.splits * batch * M * (size_t)N * sizeof(float);
+}
+
+// the plan gemm() launches: the planner's, unless a tuned-table entry or an A2M_GEMM_PLAN_RULES
+// rule fixes the tile / split count for the shape
+static Plan launch_plan(int M, int N, int K, int batch, bool gathered, int prec, int kquant, bool rows6,
+                        int force_split) {
+  Plan p = plan_for(M, N, K, batch, gathered, prec, kquant, rows6);
+  if (force_split > 0) {
+    p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk * kquant) * p.bk * kquant);
+    p.splits = (int)cdiv(K, p.kchunk);
+  }
+  const PlanRule* rule = plan_rule(M, N, K);
+  if (!rule && force_split <= 0 && g_override_split == 0 && g_override_tile == 0) rule = tuned_plan(M, N, K, prec);
+  if (const PlanRule* r = rule) {
+    if (r->tile) p.bm = r->tile;
+    if (r->splits > 0) {
+      p.kchunk = (int)(cdiv(cdiv(K, r->splits), p.bk * kquant) * p.bk * kquant);
+      p.splits = (int)cdiv(K, p.kchunk);
+    }
+  }
+  if (K == 0) { p.splits = 1; p.kchunk = p.bk; }
+  return p;
 }
 
 size_t gemm_ws_bytes(int M, int N, int K, int batch) {
-  // either operand orientation (the plan depends on whether an operand is row-gathered) and
-  // either precision
+  // every plan gemm() may launch for the shape: either operand orientation (the plan depends on
+  // whether an operand is row-gathered), either precision, conv rows or not, the tap-chunk
+  // quantum of a tap-chunked conv (1-3 taps), and the tuned / rule overrides
   size_t need = 0;
   for (bool gathered : {false, true})
     for (int prec : {0, 1, 2})
-      for (bool rows6 : {false, true}) {
-        const Plan p = plan_for(M, N, K, batch, gathered, prec, 1, rows6);
-        if (p.splits > 1) need = std::max(need, split_ws_bytes(p, M, N, batch));
-      }
+      for (bool rows6 : {false, true})
+        for (int kq : {1, 2, 3}) {
+          const Plan p = launch_plan(M, N, K, batch, gathered, prec, kq, rows6, 0);
+          if (p.splits > 1) need = std::max(need, split_ws_bytes(p, M, N, batch));
+        }
   return need;
-}
-
-// Arrival counters of the in-launch split-K combine: one int per output tile of a launch, taken
-// from a ring so that launches that may run concurrently (the decoder branches' streams, graph
-// replays) use disjoint counters; every counter is 0 between launches (zeroed once here, reset
-// by each tile's last arriver).  Allocated outside graph capture (the eager warm-up launches);
-// a launch captured before then keeps the reduce kernel.
-constexpr size_t kCntRing = 1 << 20;
-static int* g_cnt = nullptr;
-static size_t g_cnt_next = 0;
-static std::mutex g_cnt_mu;
-
-static int* fixup_counters(size_t tiles, hipStream_t stream) {
-  std::lock_guard<std::mutex> lk(g_cnt_mu);
-  if (!g_cnt) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-    if (hipMalloc(&g_cnt, kCntRing * sizeof(int)) != hipSuccess) { g_cnt = nullptr; return nullptr; }
-    if (hipMemset(g_cnt, 0, kCntRing * sizeof(int)) != hipSuccess) return nullptr;
-  }
-  if (tiles > kCntRing / 4) return nullptr;
-  if (g_cnt_next + tiles > kCntRing) g_cnt_next = 0;
-  int* c = g_cnt + g_cnt_next;
-  g_cnt_next += (tiles + 63) / 64 * 64;
-  return c;
 }
 
 // Optional per-launch timing of the engine (bench.py's live roofline).  While enabled, every
@@ -571,56 +571,16 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   const int kquant = mb == 5 ? B.tapconv : 1;
   // gathered: row-vector staging (modes 2 / 3) or gathers; k-contiguous conv rows (mode 6) load
   // like dense rows
-  Plan p = plan_for(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || (mb >= 3 && mb != 6), prec, kquant,
-                    mb == 6);
-  if (force_split > 0) {
-    p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk * kquant) * p.bk * kquant);
-    p.splits = (int)cdiv(K, p.kchunk);
-  }
-  // A2M_GEMM_PLAN_RULES="M,N,K:tile:splits;..." (tuning experiments): a fixed plan for the
-  // launches of exactly that shape, everything else keeps the planner's
-  const PlanRule* rule = plan_rule(M, N, K);
-  if (!rule && force_split <= 0 && g_override_split == 0 && g_override_tile == 0) rule = tuned_plan(M, N, K, prec);
-  if (const PlanRule* r = rule) {
-    if (r->tile) p.bm = r->tile;
-    if (r->splits > 0) {
-      p.kchunk = (int)(cdiv(cdiv(K, r->splits), p.bk * kquant) * p.bk * kquant);
-      p.splits = (int)cdiv(K, p.kchunk);
-    }
-  }
-  if (K == 0) { p.splits = 1; p.kchunk = p.bk; }
-  // A2M_GEMM_KS3=1: few-block launches (one 64x64 block per CU or less) with a tap-chunked or
-  // row-gathered B split the k range across the block's two wave groups (KS = 3): each SIMD
-  // runs two independent k pipelines.  Faster alone (the decoder conv 30.7 -> 28.8 us) and
-  // in the round-2 step, but off since round 3: in the two-stream step its 75 KB-LDS blocks
-  // cannot share a CU with the graph stack's workgroups, and the plain 64x64 tile measured
-  // 2.704-2.713 vs 2.717-2.724 ms (three pairs).  A2M_GEMM_KS3=2 also turns two-way split-K
-  // plans on such launches into KS = 3 (measured slower on every such launch).
-  static const int ks3 = env_int("A2M_GEMM_KS3", 0);
-  static const int ks3_maxb = env_int("A2M_GEMM_KS3_MAXB", 256);
-  const int64_t blocks64 = cdiv(M, 64) * cdiv(N, 64) * (int64_t)batch;
-  const int nt_all = (int)cdiv(K, p.bk);
-  // A2M_GEMM_KS3_ROWS=1: the same for one-split channels-last conv rows (mode 6; the encoder's
-  // conv3 is the one such launch, 512 blocks: with A2M_GEMM_KS3_MAXB=512 encoder 0.2988-0.3009
-  // vs 0.2982-0.3011 ms, four rounds, r04p -- neutral, off)
-  static const int ks3_rows = env_int("A2M_GEMM_KS3_ROWS", 0);
-  bool use_ks3 = prec == 0 && p.bm == 64 && ma == 0 && blocks64 <= ks3_maxb &&
-                 nt_all % (2 * kquant) == 0 && nt_all >= 8 &&
-                 ((ks3 && ((p.splits == 1 && (mb == 5 || mb == 3)) ||
-                           (ks3 >= 2 && p.splits == 2 && force_split <= 0 && g_override_split == 0 &&
-                            (mb == 0 || mb == 3 || mb == 5)))) ||
-                  (ks3_rows && p.splits == 1 && mb == 6));
-  if (use_ks3) { p.splits = 1; p.kchunk = nt_all * p.bk; }
+  const Plan p = launch_plan(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || (mb >= 3 && mb != 6), prec,
+                             kquant, mb == 6, force_split);
   // A2M_GEMM_HALO=0: mode 5 re-stores the window shifted for every tap (the round-3 loader)
   static const int halo_on = env_int("A2M_GEMM_HALO", 1);
-  a.B.halo = halo_on && mb == 5 && prec == 0 && p.bm == 64 && !use_ks3 && B.tapconv == 3 &&
+  a.B.halo = halo_on && mb == 5 && prec == 0 && p.bm == 64 && B.tapconv == 3 &&
              B.cw == -1 && B.R2 >= 16 && 64 % B.R2 == 0;
   a.splits = p.splits;
   a.kchunk = p.kchunk;
   a.partial = nullptr;
   a.xcd_group = gemm_xcd_group();
-  static const int skew = env_int("A2M_GEMM_KS3_SKEW", 1);
-  a.skew = skew;
   static const int stage_m = env_int("A2M_GEMM_MCONTIG", 1);
   // fused resample (E.interp_T): the tile always writes raw slabs (also at one split) and the
   // reduce kernel runs epilogue + resample
@@ -629,29 +589,25 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                             (size_t)E.interp_H * sizeof(float) <= 32768),
                 "gemm: fused resample needs batch 1, N a multiple of H = %d <= 8192", E.interp_H);
   a.mcontig = stage_m && E.som == 1 && M > 1 && !interp;
-  // in-launch split-K combine (A2M_GEMM_FIXUP=1; default: the reduce kernel): the one-group tiles
-  // (not the two-group KS = 2 / 3 variants), up to 16 splits (more: the wide reduce kernel)
-  // Off by default: with the 16 KB limit it measured neutral (2.719 vs 2.720 ms, three pairs, r04k)
-  static const int fix_on = env_int("A2M_GEMM_FIXUP", 0);
   static const int ks2 = env_int("A2M_GEMM_KS2", 1);
-  const bool ks2_launch = prec == 0 && p.bm == 64 && !use_ks3 && ks2 && ma == 0 &&
-                          (mb == 0 || (ks2 == 2 && mb == 6));
-  // the last arriver reads the other S - 1 slabs serially (sc1, from memory): measured a net loss
-  // where that exceeds a few tens of KB (128x128 tiles at 4-8 splits: step 2.86 vs 2.76 ms with
-  // every launch combined in-kernel, r04k), so only up to A2M_GEMM_FIXUP_KB (default 16) of slabs
-  static const int fix_kb = env_int("A2M_GEMM_FIXUP_KB", 16);
-  // LDS-DMA operand staging (KS = 4, A2M_GEMM_GLDS: 1 = 64x64 tiles, 2 = also 128x128): fp32,
-  // dense weights x dense / channels-last conv rows (modes 0 / 6 over 16-byte aligned rows)
-  static const int glds_on = env_int("A2M_GEMM_GLDS", 0);
-  const bool rows_ok = mb == 6 || (B.sr0 % 4 == 0 && B.bstride % 4 == 0);
-  const bool glds_launch = glds_on && prec == 0 && !use_ks3 && ma == 0 && (mb == 0 || mb == 6) &&
-                           rows_ok && (p.bm == 64 || glds_on >= 2);
-  a.cnt = nullptr;
-  if (fix_on && p.splits > 1 && p.splits <= 16 && !interp && !use_ks3 && !ks2_launch && !glds_launch &&
-      (p.splits - 1) * p.bm * p.bm * 4 <= fix_kb * 1024)
-    a.cnt = fixup_counters((size_t)cdiv(M, p.bm) * cdiv(N, p.bm) * batch, stream);
+  // software-pipelined one-wave-per-SIMD tile (gemm_pipe.h; A2M_GEMM_PIPE=0 restores gemm_tile):
+  // fp32 64x64, dense weights x dense rows / channels-last rows / halo tap conv, every element
+  // offset below 2^29 floats (raw buffer loads)
+  static const int pipe_on = env_int("A2M_GEMM_PIPE", 1);
+  auto below = [](int64_t v) { return v >= 0 && v < ((int64_t)1 << 29); };
+  bool pipe_ext = below((int64_t)(M - 1) * A.sr0 + K);
+  if (mb == 0) pipe_ext = pipe_ext && below((int64_t)(N - 1) * B.sr0 + K);
+  else if (mb == 6) pipe_ext = pipe_ext && below((int64_t)((N - 1) / (B.R1 * B.R2)) * B.sr0 + (int64_t)B.Lh * B.Lw * B.nhwc);
+  else if (mb == 5) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)(K / 3) * B.sk0);
+  else if (mb == 3) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)K * B.sk0);
+  // mode 3 in its plain form only: k = channel, rows (b, t) at unit stride in groups of 4
+  const bool rows3 = mb == 3 && B.K1 == 1 && B.K2 == 1 && B.R1 == 1 && B.ch == 0 && B.cw == 0 &&
+                     B.divh == 1 && B.divw == 1 && N % 4 == 0 &&
+                     ((B.R2 == 1 && B.sr0 == 1) || (B.R2 % 4 == 0 && B.ar2 == 1 && B.sw == 1 && B.Lw >= B.R2));
+  const bool pipe_launch = pipe_on && prec == 0 && p.bm == 64 && ma == 0 &&
+                           (mb == 0 || mb == 6 || (mb == 5 && a.B.halo) || rows3) && pipe_ext;
   if (p.splits > 1 || interp) {
-    const size_t need = a.cnt ? split_ws_bytes(p, M, N, batch) : (size_t)p.splits * batch * M * N * sizeof(float);
+    const size_t need = split_ws_bytes(p, M, N, batch);
     if (ws == nullptr || ws_bytes < need) {
       set_error("gemm: workspace too small (%zu < %zu bytes)", ws_bytes, need);
       return A2M_EWS;
@@ -661,7 +617,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   static const int log_launches = env_int("A2M_GEMM_LOG", 0);
   if (log_launches)
     std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d%s modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
-                 M, N, K, batch, p.bm, p.bk, p.splits, a.cnt ? " (in-launch)" : "", ma, mb, E.som, E.so0, E.so1,
+                 M, N, K, batch, p.bm, p.bk, p.splits, pipe_launch ? " (pipe)" : "", ma, mb, E.som, E.so0, E.so1,
                  E.so2, E.N1, E.N2);
   a.ts = nullptr;
   if (g_timing) {
@@ -670,7 +626,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                   batch, p.bm, p.splits, ma, mb);
     a.ts = timing_open(2.0 * M * N * (double)K * batch, desc);
     if (a.ts) {
-      g_timing_recs.back().reduce = (p.splits > 1 && !a.cnt) || interp;
+      g_timing_recs.back().reduce = p.splits > 1 || interp;
       // A2M_GEMM_TIMING_READY=1 (diagnostic): the ready mark.  Off by default: the extra kernel
       // per launch shifts how the two decoder branches share the CUs (tools/stamp_vs_trace.py)
       static const int ready = env_int("A2M_GEMM_TIMING_READY", 0);
@@ -684,10 +640,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     if (p.bm == 128) launch_tile<128, 128, 32, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
   } else {
-    if (glds_launch && p.bm == 128) launch_tile<128, 128, 32, 0, 4>(a, ma, mb, batch, stream);
-    else if (glds_launch) launch_tile<64, 64, 32, 0, 4>(a, ma, mb, batch, stream);
+    if (pipe_launch) launch_pipe(a, mb, batch, stream);
     else if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
-    else if (use_ks3) launch_tile<64, 64, 32, 0, 3>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
     // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end
     // (A2M_GEMM_KS2=2 also for channels-last conv rows, mode 6: the encoder measured 305.8 us
@@ -705,7 +659,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     hipLaunchKernelGGL(splitk_reduce_interp_kernel, dim3((unsigned)cdiv((int64_t)M * nb, RB)), dim3(256),
                        (size_t)RB * H * sizeof(float), stream, a, nb, RB, wide);
     A2M_LAUNCH_CHECK();
-  } else if (p.splits > 1 && !a.cnt) {
+  } else if (p.splits > 1) {
     const int inner = a.mcontig ? M : N;
     const int64_t total = (int64_t)M * N * batch / ((inner & 3) == 0 ? 4 : 1);
     static const int wide_on = env_int("A2M_GEMM_WIDE_REDUCE", 1);
@@ -778,8 +732,10 @@ int a2m_gemm_timing_read_ex(int64_t* launches, double* flops, double* ms_tile, d
     a2m::set_error("gemm timing: stamp read failed");
     return A2M_EHIP;
   }
-  // a kernel's duration: its longest per-XCD span (-1: no XCD stamped, i.e. it did not run since
-  // the last reset); *global: last end - first start over all XCDs (diagnostic)
+  // a kernel's duration: last block end - first block start over all XCDs (s_memrealtime is the
+  // chip's one constant-rate clock, so stamps from different XCDs are comparable: the same
+  // assumption as ms_queued and a2m_timing_mark_to_launch_end); -1: nothing stamped since the
+  // last reset.  *global is that interval, the return value too (kept for the log line).
   auto span = [](const unsigned long long* s, double* global) {
     double best = -1.0;
     unsigned long long glo = ~0ull, ghi = 0;
@@ -797,7 +753,7 @@ int a2m_gemm_timing_read_ex(int64_t* launches, double* flops, double* ms_tile, d
       ghi = std::max(ghi, hi);
     }
     *global = ghi >= glo ? (double)(ghi - glo) : -1.0;
-    return best;
+    return best < 0 ? -1.0 : *global;
   };
   int64_t n = 0, nr = 0;
   double f = 0, mt = 0, mr = 0, mq = 0;

@@ -41,11 +41,8 @@ struct GemmArgs {
   int xcd_group;   // >0: XCD-aware block remap with this many M-tiles per group; 0: identity
   int mcontig;     // output has unit m stride: the tile is staged through LDS and written
                    // along m (split-K slabs then are [N][M])
-  int skew;        // KS = 3: wave group 1 runs its k-steps half a step after group 0's
   unsigned long long* ts;   // measurement only (a2m_gemm_timing_*; null otherwise): this launch's
                             // span stamps, [tile | reduce][XCD][first start, last end]
-  int* cnt;        // split-K combined in the launch (gemm_tile's epilogue): one arrival counter
-                   // per output tile (0 between launches); null: slabs for the reduce kernel
 };
 
 // Launch-span stamps (bench.py's in-step roofline): per XCD, the earliest block start and the
@@ -679,106 +676,6 @@ struct TileLoader {
   }
 };
 
-// LDS-DMA operand staging (KS = 4; fp32, BK = 32; dense rows, mode 0, or channels-last conv
-// rows, mode 6): every k-tile row's 32 floats (128 B) go global -> LDS with
-// global_load_lds_dwordx4, no register round trip, into an unpadded [row][32] image whose 16-B
-// quads are XOR-swizzled by row (slot s of row r holds quad s ^ (r & 7)): one wave-instruction
-// fills 8 whole rows (its LDS destination is lane-linear), the swizzle is applied to the global
-// source addresses, and the fragment reads un-swizzle it, which keeps their ds_read_b128s
-// spread over the banks.  Rows / k outside the operand (and mode 6's padding pixels) read a
-// 16-B zero block instead.
-static __device__ __attribute__((aligned(16))) float g_glds_zero[4];
-template <int BR, int MODE>
-struct GldsLoader {
-  static_assert(MODE == 0 || MODE == 6, "LDS-DMA staging: k-contiguous rows only");
-  static constexpr int BK = 32;
-  static constexpr int TILE = BR * BK;     // floats
-  static constexpr int RPW = BR / 4;       // rows per wave
-  static constexpr int NI = RPW / 8;       // wave-instructions per k-tile
-  const Gather* g;
-  const float* base;
-  int K;
-  int rbase[NI];
-  int rh[NI], rw[NI];
-  bool rval[NI];
-  int qo;                                  // this lane's source quad offset (floats)
-  int lrow0;                               // the wave's first tile row
-  int k6, i6, j6, c6;
-  __device__ __forceinline__ void init(const Gather& gg, int z, int row0, int R, int KK, int tid, int kbeg) {
-    g = &gg;
-    base = gg.base + (int64_t)z * gg.bstride;
-    K = KK;
-    const int wave = tid >> 6, lane = tid & 63;
-    lrow0 = wave * RPW;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int row = lrow0 + 8 * j + (lane >> 3);
-      RowInfo ri = row_info(gg, row0 + row, R);
-      if (MODE == 6) ri.base += (ri.h * gg.Lw + ri.w) * gg.nhwc;
-      rbase[j] = ri.base;
-      rh[j] = ri.h;
-      rw[j] = ri.w;
-      rval[j] = ri.valid;
-    }
-    // the lane's row & 7 is (lane >> 3) & 7 for every instruction (rows 8j + lane / 8)
-    qo = 4 * ((lane & 7) ^ ((lane >> 3) & 7));
-    if (MODE == 6) {
-      const int tap = kbeg / gg.nhwc;
-      k6 = kbeg;
-      c6 = kbeg - tap * gg.nhwc;
-      i6 = tap / gg.K2;
-      j6 = tap - i6 * gg.K2;
-    }
-  }
-  // k-tile k0 into the stage image lds (all waves; completion counted by vmcnt)
-  __device__ __forceinline__ void issue(int k0, float* lds) {
-    int toff = 0, ti = 0, tj = 0;
-    if (MODE == 6) {
-      const int Ci = g->nhwc;
-      while (k6 < k0) {
-        k6 += BK;
-        c6 += BK;
-        if (c6 == Ci) {
-          c6 = 0;
-          if (++j6 == g->K2) { j6 = 0; ++i6; }
-        }
-      }
-      ti = i6;
-      tj = j6;
-      toff = (ti * g->Lw + tj) * Ci + c6;
-    }
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const float* src;
-      if (MODE == 0) {
-        const int k = k0 + qo;
-        src = rval[j] && k < K ? base + rbase[j] + k : g_glds_zero;
-      } else {
-        const int h = rh[j] + ti, w = rw[j] + tj;
-        const bool ok = rval[j] && k0 < K && (unsigned)h < (unsigned)g->Lh && (unsigned)w < (unsigned)g->Lw;
-        src = ok ? base + rbase[j] + toff + qo : g_glds_zero;
-      }
-      // inline asm, not the builtin: the compiler cannot tell the builtin's LDS writes from the
-      // fragment reads of the other stages and waits vmcnt(0) before every k-step's reads, which
-      // drains the DMAs meant to stay in flight; the k loop counts them itself (s_waitcnt vmcnt)
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)(lds + (lrow0 + 8 * j) * BK));
-      uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-    }
-  }
-  // the 8 k-values (k = 16 half + 8 lh + s) of tile row `row`
-  __device__ __forceinline__ static void frag(const float* lds, int row, int half, int lh, float* f) {
-    const float* rp = lds + row * BK;
-    const int q0 = 4 * half + 2 * lh, sw = row & 7;
-    const float4 v0 = *reinterpret_cast<const float4*>(rp + 4 * (q0 ^ sw));
-    const float4 v1 = *reinterpret_cast<const float4*>(rp + 4 * ((q0 + 1) ^ sw));
-    f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w;
-    f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
-  }
-};
-
 __device__ __forceinline__ int64_t epi_addr(const Epilogue& E, int m, int n) {
   int n2 = n % E.N2;
   int t = n / E.N2;
@@ -984,6 +881,78 @@ __device__ __forceinline__ void ablate_touch(const FR& f, floatx16 (&acc)[TM][TN
                                                   __builtin_bit_cast(uint32_t, f.b[0][0])) * 1e-30f;
 }
 
+// Tile epilogue (shared by gemm_tile and gemm_pipe_kernel): the accumulators of the block's
+// BM x BN tile (wave (wm, wn) holds rows wm*BM/2 + t*32 + (q&3) + 8(q>>2) + 4lh, columns
+// wn*BN/2 + u*32 + li) as split-K slabs (slab_out) or through the fused epilogue; m-contiguous
+// outputs are staged through lds (>= BN * (BM + 1) floats, free when called).
+template <int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& args, const floatx16 (&acc)[TM][TN], float* lds,
+                                              const EpiRow* epr, bool slab_out, int zz, int batch, int m0,
+                                              int n0, int tid, int wm, int wn, int li, int lh) {
+  if (args.mcontig) {
+    // m-contiguous output (node-feature layouts [.., J*64]): a direct store would put the 32
+    // lanes of each instruction (consecutive n) M floats apart.  Stage the tile as Cs[n][m]
+    // (pitch BM + 1) in the now idle LDS and write it out along m instead.
+    constexpr int LDC = BM + 1;
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          lds[(wn * (BN / 2) + u * 32 + li) * LDC + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) +
+              4 * lh] = acc[t][u][q];
+    __syncthreads();
+    const int ml = tid % BM;
+    const int m = m0 + ml;
+    if (m < args.M) {
+      if (slab_out) {
+        for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
+          const int n = n0 + nl;
+          if (n >= args.N) break;
+          args.partial[(int64_t)zz * args.M * args.N + (int64_t)n * args.M + m] = lds[nl * LDC + ml];
+        }
+      } else {
+        const EpiRow r = epr[ml];
+        const int64_t am = (int64_t)m * args.E.som;
+        EpiCol c;
+        c.set(args.E, n0 + tid / BM);
+        for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
+          if (n0 + nl >= args.N) break;
+          epi_store_p(args.E, batch, lds[nl * LDC + ml], r, c.addr(args.E) + am);
+          c.advance(args.E, 256 / BM);
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int u = 0; u < TN; ++u) {
+    const int n = n0 + wn * (BN / 2) + u * 32 + li;
+    if (n >= args.N) continue;
+    if (slab_out) {
+      float* dst = args.partial + (int64_t)zz * args.M * args.N + n;
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = m0 + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+          if (m < args.M) dst[(int64_t)m * args.N] = acc[t][u][q];
+        }
+    } else {
+      const int64_t an = epi_addr(args.E, 0, n);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int ml = wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+          const int m = m0 + ml;
+          if (m < args.M) epi_store_p(args.E, batch, acc[t][u][q], epr[ml], an + (int64_t)m * args.E.som);
+        }
+    }
+  }
+}
+
 // H = false: fp32 operands, v_mfma_f32_32x32x2_f32, BK = 32 (two 16-k halves).
 // H = true:  operands rounded to bf16 (RNE) when staged in LDS, v_mfma_f32_32x32x16_bf16 with
 //            fp32 accumulation, BK = 64 (two 32-k halves of two K16 chunks).
@@ -992,44 +961,25 @@ __device__ __forceinline__ void ablate_touch(const FR& f, floatx16 (&acc)[TM][TN
 // other's issue gaps at one block per CU); the groups stage alternate k-tiles, the partial
 // accumulators are summed through LDS before the epilogue.  (The k-halves of one k-tile are added in a
 // different order than KS = 1: results agree to fp32 rounding, not bitwise.)
-// KS = 3 (64x64 fp32 tile, any operand modes): 512 threads, two wave groups that each run the
-// whole KS = 1 pipeline (own LDS stages) over one half of the k range, in lockstep barriers;
-// the partial accumulators are summed through LDS as for KS = 2.  For launches with few blocks
-// (one per CU), where a single wave per SIMD leaves the MFMA pipe idle between its own LDS /
-// barrier waits.  The host splits the k range on whole k-tile groups (mode 5: whole channel
-// chunks, all taps).
 template <int BM, int BN, int BK, int MA, int MB, int P, int KS = 1>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
   static_assert(P == 0 ? (BK == 32 || BK == 64) : BK == (P == 1 ? 64 : 32),
                 "the k-step pipeline assumes two halves per k-tile");
   constexpr int NS = P == 0 ? BK / 32 : 1;   // fp32: 16-k fragment chunks per half
-  static_assert(KS == 1 || P == 0, "two wave groups / LDS-DMA staging: fp32 tiles only");
+  static_assert(KS == 1 || (KS == 2 && P == 0), "two wave groups: fp32 tiles only");
   constexpr int TM = BM / 64, TN = BN / 64;
   using LA = TileLoader<BM, BK, MA, P>;
   using LB = TileLoader<BN, BK, MB, P>;
   constexpr int STAGE = LA::TILE + LB::TILE;
   // mode-5 halo layout: two A stages + two chunk-wide B stages (tile_halo below)
   constexpr bool HALO = MB == 5 && P == 0 && KS == 1 && BN == 64;
-  // KS = 4: three LDS-DMA stages of unpadded [row][32] images
-  constexpr int GSTAGE = (BM + BN) * 32;
-  constexpr int LDS_F = KS == 4 ? (3 * GSTAGE > 2 * STAGE ? 3 * GSTAGE : 2 * STAGE) : (KS == 3 ? 4 : 2) * STAGE;
+  constexpr int LDS_F = 2 * STAGE;
   constexpr int LDS_H = HALO ? 2 * LA::TILE + 2 * LB::TILE_H : 0;
   constexpr int LDS_T = LDS_F > LDS_H ? LDS_F : LDS_H;
-  // KS = 4 keeps the epilogue constants inside the one staging array: with a second __shared__
-  // object the compiler cannot tell the LDS-DMA writes from the fragment reads and waits
-  // vmcnt(0) before every k-step's reads
-  constexpr int EPR_F = KS == 4 ? (int)((BM * sizeof(EpiRow) + 15) / 16 * 4) : 0;
-  __shared__ __attribute__((aligned(16))) float lds_all[LDS_T + EPR_F];
-  EpiRow* epr;   // the block's per-row epilogue constants (final-output launches)
-  if constexpr (KS == 4) {
-    epr = reinterpret_cast<EpiRow*>(lds_all + LDS_T);
-  } else {
-    __shared__ EpiRow epr_arr[BM];
-    epr = epr_arr;
-  }
+  __shared__ __attribute__((aligned(16))) float lds[LDS_T];
+  __shared__ EpiRow epr[BM];   // the block's per-row epilogue constants (final-output launches)
   static_assert(KS == 1 || (TM * TN * 16 * 256 <= 2 * STAGE), "KS = 2 partials must fit the stages");
-  const int grp = (KS == 1 || KS == 4) ? 0 : (int)(threadIdx.x >> 8);
-  float* lds = KS == 3 ? lds_all + grp * 2 * STAGE : lds_all;
+  const int grp = KS == 1 ? 0 : (int)(threadIdx.x >> 8);
   const int tid = threadIdx.x & 255;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -1064,25 +1014,17 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
   const int zz = bz;
   const int batch = zz / args.splits, split = zz % args.splits;
   const int m0 = by * BM, n0 = bx * BN;
-  int kbeg = split * args.kchunk;
-  int kend = min(args.K, kbeg + args.kchunk);
-  if constexpr (KS == 3) {   // group g: k-tiles [g * nt / 2, (g + 1) * nt / 2) of the block's range
-    const int nt = (kend - kbeg + BK - 1) / BK;
-    const int mid = kbeg + (nt / 2) * BK;
-    if (grp == 0) kend = mid;
-    else kbeg = mid;
-  }
+  const int kbeg = split * args.kchunk;
+  const int kend = min(args.K, kbeg + args.kchunk);
 
   // epilogue constants of the block's rows, visible after the k loop's first barrier
-  if ((!args.partial || args.cnt) && grp == 0 && tid < BM && m0 + tid < args.M)
+  if (!args.partial && grp == 0 && tid < BM && m0 + tid < args.M)
     epr[tid] = epi_row(args.E, m0 + tid + batch * args.E.pstride);
 
   LA la;
   LB lb;
-  if constexpr (KS != 4) {
-    la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
-    lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
-  }
+  la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
+  lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
 
   floatx16 acc[TM][TN];
 #pragma unroll
@@ -1093,65 +1035,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
 
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
-  if constexpr (KS == 4) {
-    // LDS-DMA pipeline (GldsLoader): tiles land in a ring of three LDS stages two k-steps ahead
-    // of the MFMAs, with no register staging.  Step i: issue tile i + 2 into the stage tile i - 1
-    // used (every wave is past step i - 1's barrier, after its last reads of it), read the second
-    // half's fragments, first-half MFMAs, then wait for this wave's tile i + 1 (vmcnt counted:
-    // tile i + 2's NIW DMAs may stay in flight) and its fragment reads, a raw barrier (no
-    // __syncthreads: its fence would drain the in-flight DMAs), next tile's first fragments
-    // behind the second half's first MFMAs.
-    using GA = GldsLoader<BM, MA>;
-    using GB = GldsLoader<BN, MB>;
-    constexpr int GST = GA::TILE + GB::TILE;
-    constexpr int NIW = GA::NI + GB::NI;   // DMAs per wave per k-tile
-    static_assert(NIW < 16, "vmcnt immediate");
-    GA ga;
-    GB gb;
-    ga.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
-    gb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
-    auto issue = [&](int t, int stage) {
-      float* st = lds_all + stage * GST;
-      ga.issue(kbeg + t * BK, st);
-      gb.issue(kbeg + t * BK, st + GA::TILE);
-    };
-    Frags<TM, TN, P, NS> f0, f1;
-    if (nk > 0) issue(0, 0);
-    if (nk > 1) {
-      issue(1, 1);
-      __builtin_amdgcn_s_waitcnt(0x0070 | NIW);   // vmcnt(NIW) lgkmcnt(0): tile 0 landed
-    } else {
-      __builtin_amdgcn_s_waitcnt(0x0070);
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    read_frags<BM, BN, TM, TN, P, NS, GA, GB>(lds_all, lds_all + GA::TILE, 0, wm, wn, li, lh, f0);
-    int cs = 0;
-    for (int i = 0; i < nk; ++i) {
-      const float* cur = lds_all + cs * GST;
-      const int ns = cs == 2 ? 0 : cs + 1;
-      const float* nxt = lds_all + ns * GST;
-      const bool more = i + 2 < nk;
-      if (more) issue(i + 2, ns == 2 ? 0 : ns + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      read_frags<BM, BN, TM, TN, P, NS, GA, GB>(cur, cur + GA::TILE, 1, wm, wn, li, lh, f1);
-      mfma_half(f0, acc);
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) __builtin_amdgcn_s_waitcnt(0x0070 | NIW);
-      else __builtin_amdgcn_s_waitcnt(0x0070);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_part<0, 2>(f1, acc);
-      __builtin_amdgcn_sched_barrier(0);
-      read_frags<BM, BN, TM, TN, P, NS, GA, GB>(nxt, nxt + GA::TILE, 0, wm, wn, li, lh, f0);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_part<2, 8 * NS>(f1, acc);
-      cs = ns;
-    }
-    __builtin_amdgcn_s_waitcnt(0x0070);
-    __syncthreads();  // the m-contiguous epilogue reuses the stages
-  }
-  bool halo_done = KS == 4;
+  bool halo_done = false;
   if constexpr (HALO) {
     if (args.B.halo) {
       // Tap-chunked conv1d with the halo B layout (LB::store_h): per channel chunk the x window
@@ -1221,7 +1105,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       halo_done = true;
     }
   }
-  if constexpr (KS == 1 || KS == 3) {
+  if constexpr (KS == 1) {
    if (!halo_done) {
     Frags<TM, TN, P, NS> f0, f1;
     if (nk > 0) {
@@ -1236,35 +1120,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
     }
     __syncthreads();
     if (nk > 0) read_frags<BM, BN, TM, TN, P, NS, LA, LB>(lds, lds + LA::TILE, 0, wm, wn, li, lh, f0);
-    if (KS == 3 && grp == 1 && args.skew) {
-      // Group 1 issues both halves' MFMAs before the (shared) barrier and the next tile's first
-      // fragment reads after it, so between two barriers its staging comes first and its MFMAs
-      // last, while group 0's second-half MFMAs come first: the two groups' MFMA phases are
-      // offset instead of meeting at every barrier.  Hazards as for group 0: the barrier follows
-      // all of this wave's tile stores (lgkmcnt 0), and a stage is overwritten only after the
-      // barrier that follows its last fragment reads.
-      for (int i = 0; i < nk; ++i) {
-        const float* cur = lds + (i & 1) * STAGE;
-        float* nxt = lds + ((i + 1) & 1) * STAGE;
-        if (i + 1 < nk) {
-          la.store(nxt);
-          lb.store(nxt + LA::TILE);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (i + 2 < nk) {
-          la.load(kbeg + (i + 2) * BK);
-          lb.load(kbeg + (i + 2) * BK);
-        }
-        read_frags<BM, BN, TM, TN, P, NS, LA, LB>(cur, cur + LA::TILE, 1, wm, wn, li, lh, f1);
-        mfma_half(f0, acc);
-        mfma_half(f1, acc);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        read_frags<BM, BN, TM, TN, P, NS, LA, LB>(nxt, nxt + LA::TILE, 0, wm, wn, li, lh, f0);
-      }
-    } else
     for (int i = 0; i < nk; ++i) {
       const float* cur = lds + (i & 1) * STAGE;
       float* nxt = lds + ((i + 1) & 1) * STAGE;
@@ -1308,30 +1163,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
       else ablate_touch(f1, acc);
     }
     __syncthreads();  // the m-contiguous epilogue reuses the stages
-    if constexpr (KS == 3) {   // group 1's partial accumulators -> LDS -> group 0
-      if (grp == 1) {
-#pragma unroll
-        for (int t = 0; t < TM; ++t)
-#pragma unroll
-          for (int u = 0; u < TN; ++u)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) lds_all[((t * TN + u) * 16 + q) * 256 + tid] = acc[t][u][q];
-      }
-      __syncthreads();
-      if (grp == 0) {
-#pragma unroll
-        for (int t = 0; t < TM; ++t)
-#pragma unroll
-          for (int u = 0; u < TN; ++u)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) acc[t][u][q] += lds_all[((t * TN + u) * 16 + q) * 256 + tid];
-      }
-      __syncthreads();  // the partials region is free again
-      if (grp == 1) {
-        if (args.mcontig) __syncthreads();  // the epilogue's one barrier
-        return;
-      }
-    }
    }
   } else if constexpr (KS == 2) {
     // The groups take turns staging: group j % 2 loads k-tile j three steps ahead and stores it
@@ -1400,149 +1231,13 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args) {
     }
   }
 
-  // In-launch split-K combine (args.cnt; KS = 1 tiles only, host): every split block stores its
-  // partial accumulators as a slab in fragment order (thread-linear float4s: one coalesced
-  // 4 KB row per instruction) with write-through (sc1) stores, drains them, and takes a ticket
-  // on the tile's arrival counter (one relaxed agent-scope add by one lane after the block's
-  // barrier); the block that draws the last ticket resets the counter for the next launch,
-  // reads the other slabs back with sc1 loads (no L2 write-back fence on the producers, no
-  // stale L1 / other-XCD L2 lines on the reader: the guide's split-K seam) and sums all S
-  // partials in the order s = 0, 1, ..., S - 1 from 0 (its own from registers) -- the reduce
-  // kernel's order, so the sums are bitwise those of splitk_reduce_kernel -- then runs the
-  // normal epilogue.  No block waits for another: the combine costs the last arriver S - 1
-  // slab reads instead of a second launch and its slab round trip.
-  bool slab_out = args.partial != nullptr;
-  if constexpr (KS == 1) {
-    if (args.cnt) {
-      constexpr int NQ4 = TM * TN * 4;   // float4s per thread
-      constexpr int SLAB = BM * BN;      // floats per slab
-      const int S = args.splits;
-      const int tile = (batch * (int)gridDim.y + by) * (int)gridDim.x + bx;
-      float* tb = args.partial + (int64_t)tile * S * SLAB;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          tb, (short)0, __builtin_amdgcn_readfirstlane(S * SLAB * 4), 0x00020000);
-#pragma unroll
-      for (int c = 0; c < NQ4; ++c) {
-        const int t = c / (4 * TN), u = (c / 4) % TN, q = 4 * (c % 4);
-        const float4 v = make_float4(acc[t][u][q], acc[t][u][q + 1], acc[t][u][q + 2], acc[t][u][q + 3]);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, v), rs,
-                                               ((split * NQ4 + c) * 256 + tid) * 16, 0, 16);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
-      __syncthreads();
-      int* flag = reinterpret_cast<int*>(lds_all);
-      if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(args.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == S - 1;
-        if (last) __hip_atomic_store(args.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        flag[0] = last;
-      }
-      __syncthreads();
-      const int last = flag[0];
-      __syncthreads();   // the flag word is read before the epilogue may reuse the stages
-      if (!last) return;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the slab loads below
-      floatx16 own[TM][TN];
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int u = 0; u < TN; ++u) {
-          own[t][u] = acc[t][u];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) acc[t][u][q] = 0.f;
-        }
-      for (int sl = 0; sl < S; ++sl) {
-        if (sl == split) {
-#pragma unroll
-          for (int t = 0; t < TM; ++t)
-#pragma unroll
-            for (int u = 0; u < TN; ++u)
-#pragma unroll
-              for (int q = 0; q < 16; ++q) acc[t][u][q] += own[t][u][q];
-          continue;
-        }
-        float4 v[NQ4];
-#pragma unroll
-        for (int c = 0; c < NQ4; ++c)
-          v[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((sl * NQ4 + c) * 256 + tid) * 16, 0, 16));
-#pragma unroll
-        for (int c = 0; c < NQ4; ++c) {
-          const int t = c / (4 * TN), u = (c / 4) % TN, q = 4 * (c % 4);
-          acc[t][u][q] += v[c].x; acc[t][u][q + 1] += v[c].y; acc[t][u][q + 2] += v[c].z; acc[t][u][q + 3] += v[c].w;
-        }
-      }
-      slab_out = false;
-    }
-  }
-
-  // epilogue
-  if (args.mcontig) {
-    // m-contiguous output (node-feature layouts [.., J*64]): a direct store would put the 32
-    // lanes of each instruction (consecutive n) M floats apart.  Stage the tile as Cs[n][m]
-    // (pitch BM + 1) in the now idle LDS and write it out along m instead.
-    static_assert(BN * (BM + 1) <= 2 * STAGE, "C tile must fit the LDS stages");
-    constexpr int LDC = BM + 1;
-#pragma unroll
-    for (int u = 0; u < TN; ++u)
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-          lds[(wn * (BN / 2) + u * 32 + li) * LDC + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) +
-              4 * lh] = acc[t][u][q];
-    __syncthreads();
-    const int ml = tid % BM;
-    const int m = m0 + ml;
-    if (m < args.M) {
-      if (slab_out) {
-        for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
-          const int n = n0 + nl;
-          if (n >= args.N) break;
-          args.partial[(int64_t)zz * args.M * args.N + (int64_t)n * args.M + m] = lds[nl * LDC + ml];
-        }
-      } else {
-        const EpiRow r = epr[ml];
-        const int64_t am = (int64_t)m * args.E.som;
-        EpiCol c;
-        c.set(args.E, n0 + tid / BM);
-        for (int nl = tid / BM; nl < BN; nl += 256 / BM) {
-          if (n0 + nl >= args.N) break;
-          epi_store_p(args.E, batch, lds[nl * LDC + ml], r, c.addr(args.E) + am);
-          c.advance(args.E, 256 / BM);
-        }
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int u = 0; u < TN; ++u) {
-    const int n = n0 + wn * (BN / 2) + u * 32 + li;
-    if (n >= args.N) continue;
-    if (slab_out) {
-      float* dst = args.partial + (int64_t)zz * args.M * args.N + n;
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int m = m0 + wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-          if (m < args.M) dst[(int64_t)m * args.N] = acc[t][u][q];
-        }
-    } else {
-      const int64_t an = epi_addr(args.E, 0, n);
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int ml = wm * (BM / 2) + t * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-          const int m = m0 + ml;
-          if (m < args.M) epi_store_p(args.E, batch, acc[t][u][q], epr[ml], an + (int64_t)m * args.E.som);
-        }
-    }
-  }
+  const bool slab_out = args.partial != nullptr;
+  static_assert(BN * (BM + 1) <= 2 * STAGE, "C tile must fit the LDS stages");
+  tile_epilogue<BM, BN, TM, TN>(args, acc, lds, epr, slab_out, zz, batch, m0, n0, tid, wm, wn, li, lh);
 }
 
 template <int BM, int BN, int BK, int MA, int MB, int P, int KS = 1>
-__global__ __launch_bounds__(256 * ((KS == 1 || KS == 4) ? 1 : 2)) void gemm_kernel(GemmArgs args) {
+__global__ __launch_bounds__(256 * KS) void gemm_kernel(GemmArgs args) {
   span_begin(args.ts);
   gemm_tile<BM, BN, BK, MA, MB, P, KS>(args);
   span_end(args.ts);
@@ -1555,13 +1250,9 @@ template <int BM, int BN, int BK, int P, int KS = 1>
 void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   dim3 grid((unsigned)cdiv(a.N, BN), (unsigned)cdiv(a.M, BM), (unsigned)(batch * a.splits));
 #define A2M_L(MA_, MB_) \
-  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3((KS == 1 || KS == 4) ? 256 : 512), 0, st, a); return; }
+  if (ma == MA_ && mb == MB_) { hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, MA_, MB_, P, KS>), grid, dim3(256 * KS), 0, st, a); return; }
   // (else-chained, so a wave-group variant instantiates only the mode pairs it serves)
   if constexpr (KS == 2) {  // dense (or channels-last conv, mode 6) operands only (gemm.hip)
-    A2M_L(0, 0) A2M_L(0, 6)
-  } else if constexpr (KS == 3) {  // dense / gathered weights x tap-chunked conv1d operands (gemm.hip)
-    A2M_L(0, 5) A2M_L(0, 3) A2M_L(0, 0) A2M_L(0, 6)
-  } else if constexpr (KS == 4) {  // LDS-DMA staging: dense weights x dense / channels-last rows
     A2M_L(0, 0) A2M_L(0, 6)
   } else {
     A2M_L(0, 0) A2M_L(0, 1) A2M_L(0, 2) A2M_L(0, 3) A2M_L(0, 4)
@@ -1576,9 +1267,6 @@ void launch_tile(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
 
 extern template void launch_tile<64, 64, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 32, 0, 2>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<64, 64, 32, 0, 3>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<64, 64, 32, 0, 4>(const GemmArgs&, int, int, int, hipStream_t);
-extern template void launch_tile<128, 128, 32, 0, 4>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 32, 0>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<64, 64, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);
 extern template void launch_tile<128, 128, 64, 1>(const GemmArgs&, int, int, int, hipStream_t);

@@ -1,0 +1,408 @@
+// Software-pipelined 64x64 fp32 tile of the implicit-GEMM engine (one wave per SIMD).
+//
+// gemm_tile's k loop issues a k-step's operand work (global loads, their LDS stores, address
+// arithmetic, exec-masked bound checks) as one block in front of the step's 16 MFMAs.  A wave
+// issues in order, so with one wave per SIMD -- every launch of at most 256 64x64 tiles, which
+// is most of the decoders' and the encoder's -- that block and the MFMAs add up: without its
+// MFMAs the decoder conv's k loop still took 14.2 of its 24.7 us (profiles/r02_gemm_ablation.txt).
+// A v_mfma_f32_32x32x2_f32 occupies the matrix pipe for 64 cycles, during which the wave can
+// issue other, independent instructions.  This kernel puts the operand work INTO those shadows:
+//   * every operand load is a raw buffer load (out-of-range rows, k and padding taps get an
+//     offset past the buffer and read 0), so the k-step body has no branches;
+//   * a k-step is written as explicit slices -- one MFMA, then one piece of operand work --
+//     separated by sched_barrier, so the scheduler cannot hoist the pieces back into a block.
+// The LDS schedule is gemm_tile's (double-buffered [row][36] stages, one barrier per k-step
+// after the first half's MFMAs, the next tile's first fragments read behind the second half's
+// first MFMAs), so the MFMAs see the same operands in the same order: results are bitwise
+// those of gemm_tile's one-group (KS = 1) tile.
+//
+// B operand modes: 0 dense k-contiguous rows, 3 row-contiguous [B][C][T] / [K][R] operands (the
+// 1x1 projections), 6 channels-last conv rows (Gather::nhwc), 5 the tap-chunked conv1d in the
+// halo layout (Gather::halo: 3 taps, pad 1, clips T >= 16 that tile the 64 rows).  A is always
+// dense rows (mode 0; the packed conv weights).
+#pragma once
+#include "gemm_kernel.h"
+
+namespace a2m {
+
+constexpr uint32_t kPipeOOB = 0x80000000u;   // a buffer offset past every operand: loads read 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pipe_rsrc(const float* base) {
+  // raw buffer, 2 GB range: the host keeps every valid element offset below 2^29 floats
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ float4 pipe_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+
+constexpr int kPipeLDK = 36;   // [row][k] pitch of a 32-k stage (conflict-free ds_read_b128)
+
+// k-contiguous rows (mode 0): a 64-row x 32-k tile, two float4 per thread (rows tid/8 and
+// tid/8 + 32 at k offset 4 (tid % 8)), advanced one k-tile per load
+struct PipeRows {
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t off[2];   // byte offsets of the thread's rows at the next load's k (kPipeOOB: row invalid)
+  int kq, lrow, knext, K;
+  __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
+    rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
+    kq = (tid & 7) * 4;
+    lrow = tid >> 3;
+    K = KK;
+    knext = kbeg;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int row = row0 + lrow + 32 * p;
+      off[p] = row < R ? (uint32_t)(row * g.sr0 + kbeg + kq) * 4u : kPipeOOB;
+    }
+  }
+  __device__ __forceinline__ void load(float4 (&r)[2], int p) {
+    r[p] = pipe_load(rs, knext + kq < K ? off[p] : kPipeOOB);
+    off[p] += 4u * 32;
+    if (p == 1) knext += 32;
+  }
+  __device__ __forceinline__ void store(float* st, const float4 (&r)[2], int p) const {
+    *reinterpret_cast<float4*>(st + (lrow + 32 * p) * kPipeLDK + kq) = r[p];
+  }
+};
+
+// channels-last conv rows (mode 6): a k-tile is 32 channels of one tap (i, j); each row reads its
+// pixel (h + i, w + j) if it lies in the image
+struct PipeNhwc {
+  __amdgpu_buffer_rsrc_t rs;
+  int rbase[2], rh[2], rw[2];
+  bool rv[2];
+  int kq, lrow;
+  int i6, j6, c6;   // tap and channel offset of the next load's k-tile (uniform)
+  int Ci, K2, Lh, Lw;
+  __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
+    (void)KK;
+    rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
+    kq = (tid & 7) * 4;
+    lrow = tid >> 3;
+    Ci = g.nhwc; K2 = g.K2; Lh = g.Lh; Lw = g.Lw;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const RowInfo ri = row_info(g, row0 + lrow + 32 * p, R);
+      rbase[p] = ri.base + (ri.h * g.Lw + ri.w) * Ci + kq;
+      rh[p] = ri.h;
+      rw[p] = ri.w;
+      rv[p] = ri.valid;
+    }
+    const int tap = kbeg / Ci;
+    c6 = kbeg - tap * Ci;
+    i6 = tap / K2;
+    j6 = tap - i6 * K2;
+  }
+  __device__ __forceinline__ void load(float4 (&r)[2], int p) {
+    const int h = rh[p] + i6, w = rw[p] + j6;
+    const bool ok = rv[p] && (unsigned)h < (unsigned)Lh && (unsigned)w < (unsigned)Lw;
+    r[p] = pipe_load(rs, ok ? (uint32_t)(rbase[p] + (i6 * Lw + j6) * Ci + c6) * 4u : kPipeOOB);
+    if (p == 1) {
+      c6 += 32;
+      if (c6 == Ci) {
+        c6 = 0;
+        if (++j6 == K2) { j6 = 0; ++i6; }
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* st, const float4 (&r)[2], int p) const {
+    *reinterpret_cast<float4*>(st + (lrow + 32 * p) * kPipeLDK + kq) = r[p];
+  }
+};
+
+// row-contiguous operand (mode 3, plain case): element (n, k) at b * sr0 + t + k * sk0 with
+// n = b * R2 + t -- a [K][R] matrix (R2 = 1, sr0 = 1) or a [B][C][T] activation read as rows
+// (b, t) and k = c (the 1x1 convs / projections).  Thread (lrow / 4, kq) loads 4 consecutive rows
+// of k = kq and kq + 16 as one float4 each and writes them transposed into the [row][36] stage
+// (gemm_tile's mode-3 map)
+struct PipeRowsT {
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t off;     // byte offset of the thread's 4 rows at the next load's k = kq (kPipeOOB: invalid)
+  int kq, lrow, knext, K, sk0;
+  __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
+    rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
+    lrow = (tid >> 4) * 4;
+    kq = tid & 15;
+    K = KK;
+    knext = kbeg;
+    sk0 = g.sk0;
+    const int n = row0 + lrow;
+    const int b = n / g.R2, t = n - b * g.R2;
+    off = n < R ? (uint32_t)(b * g.sr0 + t + (kbeg + kq) * sk0) * 4u : kPipeOOB;
+  }
+  __device__ __forceinline__ void load(float4 (&r)[2], int p) {
+    r[p] = pipe_load(rs, knext + kq + 16 * p < K ? off + 4u * 16 * sk0 * p : kPipeOOB);
+    if (p == 1) {
+      knext += 32;
+      off += 4u * 32 * sk0;
+    }
+  }
+  __device__ __forceinline__ void store(float* st, const float4 (&r)[2], int p) const {
+    float* q = st + lrow * kPipeLDK + kq + 16 * p;
+    q[0] = r[p].x;
+    q[kPipeLDK] = r[p].y;
+    q[2 * kPipeLDK] = r[p].z;
+    q[3 * kPipeLDK] = r[p].w;
+  }
+};
+
+// tap-chunked conv1d, halo layout (mode 5, Gather::halo): per 32-channel chunk the x window
+// x[b][c][t] of the tile's 64 rows (whole clips of T >= 16) is loaded once -- thread (lrow / 4,
+// kq) reads 4 consecutive t of channels kq and kq + 16 -- and stored once, row n of the tile at
+// halo row (n / T) (T + 2) + 1 + n % T of a chunk-parity stage whose rows before and after each
+// clip are zero; tap j then reads the stage shifted by j - 1 rows
+struct PipeHalo {
+  static constexpr int HR = 64 + 2 * 4;   // halo stage rows (at most four clips)
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t off;      // byte offset of x[b][next chunk * 32 + kq][t] (kPipeOOB: rows invalid)
+  int kq, lrow, ch, Ci, sk0;
+  int h5[4];         // LDS offsets of the thread's 4 rows in a halo stage
+  __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
+    rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
+    lrow = (tid >> 4) * 4;
+    kq = tid & 15;
+    const int T = g.R2;
+    const int n = row0 + lrow;
+    const int b = n / T, tt = n - b * T;
+    Ci = KK / 3;
+    sk0 = g.sk0;
+    ch = (kbeg / 96) * 32 + kq;
+    off = n < R ? (uint32_t)(b * g.sr0 + tt + ch * sk0) * 4u : kPipeOOB;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int nn = lrow + e;
+      h5[e] = ((nn / T) * (T + 2) + 1 + nn % T) * kPipeLDK + kq;
+    }
+  }
+  __device__ __forceinline__ void load(float4 (&r)[2], int p) {
+    r[p] = pipe_load(rs, ch + 16 * p < Ci ? off + 4u * 16 * sk0 * p : kPipeOOB);
+    if (p == 1) {
+      ch += 32;
+      off += 4u * 32 * sk0;
+    }
+  }
+  // half p of the chunk's registers: channel kq + 16 p of the 4 rows
+  __device__ __forceinline__ void store(float* st, const float4 (&r)[2], int p) const {
+    st[h5[0] + 16 * p] = r[p].x;
+    st[h5[1] + 16 * p] = r[p].y;
+    st[h5[2] + 16 * p] = r[p].z;
+    st[h5[3] + 16 * p] = r[p].w;
+  }
+};
+
+__device__ __forceinline__ void pipe_frag(const float* p, float (&f)[8]) {
+  const float4 v0 = *reinterpret_cast<const float4*>(p);
+  const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w;
+  f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
+}
+
+#define A2M_SB() __builtin_amdgcn_sched_barrier(0)
+
+// One k-step.  ca / cb: this lane's fragment rows of tile i (A, B) at half 0 (the half-1
+// fragments are 16 floats further); na / nb: those of tile i + 1.  f0 holds tile i's half-0
+// fragments on entry and tile i + 1's on exit.  work(s), s = 0..7, is the operand work placed
+// behind half-0 MFMA s (stores of tile i + 1 first, then loads of tile i + 2).
+template <class W>
+__device__ __forceinline__ void pipe_step(floatx16& acc, float (&fa0)[8], float (&fb0)[8], const float* ca,
+                                          const float* cb, const float* na, const float* nb, W&& work) {
+  float fa1[8], fb1[8];
+  pipe_frag(ca + 16, fa1);
+  pipe_frag(cb + 16, fb1);
+  A2M_SB();
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0[s], fb0[s], acc, 0, 0, 0);
+    work(s);
+    A2M_SB();
+  }
+  // every wave's stores of tile i + 1 have landed (LDS ops retire in order, so after the
+  // fragment reads issued before them), and no wave reads tile i's half 0 any more
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  A2M_SB();
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[0], fb1[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[1], fb1[1], acc, 0, 0, 0);
+  A2M_SB();
+  pipe_frag(na, fa0);
+  pipe_frag(nb, fb0);
+  A2M_SB();
+#pragma unroll
+  for (int s = 2; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[s], fb1[s], acc, 0, 0, 0);
+  A2M_SB();
+}
+
+template <int MB>
+__global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
+  span_begin(args.ts);
+  constexpr int BM = 64, BN = 64, BK = 32, LDK = kPipeLDK;
+  constexpr bool HALO = MB == 5;
+  constexpr int TA = BM * LDK;
+  constexpr int TB = (HALO ? PipeHalo::HR : BN) * LDK;
+  __shared__ __attribute__((aligned(16))) float lds[2 * TA + 2 * TB];   // A stages, then B stages
+  __shared__ EpiRow epr[BM];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // block -> (n-tile, m-tile, batch * split), XCD-grouped as in gemm_tile
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (args.xcd_group > 0) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int q = total / 8, r = total % 8, x = L % 8;
+    const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
+    bz = t / (gx * gy);
+    const int rem = t - bz * gx * gy;
+    const int gm = args.xcd_group;
+    const int group = rem / (gm * gx);
+    const int first_m = group * gm;
+    const int gsz = min(gy - first_m, gm);
+    const int in = rem - group * gm * gx;
+    by = first_m + in % gsz;
+    bx = in / gsz;
+  }
+  bx = __builtin_amdgcn_readfirstlane(bx);
+  by = __builtin_amdgcn_readfirstlane(by);
+  bz = __builtin_amdgcn_readfirstlane(bz);
+  const int zz = bz;
+  const int batch = zz / args.splits, split = zz % args.splits;
+  const int m0 = by * BM, n0 = bx * BN;
+  const int kbeg = split * args.kchunk;
+  const int kend = min(args.K, kbeg + args.kchunk);
+  const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
+
+  if (!args.partial && tid < BM && m0 + tid < args.M) epr[tid] = epi_row(args.E, m0 + tid + batch * args.E.pstride);
+
+  PipeRows la;
+  la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
+  using LB = typename std::conditional<
+      MB == 5, PipeHalo,
+      typename std::conditional<MB == 6, PipeNhwc, typename std::conditional<MB == 3, PipeRowsT, PipeRows>::type>::type>::type;
+  LB lb;
+  lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
+
+  float* const As = lds;
+  float* const Bs = lds + 2 * TA;
+  const int arow = (wm * 32 + li) * LDK + lh * 8;   // this lane's fragment row offsets
+  const int brow_i = wn * 32 + li;
+  floatx16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  float fa0[8], fb0[8];
+  float4 ra[2], rb[2];
+
+  if constexpr (!HALO) {
+    const int brow = brow_i * LDK + lh * 8;
+    // prologue: tile 0 -> stage 0, tile 1 -> registers
+    la.load(ra, 0); la.load(ra, 1);
+    lb.load(rb, 0); lb.load(rb, 1);
+    la.store(As, ra, 0); la.store(As, ra, 1);
+    lb.store(Bs, rb, 0); lb.store(Bs, rb, 1);
+    la.load(ra, 0); la.load(ra, 1);
+    lb.load(rb, 0); lb.load(rb, 1);
+    __syncthreads();
+    pipe_frag(As + arow, fa0);
+    pipe_frag(Bs + brow, fb0);
+    for (int i = 0; i < nk; ++i) {
+      const int c = (i & 1) * TA, n = TA - c;   // stage offsets of tiles i, i + 1 (TA == TB)
+      float* const nA = As + n;
+      float* const nB = Bs + n;
+      pipe_step(acc, fa0, fb0, As + c + arow, Bs + c + brow, nA + arow, nB + brow, [&](int s) {
+        switch (s) {   // stores of tile i + 1, then loads of tile i + 2
+          case 0: la.store(nA, ra, 0); break;
+          case 1: la.store(nA, ra, 1); break;
+          case 2: lb.store(nB, rb, 0); break;
+          case 3: lb.store(nB, rb, 1); break;
+          case 4: la.load(ra, 0); break;
+          case 5: la.load(ra, 1); break;
+          case 6: lb.load(rb, 0); break;
+          default: lb.load(rb, 1); break;
+        }
+      });
+    }
+  } else {
+    // halo layout: A in k-tile parity stages, B in chunk parity stages (one per 3 k-tiles)
+    const int T = args.B.R2;
+    for (int idx = tid; idx < 2 * (BN / T) * 2 * LDK; idx += 256) {   // zero rows around each clip
+      const int col = idx % LDK, q = idx / LDK;
+      const int which = q & 1, clip = (q >> 1) % (BN / T), stage = (q >> 1) / (BN / T);
+      Bs[stage * TB + (clip * (T + 2) + (which ? T + 1 : 0)) * LDK + col] = 0.f;
+    }
+    const int bsh = 2 * (brow_i / T) + 1;                     // halo rows above this lane's B row
+    const int brow = (brow_i + bsh) * LDK + lh * 8;           // tap 1 (shift 0)
+    la.load(ra, 0); la.load(ra, 1);
+    lb.load(rb, 0); lb.load(rb, 1);
+    la.store(As, ra, 0); la.store(As, ra, 1);
+    lb.store(Bs, rb, 0); lb.store(Bs, rb, 1);
+    la.load(ra, 0); la.load(ra, 1);
+    __syncthreads();
+    pipe_frag(As + arow, fa0);
+    pipe_frag(Bs + brow - LDK, fb0);   // tile 0 = tap 0: shift -1
+    const int nch = nk / 3;
+    for (int cc = 0; cc < nch; ++cc) {
+      const int i0 = 3 * cc;
+      float* const bc = Bs + (cc & 1) * TB;          // this chunk's B stage
+      float* const bn = Bs + ((cc & 1) ^ 1) * TB;    // the next chunk's
+      // tap 0: stores A(i0 + 1), loads A(i0 + 2)
+      {
+        const int c = (i0 & 1) * TA, n = TA - c;
+        float* const nA = As + n;
+        pipe_step(acc, fa0, fb0, As + c + arow, bc + brow - LDK, nA + arow, bc + brow, [&](int s) {
+          switch (s) {
+            case 0: la.store(nA, ra, 0); break;
+            case 1: la.store(nA, ra, 1); break;
+            case 4: la.load(ra, 0); break;
+            case 5: la.load(ra, 1); break;
+            default: break;
+          }
+        });
+      }
+      // tap 1: stores A(i0 + 2), loads A(i0 + 3) and the next chunk's x window
+      {
+        const int c = ((i0 + 1) & 1) * TA, n = TA - c;
+        float* const nA = As + n;
+        pipe_step(acc, fa0, fb0, As + c + arow, bc + brow, nA + arow, bc + brow + LDK, [&](int s) {
+          switch (s) {
+            case 0: la.store(nA, ra, 0); break;
+            case 1: la.store(nA, ra, 1); break;
+            case 4: la.load(ra, 0); break;
+            case 5: la.load(ra, 1); break;
+            case 6: lb.load(rb, 0); break;
+            case 7: lb.load(rb, 1); break;
+            default: break;
+          }
+        });
+      }
+      // tap 2: stores A(i0 + 3) and the next chunk's window, loads A(i0 + 4)
+      {
+        const int c = ((i0 + 2) & 1) * TA, n = TA - c;
+        float* const nA = As + n;
+        pipe_step(acc, fa0, fb0, As + c + arow, bc + brow + LDK, nA + arow, bn + brow - LDK, [&](int s) {
+          switch (s) {
+            case 0: la.store(nA, ra, 0); break;
+            case 1: la.store(nA, ra, 1); break;
+            case 2: lb.store(bn, rb, 0); break;
+            case 3: lb.store(bn, rb, 1); break;
+            case 4: la.load(ra, 0); break;
+            case 5: la.load(ra, 1); break;
+            default: break;
+          }
+        });
+      }
+    }
+  }
+  __syncthreads();   // the m-contiguous epilogue reuses the stages
+  floatx16 accs[1][1];
+  accs[0][0] = acc;
+  tile_epilogue<BM, BN, 1, 1>(args, accs, lds, epr, args.partial != nullptr, zz, batch, m0, n0, tid, wm, wn, li, lh);
+  span_end(args.ts);
+}
+
+#undef A2M_SB
+
+void launch_pipe(const GemmArgs& a, int mb, int batch, hipStream_t st);
+
+}  // namespace a2m

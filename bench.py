@@ -213,8 +213,8 @@ def instep_timing(dev, g, wave, reps=20, warm=None, marks=(0,), gemm=True, enc_l
     finally:
         if hook is not None:
             hook.remove()
-    acc = {'launches': 0, 'flops': 0.0, 'ms_tile': 0.0, 'ms_reduce': 0.0, 'ms_queued': 0.0, 'mel_ms': 0.0,
-           'mel_enc_ms': 0.0}
+    acc = {'launches': 0, 'reduces': 0, 'flops': 0.0, 'ms_tile': 0.0, 'ms_reduce': 0.0, 'ms_queued': 0.0,
+           'mel_ms': 0.0, 'mel_enc_ms': 0.0}
     try:
         graph.replay()
         torch.cuda.synchronize()
@@ -231,6 +231,7 @@ def instep_timing(dev, g, wave, reps=20, warm=None, marks=(0,), gemm=True, enc_l
             if gemm:
                 t.read()
                 acc['launches'] += t.launches
+                acc['reduces'] += t.reduces
                 acc['flops'] += t.flops
                 acc['ms_tile'] += t.ms_tile
                 acc['ms_reduce'] += t.ms_reduce
@@ -246,6 +247,7 @@ def instep_timing(dev, g, wave, reps=20, warm=None, marks=(0,), gemm=True, enc_l
         del graph
     out = {k: v / reps for k, v in acc.items()}
     out['launches'] = int(round(out['launches']))
+    out['reduces'] = int(round(out['reduces']))
     return out
 
 
@@ -494,42 +496,176 @@ def mfma_peak(dtype):
             'bf16x6': BF16_MFMA_PEAK_TFLOPS / 6}[dtype]
 
 
-def roofline_entry(it, gt, peak=None, dispatch_ms=0.0):
-    """`roofline` for the dominant family (the implicit-GEMM engine's gemm_kernel): algorithmic
-    FLOPs per step / summed tile-kernel time per step, both from `instep_timing` (the replayed
-    step graph, branches concurrent).  `serialised_eager` keeps the round-3 basis (one eager step,
-    decoder branches serialised, every launch alone on the chip) for comparison."""
+def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
+    """`roofline` for the dominant family, the implicit-GEMM engine: every tile-kernel launch
+    (gemm_kernel / gemm_pipe_kernel) AND every split-K reduce of one step.  `achieved` =
+    algorithmic FLOPs per step (2*M*N*K summed over the step's engine launches) / the family's
+    summed kernel-trace durations per step (`traced_family`: rocprofv3 --kernel-trace of the
+    replayed bench graph, the figure a kernel-trace breakdown gives); without a trace, the span
+    stamps plus the measured per-launch dispatch overhead.  `frac_execution`: the stamps alone
+    (first block start .. last block end over all XCDs, tile kernels + reduces)."""
     peak = peak or FP32_MFMA_PEAK_TFLOPS
-    n = max(it['launches'], 1)
-    ms_disp = it['ms_tile'] + n * dispatch_ms     # as a kernel trace accounts each launch
-    tf = it['flops'] / (ms_disp * 1e-3) / 1e12
-    tf_exec = it['flops'] / (it['ms_tile'] * 1e-3) / 1e12
-    tf_q = it['flops'] / (it['ms_queued'] * 1e-3) / 1e12 if it['ms_queued'] > 0 else None
-    tf_ser = gt.flops / (gt.ms_tile * 1e-3) / 1e12
-    tr = load_traffic('gemm_kernel') if peak == FP32_MFMA_PEAK_TFLOPS else None
-    return {'bound': 'mfma', 'kernel': 'gemm_kernel (implicit-GEMM engine: every launch of one step)',
+    n_tile = max(it['launches'], 1)
+    n_all = n_tile + it.get('reduces', 0)
+    ms_exec = it['ms_tile'] + it['ms_reduce']
+    ms_disp = ms_exec + n_all * dispatch_ms
+    tf_exec = it['flops'] / (ms_exec * 1e-3) / 1e12
+    tf_disp = it['flops'] / (ms_disp * 1e-3) / 1e12
+    tf_ser = gt.flops / ((gt.ms_tile + gt.ms_reduce) * 1e-3) / 1e12
+    traffic = load_traffic('gemm_kernel') if peak == FP32_MFMA_PEAK_TFLOPS else None
+    if tr:
+        ms_fam = tr['family_us'] / 1e3
+        tf = it['flops'] / (ms_fam * 1e-3) / 1e12
+        basis = (f'kernel trace: rocprofv3 --kernel-trace of the replayed bench graph ({tr["reps"]} replays '
+                 f'after a marker kernel, each followed by a device sync; bench.py --trace-child), the summed '
+                 f'durations of every engine tile kernel and split-K reduce per step; FLOPs = 2*M*N*K over the '
+                 f'step\'s engine launches')
+    else:
+        ms_fam = ms_disp
+        tf = tf_disp
+        basis = ('span stamps (no kernel trace available): first block start .. last block end of every engine '
+                 'tile kernel and split-K reduce in the replayed step graph, plus the measured per-launch '
+                 'dispatch overhead')
+    return {'bound': 'mfma',
+            'kernel': 'implicit-GEMM engine family (gemm_kernel, gemm_pipe_kernel, splitk_reduce*): every launch of one step',
             'achieved': round(tf, 2), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(tf / peak, 4),
-            'traffic': tr['bytes_per_launch'] if tr else None,
-            'traffic_source': tr['source'] if tr else None,
-            'basis': 'in-step: the bench graph re-captured with the engine launches stamping their own '
-                     'spans (first block start .. last block end, GPU wall clock), replayed 20 times '
-                     '(each after three back-to-back replays of the timed graph), plus the measured '
-                     'per-launch dispatch overhead (dispatch_ms_per_launch) that a kernel trace counts '
-                     'in each kernel; cross-check: rocprof kernel trace of replayed steps only '
-                     '(tools/step_pmc.sh; per launch tools/stamp_vs_trace.py, profiles/)',
-            'launches_per_step': it['launches'], 'ms_per_launch': round(ms_disp / n, 4),
-            'dispatch_ms_per_launch': round(dispatch_ms, 4),
+            'traffic': traffic['bytes_per_launch'] if traffic else None,
+            'traffic_source': traffic['source'] if traffic else None,
+            'basis': basis,
+            'family_ms_per_step': round(ms_fam, 4),
+            'launches_per_step': it['launches'], 'reduces_per_step': it.get('reduces', 0),
+            'gflop_per_step': round(it['flops'] / 1e9, 2),
+            'trace_launches_per_step': round(tr['launches'], 1) if tr else None,
+            'trace_reduce_ms_per_step': round(tr['reduce_us'] / 1e3, 4) if tr else None,
             'frac_execution': round(tf_exec / peak, 4),
-            **({'frac_queued': round(tf_q / peak, 4),
-                'frac_queued_basis': 'A2M_GEMM_TIMING_READY=1: each launch from a ready mark (a one-thread '
-                                     'kernel enqueued just before it on its stream) to its last block end'}
-               if tf_q else {}),
-            'gflop_per_launch': round(it['flops'] / n / 1e9, 3),
-            'ms_tile_per_step': round(it['ms_tile'], 4),
-            'splitk_reduce_ms_per_step': round(it['ms_reduce'], 4),
+            'frac_stamps_dispatch': round(tf_disp / peak, 4),
+            'dispatch_ms_per_launch': round(dispatch_ms, 4),
+            'stamps_ms_tile_per_step': round(it['ms_tile'], 4),
+            'stamps_ms_reduce_per_step': round(it['ms_reduce'], 4),
             'serialised_eager': {'achieved': round(tf_ser, 2), 'frac': round(tf_ser / peak, 4),
-                                 'ms_tile_per_step': round(gt.ms_tile, 4)}}
+                                 'ms_per_step': round(gt.ms_tile + gt.ms_reduce, 4)}}
+
+
+GEMM_FAMILY = ('gemm_kernel', 'gemm_pipe_kernel', 'splitk_reduce')   # the engine's kernels
+
+
+def trace_child(args):
+    """`--trace-child R` (run by traced_family under rocprofv3 --kernel-trace): the bench step
+    exactly as the timed run builds it (rank 0's seeds), captured in one graph, one replay, a
+    marker kernel (torch.cuda._sleep), then R replays each followed by a device sync (free-running
+    replays run ~11 % slower under the kernel trace than unprofiled: DESIGN.md 6)."""
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(dev)
+    import a2m
+    a2m.set_gemm_precision(args.dtype)
+    g, wave = build_infer(args.batch, args.frames, 0, dev)
+    with torch.no_grad():
+        graph, _ = capture_step(dev, infer_step(g, wave))
+        graph.replay()
+        torch.cuda.synchronize()
+        torch.cuda._sleep(1000)          # the marker dispatch: everything after it is a replayed step
+        torch.cuda.synchronize()
+        for _ in range(args.trace_child):
+            graph.replay()
+            torch.cuda.synchronize()
+
+
+def _is_marker(name):
+    n = name.lower()
+    return ('sleep' in n or 'spin_kernel' in n) and 'a2m' not in n
+
+
+def traced_family(args, flops_per_step, reps=10, keep_dir=None):
+    """rocprofv3 --kernel-trace of the replayed bench step (a child process running
+    `bench.py --trace-child`): per step, the summed durations of the engine's kernel family --
+    tile kernels AND split-K reduces -- the figure `roofline.frac` is computed from, plus the
+    trace's log-mel start .. encoder end interval and a per-kernel breakdown.  The trace CSV and
+    breakdown are kept in keep_dir (A2M_BENCH_TRACE_DIR) when given.  None if rocprofv3 is
+    unavailable or the child fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which('rocprofv3')
+    if prof is None:
+        return None
+    tmp = tempfile.mkdtemp(prefix='a2m_trace_')
+    cmd = [prof, '--kernel-trace', '--output-format', 'csv', '-d', tmp, '-o', 'run', '--',
+           sys.executable, os.path.abspath(__file__), '--trace-child', str(reps), '--batch', str(args.batch),
+           '--frames', str(args.frames), '--dtype', args.dtype]
+    env = dict(os.environ, TMPDIR=os.environ.get('TMPDIR', '/tmp'))
+    env.pop('WORLD_SIZE', None)
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240, env=env)
+        files = glob.glob(os.path.join(tmp, '**', '*kernel_trace.csv'), recursive=True)
+        if r.returncode != 0 or not files:
+            sys.stderr.write(f'bench.py: kernel-trace child failed (rc {r.returncode})\n' +
+                             r.stdout.decode(errors='replace')[-2000:])
+            return None
+        rows = []
+        for fn in files:
+            with open(fn, newline='') as f:
+                rows.extend(csv.DictReader(f))
+        did = lambda row: int(row.get('Dispatch_Id') or row.get('Correlation_Id'))  # noqa: E731
+        marks = [did(x) for x in rows if _is_marker(x.get('Kernel_Name', ''))]
+        if not marks:
+            return None
+        rows = sorted((x for x in rows if did(x) > max(marks)), key=lambda x: int(x['Start_Timestamp']))
+        dur = lambda x: (int(x['End_Timestamp']) - int(x['Start_Timestamp'])) / 1e3  # noqa: E731  us
+        name = lambda x: x['Kernel_Name'].split('(')[0].replace('void ', '')  # noqa: E731
+        fam = [x for x in rows if any(k in name(x) for k in GEMM_FAMILY)]
+        fam_us = sum(dur(x) for x in fam) / reps
+        red_us = sum(dur(x) for x in fam if 'splitk_reduce' in name(x)) / reps
+        # per step: the log-mel's start .. the end of the encoder's last engine launch (its fused
+        # resample reduce) -- north_star's mel + encoder path in the step
+        starts = [i for i, x in enumerate(rows) if 'logmel' in name(x)]
+        mel_enc = []
+        for i in starts:
+            j = next((k for k in range(i, len(rows)) if 'splitk_reduce_interp' in name(rows[k])), None)
+            if j is not None:
+                mel_enc.append((int(rows[j]['End_Timestamp']) - int(rows[i]['Start_Timestamp'])) / 1e3)
+        agg = {}
+        for x in rows:
+            a = agg.setdefault(name(x)[:90], [0, 0.0])
+            a[0] += 1
+            a[1] += dur(x)
+        tot = sum(v[1] for v in agg.values()) / reps
+        lines = [f'{len(rows)} dispatches after the marker = {reps} replayed steps (device sync after each); '
+                 f'kernel-time sum {tot:.1f} us/step',
+                 f'engine family (gemm_kernel + gemm_pipe_kernel + splitk_reduce*): {len(fam) / reps:.1f} launches/step, '
+                 f'{fam_us:.1f} us/step ({red_us:.1f} us of split-K reduces)',
+                 f'engine roofline: {flops_per_step / 1e9:.1f} GFLOP / {fam_us:.1f} us = '
+                 f'{flops_per_step / (fam_us * 1e-6) / 1e12:.1f} TF']
+        for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+            lines.append(f'{t / reps:9.1f} us/step {c / reps:6.1f} calls/step {t / c:8.1f} us/call  {k}')
+        if keep_dir:
+            os.makedirs(keep_dir, exist_ok=True)
+            shutil.copy(files[0], os.path.join(keep_dir, 'step_trace_replayed_kernel_trace.csv'))
+            with open(os.path.join(keep_dir, 'step_breakdown.txt'), 'w') as f:
+                f.write('\n'.join(lines) + '\n')
+        return {'family_us': fam_us, 'reduce_us': red_us, 'launches': len(fam) / reps, 'reps': reps,
+                'mel_enc_us': sorted(mel_enc)[len(mel_enc) // 2] if mel_enc else None}
+    except (OSError, subprocess.SubprocessError, ValueError, KeyError) as e:
+        sys.stderr.write(f'bench.py: kernel-trace child failed: {e}\n')
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def build_infer(B, T, rank, dev):
+    """The bench's generator (random init, attention gammas 0.3, eval) and synthetic waves."""
+    from a2m.real_motion_model import SelfAttention_G
+    n = (T - 1) * HOP + WIN
+    torch.manual_seed(1234 + rank)
+    g = SelfAttention_G(time_steps=T, p=0.2)
+    for m in g.modules():
+        if hasattr(m, 'gamma'):
+            torch.nn.init.constant_(m.gamma, 0.3)
+    g = g.to(dev).eval()
+    return g, synth_wave(B, n, seed=rank, device=dev)
+
 
 
 def spawn_ranks(n):
@@ -567,7 +703,12 @@ def main():
                     help='train mode: gradient all-reduce bucket size (MB)')
     ap.add_argument('--dtype', choices=('fp32', 'bf16', 'bf16x6'), default='fp32',
                     help='GEMM operand precision (bf16: configs[4], fp32 accumulation/storage)')
+    ap.add_argument('--trace-child', type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument('--no-trace', action='store_true',
+                    help='skip the kernel-trace pass (roofline from the span stamps only)')
     args = ap.parse_args()
+    if args.trace_child:
+        return trace_child(args)
     if args.steps is None:
         args.steps = 200 if args.mode == 'infer' else 20
     if args.warmup is None:
@@ -600,17 +741,8 @@ def main():
     if args.mode == 'train':
         return run_train(args, world, rank, dev)
 
-    from a2m.real_motion_model import SelfAttention_G
-
     B, T = args.batch, args.frames
-    n = (T - 1) * HOP + WIN
-    torch.manual_seed(1234 + rank)
-    g = SelfAttention_G(time_steps=T, p=0.2)
-    for m in g.modules():
-        if hasattr(m, 'gamma'):
-            torch.nn.init.constant_(m.gamma, 0.3)
-    g = g.to(dev).eval()
-    wave = synth_wave(B, n, seed=rank, device=dev)
+    g, wave = build_infer(B, T, rank, dev)
 
     step = infer_step(g, wave)
     with torch.no_grad():
@@ -662,6 +794,12 @@ def main():
         mel_enc['instep_mel_ms'] = round(it['mel_ms'], 4)
         mel_enc['instep_mel_encoder_ms'] = round(it['mel_enc_ms'], 4)
         mel_enc['path_frac_instep'] = round(mel_enc['path_roofline_ms'] / it['mel_enc_ms'], 4)
+        tr = None
+        if world == 1 and not args.no_trace and graph is not None and not args.branch_graphs:
+            tr = traced_family(args, it['flops'], keep_dir=os.environ.get('A2M_BENCH_TRACE_DIR'))
+        if tr and tr['mel_enc_us']:
+            mel_enc['instep_mel_encoder_ms_trace'] = round(tr['mel_enc_us'] / 1e3, 4)
+            mel_enc['path_frac_instep_trace'] = round(mel_enc['path_roofline_ms'] / (tr['mel_enc_us'] / 1e3), 4)
     path_tf = g_forward_flops(B, T) / (ms_step * 1e-3) / 1e12
     peak = mfma_peak(args.dtype)
     if args.dtype == 'bf16':
@@ -681,7 +819,7 @@ def main():
         'data': 'synthetic 16 kHz speech-like audio, random-init weights',
         'config': {'workload': workload, 'global_batch': B * world, 'seq_len': T,
                    'parallelism': f'replicas{world}', 'hip_graph': 'none' if graph is None else ('per-branch graphs, two streams' if args.branch_graphs else 'one graph')},
-        'roofline': roofline_entry(it, gt, peak, disp_ms),
+        'roofline': roofline_entry(it, gt, peak, disp_ms, tr),
         'mel_roofline': {'bound': 'hbm', 'achieved': round(mel_bytes / (mel_ms * 1e-3) / 1e9, 1),
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(mel_bytes / (mel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -504,8 +504,9 @@ int a2m_window_gather_f32(const float* data, int64_t length, int32_t C, const in
                           const float* std_, float* out, void* stream);
 
 /* Measurement hook (bench.py): while enabled, every launch of the implicit-GEMM engine (up to
- * 4096 per window) carries a record of span stamps that its tile kernel and split-K reduce write
- * themselves (earliest block start, latest wave end, GPU wall clock), eagerly or inside a graph
+ * 1024 per window; more make _read fail) carries a record of span stamps that its tile kernel and
+ * split-K reduce write themselves (earliest block start, latest wave end on the GPU's constant-rate
+ * wall clock, which all XCDs share; a span is last end - first start over all XCDs), eagerly or inside a graph
  * captured while enabled.  _read synchronises the device and returns the launch count, the
  * launches' algorithmic FLOPs (2*M*N*K*batch), the summed tile-kernel spans and the summed
  * split-K reduce spans (ms) of the latest execution, then re-arms the stamps (so it can follow

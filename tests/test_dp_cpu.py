@@ -230,9 +230,11 @@ def test_syncbn_plumbing_two_ranks():
         assert t == [[1.5 + 2.5, 2.0]]                          # SUM over the ranks, float64
 
 
-def _mismatch_worker(rank, world, port, q):
-    """Rank 1 sends a gradient through a parameter outside the learnt set on the second step:
-    both ranks must raise together (no rank left waiting in a bucket all-reduce)."""
+def _mismatch_worker(rank, world, port, q, bad_step=1, check_every=None, flush=False):
+    """Rank 1 sends a gradient through a parameter outside the learnt set on step `bad_step`
+    (0-based iteration): both ranks must raise together (no rank left waiting in a bucket
+    all-reduce) -- at once on the synchronously checked first steps, at the next periodic check
+    (GradReducer.CHECK_EVERY) or at GANTrainer.flush() after them."""
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
@@ -256,31 +258,43 @@ def _mismatch_worker(rank, world, port, q):
         torch.manual_seed(11)
         g = BranchG()
         tr = GANTrainer(g, TinyD(), lr=1e-2, fixed_labels=(0.93, 0.07), bucket_mb=0.009)
+        if check_every:
+            tr.red_G.CHECK_EVERY = tr.red_D.CHECK_EVERY = check_every
         audio, pose = _data()
-        tr.iteration(audio[rank::world], pose[rank::world], epoch=0, g_freq=1, d_freq=1)
-        g.use_extra = rank == 1
+        at = None
         try:
-            tr.iteration(audio[rank::world], pose[rank::world], epoch=1, g_freq=1, d_freq=1)
+            for it in range(bad_step + 4):
+                g.use_extra = rank == 1 and it == bad_step
+                at = it
+                tr.iteration(audio[rank::world], pose[rank::world], epoch=it, g_freq=1, d_freq=1)
+            at = 'flush'
+            if flush:
+                tr.flush()
             q.put((rank, 'no error'))
         except RuntimeError as e:
-            q.put((rank, 'raised: ' + str(e)[:60]))
+            q.put((rank, f'raised at {at}: ' + str(e)[:60]))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_grad_reducer_mismatch_raises_on_every_rank():
+@pytest.mark.parametrize('bad_step,check_every,flush,where', [
+    (1, None, False, 1),          # a synchronously checked step: raises in that step
+    (3, 2, False, 4),             # G's 4th finish() is a check step (4 % 2): read at the next finish()
+    (3, 50, True, 'flush')])      # no check before the end: GANTrainer.flush() raises
+def test_grad_reducer_mismatch_raises_on_every_rank(bad_step, check_every, flush, where):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_mismatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_mismatch_worker, args=(r, 2, port, q, bad_step, check_every, flush))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(30)
         assert p.exitcode == 0
-    assert all(v.startswith('raised: GradReducer') for v in res.values()), res
+    assert all(v.startswith(f'raised at {where}: GradReducer') for v in res.values()), res
 
 
 def _seed_worker(rank, world, port, q):
