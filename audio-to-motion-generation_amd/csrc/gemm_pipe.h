@@ -23,6 +23,12 @@
 #pragma once
 #include "gemm_kernel.h"
 
+// Diagnostic builds only (never the shipped library): A2M_PIPE_ABL = 1 drops the k loop's global
+// loads, 2 its barriers, 3 its MFMAs (results wrong; what remains times the rest)
+#ifndef A2M_PIPE_ABL
+#define A2M_PIPE_ABL 0
+#endif
+
 namespace a2m {
 
 constexpr uint32_t kPipeOOB = 0x80000000u;   // a buffer offset past every operand: loads read 0
@@ -33,6 +39,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pipe_rsrc(const float* base) {
 }
 __device__ __forceinline__ float4 pipe_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+__device__ __forceinline__ void pipe_mfma(floatx16& acc, float a, float b) {
+  if (A2M_PIPE_ABL == 3) acc[0] += a * b;
+  else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
 }
 
 constexpr int kPipeLDK = 36;   // [row][k] pitch of a 32-k stage (conflict-free ds_read_b128)
@@ -212,23 +222,23 @@ __device__ __forceinline__ void pipe_step(floatx16& acc, float (&fa0)[8], float 
   A2M_SB();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0[s], fb0[s], acc, 0, 0, 0);
-    work(s);
+    pipe_mfma(acc, fa0[s], fb0[s]);
+    if (A2M_PIPE_ABL != 1 || s < 4) work(s);
     A2M_SB();
   }
   // every wave's stores of tile i + 1 have landed (LDS ops retire in order, so after the
   // fragment reads issued before them), and no wave reads tile i's half 0 any more
   __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-  __builtin_amdgcn_s_barrier();
+  if (A2M_PIPE_ABL != 2) __builtin_amdgcn_s_barrier();
   A2M_SB();
-  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[0], fb1[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[1], fb1[1], acc, 0, 0, 0);
+  pipe_mfma(acc, fa1[0], fb1[0]);
+  pipe_mfma(acc, fa1[1], fb1[1]);
   A2M_SB();
   pipe_frag(na, fa0);
   pipe_frag(nb, fb0);
   A2M_SB();
 #pragma unroll
-  for (int s = 2; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[s], fb1[s], acc, 0, 0, 0);
+  for (int s = 2; s < 8; ++s) pipe_mfma(acc, fa1[s], fb1[s]);
   A2M_SB();
 }
 
@@ -274,8 +284,6 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   const int kend = min(args.K, kbeg + args.kchunk);
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
 
-  if (!args.partial && tid < BM && m0 + tid < args.M) epr[tid] = epi_row(args.E, m0 + tid + batch * args.E.pstride);
-
   PipeRows la;
   la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
   using LB = typename std::conditional<
@@ -292,39 +300,62 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.f;
   float fa0[8], fb0[8];
-  float4 ra[2], rb[2];
+  // Operand registers, two sets: tile t is loaded two k-steps before it is stored (set t & 1;
+  // the store of tile i + 1 at step i frees the set that the load of tile i + 3 then takes), so
+  // every global load has about two k-steps (~2,000 cycles) to land.  The loop is unrolled by
+  // two (by two channel chunks in the halo layout) so that the set indices are static.
+  float4 ra[2][2], rb[2][2];
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  // the block's epilogue constants: their loads are issued after tile 0's, so both round trips
+  // overlap (visible after the prologue's barrier)
+  auto epi_consts = [&]() {
+    if (!args.partial && tid < BM && m0 + tid < args.M) epr[tid] = epi_row(args.E, m0 + tid + batch * args.E.pstride);
+  };
 
   if constexpr (!HALO) {
     const int brow = brow_i * LDK + lh * 8;
-    // prologue: tile 0 -> stage 0, tile 1 -> registers
-    la.load(ra, 0); la.load(ra, 1);
-    lb.load(rb, 0); lb.load(rb, 1);
-    la.store(As, ra, 0); la.store(As, ra, 1);
-    lb.store(Bs, rb, 0); lb.store(Bs, rb, 1);
-    la.load(ra, 0); la.load(ra, 1);
-    lb.load(rb, 0); lb.load(rb, 1);
+    la.load(ra[0], 0); la.load(ra[0], 1);
+    lb.load(rb[0], 0); lb.load(rb[0], 1);
+    epi_consts();
+    la.load(ra[1], 0); la.load(ra[1], 1);
+    lb.load(rb[1], 0); lb.load(rb[1], 1);
+    la.store(As, ra[0], 0); la.store(As, ra[0], 1);
+    lb.store(Bs, rb[0], 0); lb.store(Bs, rb[0], 1);
+    la.load(ra[0], 0); la.load(ra[0], 1);
+    lb.load(rb[0], 0); lb.load(rb[0], 1);
     __syncthreads();
     pipe_frag(As + arow, fa0);
     pipe_frag(Bs + brow, fb0);
-    for (int i = 0; i < nk; ++i) {
+    // step i (parity P = i & 1): stores of tile i + 1 from set (P + 1) & 1, then the loads of
+    // tile i + 3 into that set
+    auto step = [&](auto par, int i) {
+      constexpr int Q = (decltype(par)::value + 1) & 1;
       const int c = (i & 1) * TA, n = TA - c;   // stage offsets of tiles i, i + 1 (TA == TB)
       float* const nA = As + n;
       float* const nB = Bs + n;
       pipe_step(acc, fa0, fb0, As + c + arow, Bs + c + brow, nA + arow, nB + brow, [&](int s) {
-        switch (s) {   // stores of tile i + 1, then loads of tile i + 2
-          case 0: la.store(nA, ra, 0); break;
-          case 1: la.store(nA, ra, 1); break;
-          case 2: lb.store(nB, rb, 0); break;
-          case 3: lb.store(nB, rb, 1); break;
-          case 4: la.load(ra, 0); break;
-          case 5: la.load(ra, 1); break;
-          case 6: lb.load(rb, 0); break;
-          default: lb.load(rb, 1); break;
+        switch (s) {
+          case 0: la.store(nA, ra[Q], 0); break;
+          case 1: la.store(nA, ra[Q], 1); break;
+          case 2: lb.store(nB, rb[Q], 0); break;
+          case 3: lb.store(nB, rb[Q], 1); break;
+          case 4: la.load(ra[Q], 0); break;
+          case 5: la.load(ra[Q], 1); break;
+          case 6: lb.load(rb[Q], 0); break;
+          default: lb.load(rb[Q], 1); break;
         }
       });
+    };
+    int i = 0;
+    for (; i + 1 < nk; i += 2) {
+      step(P0(), i);
+      step(P1(), i + 1);
     }
+    if (i < nk) step(P0(), i);
   } else {
-    // halo layout: A in k-tile parity stages, B in chunk parity stages (one per 3 k-tiles)
+    // halo layout: A in k-tile parity stages, B in chunk parity stages (one per 3 k-tiles); the
+    // next chunk's x window is loaded at the chunk's tap 0 and stored at its tap 2
     const int T = args.B.R2;
     for (int idx = tid; idx < 2 * (BN / T) * 2 * LDK; idx += 256) {   // zero rows around each clip
       const int col = idx % LDK, q = idx / LDK;
@@ -333,66 +364,76 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
     }
     const int bsh = 2 * (brow_i / T) + 1;                     // halo rows above this lane's B row
     const int brow = (brow_i + bsh) * LDK + lh * 8;           // tap 1 (shift 0)
-    la.load(ra, 0); la.load(ra, 1);
-    lb.load(rb, 0); lb.load(rb, 1);
-    la.store(As, ra, 0); la.store(As, ra, 1);
-    lb.store(Bs, rb, 0); lb.store(Bs, rb, 1);
-    la.load(ra, 0); la.load(ra, 1);
+    float4 rx[2];                                             // a chunk's x window
+    la.load(ra[0], 0); la.load(ra[0], 1);
+    lb.load(rx, 0); lb.load(rx, 1);
+    epi_consts();
+    la.load(ra[1], 0); la.load(ra[1], 1);
+    la.store(As, ra[0], 0); la.store(As, ra[0], 1);
+    lb.store(Bs, rx, 0); lb.store(Bs, rx, 1);
+    la.load(ra[0], 0); la.load(ra[0], 1);
     __syncthreads();
     pipe_frag(As + arow, fa0);
     pipe_frag(Bs + brow - LDK, fb0);   // tile 0 = tap 0: shift -1
     const int nch = nk / 3;
-    for (int cc = 0; cc < nch; ++cc) {
+    // chunk cc (parity P = cc & 1, so tile 3 cc + j has parity (P + j) & 1): tap j stores
+    // A(3 cc + j + 1) from set (P + j + 1) & 1 and loads A(3 cc + j + 3) into it
+    auto chunk = [&](auto par, int cc) {
+      constexpr int P = decltype(par)::value;
+      constexpr int Q0 = (P + 1) & 1, Q1 = P, Q2 = (P + 1) & 1;
       const int i0 = 3 * cc;
       float* const bc = Bs + (cc & 1) * TB;          // this chunk's B stage
       float* const bn = Bs + ((cc & 1) ^ 1) * TB;    // the next chunk's
-      // tap 0: stores A(i0 + 1), loads A(i0 + 2)
-      {
+      {   // tap 0 (+ the next chunk's x window loads)
         const int c = (i0 & 1) * TA, n = TA - c;
         float* const nA = As + n;
         pipe_step(acc, fa0, fb0, As + c + arow, bc + brow - LDK, nA + arow, bc + brow, [&](int s) {
           switch (s) {
-            case 0: la.store(nA, ra, 0); break;
-            case 1: la.store(nA, ra, 1); break;
-            case 4: la.load(ra, 0); break;
-            case 5: la.load(ra, 1); break;
+            case 0: la.store(nA, ra[Q0], 0); break;
+            case 1: la.store(nA, ra[Q0], 1); break;
+            case 4: la.load(ra[Q0], 0); break;
+            case 5: la.load(ra[Q0], 1); break;
+            case 6: lb.load(rx, 0); break;
+            case 7: lb.load(rx, 1); break;
             default: break;
           }
         });
       }
-      // tap 1: stores A(i0 + 2), loads A(i0 + 3) and the next chunk's x window
-      {
+      {   // tap 1
         const int c = ((i0 + 1) & 1) * TA, n = TA - c;
         float* const nA = As + n;
         pipe_step(acc, fa0, fb0, As + c + arow, bc + brow, nA + arow, bc + brow + LDK, [&](int s) {
           switch (s) {
-            case 0: la.store(nA, ra, 0); break;
-            case 1: la.store(nA, ra, 1); break;
-            case 4: la.load(ra, 0); break;
-            case 5: la.load(ra, 1); break;
-            case 6: lb.load(rb, 0); break;
-            case 7: lb.load(rb, 1); break;
+            case 0: la.store(nA, ra[Q1], 0); break;
+            case 1: la.store(nA, ra[Q1], 1); break;
+            case 4: la.load(ra[Q1], 0); break;
+            case 5: la.load(ra[Q1], 1); break;
             default: break;
           }
         });
       }
-      // tap 2: stores A(i0 + 3) and the next chunk's window, loads A(i0 + 4)
-      {
+      {   // tap 2 (+ the next chunk's x window stores)
         const int c = ((i0 + 2) & 1) * TA, n = TA - c;
         float* const nA = As + n;
         pipe_step(acc, fa0, fb0, As + c + arow, bc + brow + LDK, nA + arow, bn + brow - LDK, [&](int s) {
           switch (s) {
-            case 0: la.store(nA, ra, 0); break;
-            case 1: la.store(nA, ra, 1); break;
-            case 2: lb.store(bn, rb, 0); break;
-            case 3: lb.store(bn, rb, 1); break;
-            case 4: la.load(ra, 0); break;
-            case 5: la.load(ra, 1); break;
+            case 0: la.store(nA, ra[Q2], 0); break;
+            case 1: la.store(nA, ra[Q2], 1); break;
+            case 2: lb.store(bn, rx, 0); break;
+            case 3: lb.store(bn, rx, 1); break;
+            case 4: la.load(ra[Q2], 0); break;
+            case 5: la.load(ra[Q2], 1); break;
             default: break;
           }
         });
       }
+    };
+    int cc = 0;
+    for (; cc + 1 < nch; cc += 2) {
+      chunk(P0(), cc);
+      chunk(P1(), cc + 1);
     }
+    if (cc < nch) chunk(P0(), cc);
   }
   __syncthreads();   // the m-contiguous epilogue reuses the stages
   floatx16 accs[1][1];
