@@ -7,11 +7,9 @@
 // runs on the LDS tile, and the PV product + epilogue follow without leaving the workgroup.
 // The normalised attention matrix is also written out when the backward pass needs it.
 // Replaces three launches (score GEMM, softmax, PV GEMM) of the general path.
-#include "a2m_internal.h"
+#include "gemm_pipe.h"
 
 namespace a2m {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int AT = 64;        // max sequence length / tile edge
 constexpr int AP = AT + 4;    // LDS pitch: conflict-free ds_read_b128 rows
@@ -202,90 +200,76 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   const int wt = (wave & 3) >> 1, wc = wave & 1;
   const float* xb = x + (int64_t)b * x_bs;
 
-  // staging maps.  x tile [t][c] from x[c][t]: thread -> (c = e % 32, t quad = e / 32), one
+  // Staging maps.  x tile [t][c] from x[c][t]: thread -> (c = tid % 32, t quad = tid / 32), one
   // float4 per thread, transposed writes conflict-free (32 lanes = 32 consecutive c).
   // w tile [col][c]: stacked rows Q 0..Cq-1 -> cols 0.., K Cq.. -> 32.., V 2Cq + c0.. -> 64..;
-  // two float4 per thread along c.
-  int wrow[2];
+  // two float4 per thread along c.  All loads are raw buffer loads (rows past Cq / t past T read
+  // 0), so the k-step below is branch-free and its operand work is placed between the MFMAs
+  // (pipe_step, gemm_pipe.h: tile i + 1 stored and tile i + 3 loaded behind the first half's
+  // MFMAs, one barrier, the next fragments read behind the second half's first MFMAs).
+  const __amdgpu_buffer_rsrc_t xrs = pipe_rsrc(xb), wrs = pipe_rsrc(wqkv);
+  const int xc = tid & 31, xq = tid >> 5;
+  uint32_t xoff = 4 * xq < T ? (uint32_t)(xc * T + 4 * xq) * 4u : kPipeOOB;   // advanced 32 channels a tile
+  uint32_t woff[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int col = (tid + u * 512) >> 3;
-    wrow[u] = col < 32 ? (col < Cq ? col : -1)
-                       : col < 64 ? (col - 32 < Cq ? Cq + col - 32 : -1) : 2 * Cq + c0 + col - 64;
+    const int wrow = col < 32 ? (col < Cq ? col : -1)
+                              : col < 64 ? (col - 32 < Cq ? Cq + col - 32 : -1) : 2 * Cq + c0 + col - 64;
+    woff[u] = wrow >= 0 ? (uint32_t)(wrow * C + ((tid + u * 512) & 7) * 4) * 4u : kPipeOOB;
   }
-  // two register sets, so a tile's global loads are issued two k-steps before its LDS store
-  // (one step of MFMAs, ~1k cycles, does not cover an L2 / HBM round trip)
-  auto load_tile = [&](int kt, float4& xr, float4 (&wr)[2]) {
-    const int cb = kt * FK;
-    {
-      const int c = tid & 31, tq = tid >> 5;
-      xr = 4 * tq < T ? *reinterpret_cast<const float4*>(xb + (int64_t)(cb + c) * T + 4 * tq)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int kq = ((tid + u * 512) & 7) * 4;
-      wr[u] = wrow[u] >= 0 ? *reinterpret_cast<const float4*>(wqkv + (int64_t)wrow[u] * C + cb + kq)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+  struct Regs { float4 x, w[2]; };
+  Regs rg[2];
+  // the straight-line prefetch also issues the loads of the (unused) tiles past the last one:
+  // those must read 0 (kPipeOOB), not channels past C -- for the last clip and the last weight
+  // rows that would be memory past the tensors
+  int cnext = 0;   // first channel of the next tile to load
+  auto load_piece = [&](Regs& r, int piece) {   // piece 0: x, 1-2: w rows
+    const bool ok = cnext < C;
+    if (piece == 0) { r.x = pipe_load(xrs, ok ? xoff : kPipeOOB); xoff += 4u * FK * T; }
+    else { r.w[piece - 1] = pipe_load(wrs, ok ? woff[piece - 1] : kPipeOOB); woff[piece - 1] += 4u * FK; }
+    if (piece == 2) cnext += FK;
   };
-  auto store_tile = [&](float* st, const float4& xr, const float4 (&wr)[2]) {
-    float* xs = st;
-    float* ws = st + XT;
-    {
-      const int c = tid & 31, t = 4 * (tid >> 5);
-      xs[(t + 0) * FKP + c] = xr.x;
-      xs[(t + 1) * FKP + c] = xr.y;
-      xs[(t + 2) * FKP + c] = xr.z;
-      xs[(t + 3) * FKP + c] = xr.w;
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + u * 512;
-      *reinterpret_cast<float4*>(ws + (e >> 3) * FKP + (e & 7) * 4) = wr[u];
+  auto store_piece = [&](float* st, const Regs& r, int piece) {   // 0-1: x halves, 2-3: w rows
+    if (piece < 2) {
+      float* xs = st + (4 * xq + 2 * piece) * FKP + xc;
+      xs[0] = piece == 0 ? r.x.x : r.x.z;
+      xs[FKP] = piece == 0 ? r.x.y : r.x.w;
+    } else {
+      const int e = tid + (piece - 2) * 512;
+      *reinterpret_cast<float4*>(st + XT + (e >> 3) * FKP + (e & 7) * 4) = r.w[piece - 2];
     }
   };
 
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  auto mma_tile = [&](const float* cur) {
-    float af[2][8], bf[2][8];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {  // both halves' fragments first
-      const float* ap = cur + (pt * 32 + li) * FKP + half * 16 + lh * 8;
-      const float* bp = cur + XT + (pc * 32 + li) * FKP + half * 16 + lh * 8;
-      const float4 a0 = *reinterpret_cast<const float4*>(ap), a1 = *reinterpret_cast<const float4*>(ap + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(bp), b1 = *reinterpret_cast<const float4*>(bp + 4);
-      af[half][0] = a0.x; af[half][1] = a0.y; af[half][2] = a0.z; af[half][3] = a0.w;
-      af[half][4] = a1.x; af[half][5] = a1.y; af[half][6] = a1.z; af[half][7] = a1.w;
-      bf[half][0] = b0.x; bf[half][1] = b0.y; bf[half][2] = b0.z; bf[half][3] = b0.w;
-      bf[half][4] = b1.x; bf[half][5] = b1.y; bf[half][6] = b1.z; bf[half][7] = b1.w;
-    }
-#pragma unroll
-    for (int half = 0; half < 2; ++half)
-#pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[half][s2], bf[half][s2], acc, 0, 0, 0);
-  };
   const int nk = C / FK;   // even (C in {128, 256})
-  float4 xa, wa[2], xb2, wb2[2];
-  load_tile(0, xa, wa);
-  store_tile(lds, xa, wa);
-  if (nk > 1) load_tile(1, xa, wa);          // set A: tile 1
+  const int arow = (pt * 32 + li) * FKP + lh * 8, brow = XT + (pc * 32 + li) * FKP + lh * 8;
+  float fa0[8], fb0[8];
+  for (int pc2 = 0; pc2 < 3; ++pc2) load_piece(rg[0], pc2);   // tile 0
+  for (int pc2 = 0; pc2 < 3; ++pc2) load_piece(rg[1], pc2);   // tile 1
+  for (int pc2 = 0; pc2 < 4; ++pc2) store_piece(lds, rg[0], pc2);
+  for (int pc2 = 0; pc2 < 3; ++pc2) load_piece(rg[0], pc2);   // tile 2
   __syncthreads();
+  pipe_frag(lds + arow, fa0);
+  pipe_frag(lds + brow, fb0);
+  // step i: tile i in stage i & 1; stores tile i + 1 from set (i + 1) & 1, then loads tile
+  // i + 3 into that set (tiles past nk read channels past C: harmless, never stored as used)
+  auto step = [&](auto par, int i) {
+    constexpr int Q = (decltype(par)::value + 1) & 1;
+    float* const cur = lds + (i & 1) * STG;
+    float* const nxt = lds + ((i + 1) & 1) * STG;
+    pipe_step(acc, fa0, fb0, cur + arow, cur + brow, nxt + arow, nxt + brow, [&](int s) {
+      if (s < 4) store_piece(nxt, rg[Q], s);
+      else if (s < 7) load_piece(rg[Q], s - 4);
+    });
+  };
   for (int kt = 0; kt < nk; kt += 2) {
-    // step kt (stage 0): tile kt+1 waits in set A, tile kt+2 loads into set B
-    if (kt + 2 < nk) load_tile(kt + 2, xb2, wb2);
-    mma_tile(lds);
-    if (kt + 1 < nk) store_tile(lds + STG, xa, wa);
-    __syncthreads();
-    if (kt + 1 >= nk) break;
-    // step kt+1 (stage 1): tile kt+2 waits in set B, tile kt+3 loads into set A
-    if (kt + 3 < nk) load_tile(kt + 3, xa, wa);
-    mma_tile(lds + STG);
-    if (kt + 2 < nk) store_tile(lds, xb2, wb2);
-    __syncthreads();
+    step(std::integral_constant<int, 0>(), kt);
+    step(std::integral_constant<int, 1>(), kt + 1);
   }
+  __syncthreads();   // the stages are overlaid by Q^T / K^T / V below
 
   // projection outputs (+ bias) to LDS: acc[r] = P[t][col], t = 32 pt + (r&3) + 8 (r>>2) + 4 lh,
   // col = 32 pc + li.  Q^T / K^T rows t (zero past Cq), V chunk rows c (zero past T)
