@@ -598,14 +598,16 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   bool pipe_ext = below((int64_t)(M - 1) * A.sr0 + K);
   if (mb == 0) pipe_ext = pipe_ext && below((int64_t)(N - 1) * B.sr0 + K);
   else if (mb == 6) pipe_ext = pipe_ext && below((int64_t)((N - 1) / (B.R1 * B.R2)) * B.sr0 + (int64_t)B.Lh * B.Lw * B.nhwc);
-  else if (mb == 5) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)(K / 3) * B.sk0);
+  else if (mb == 5) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)(K / B.tapconv) * B.sk0);
   else if (mb == 3) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)K * B.sk0);
   // mode 3 in its plain form only: k = channel, rows (b, t) at unit stride in groups of 4
   const bool rows3 = mb == 3 && B.K1 == 1 && B.K2 == 1 && B.R1 == 1 && B.ch == 0 && B.cw == 0 &&
                      B.divh == 1 && B.divw == 1 && N % 4 == 0 &&
                      ((B.R2 == 1 && B.sr0 == 1) || (B.R2 % 4 == 0 && B.ar2 == 1 && B.sw == 1 && B.Lw >= B.R2));
   const bool pipe_launch = pipe_on && prec == 0 && p.bm == 64 && ma == 0 &&
-                           (mb == 0 || mb == 6 || (mb == 5 && a.B.halo) || rows3) && pipe_ext;
+                           (mb == 0 || mb == 6 || rows3 ||
+                            (mb == 5 && (a.B.halo || (B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 &&
+                                                      64 % B.R2 == 0)))) && pipe_ext;
   if (p.splits > 1 || interp) {
     const size_t need = split_ws_bytes(p, M, N, batch);
     if (ws == nullptr || ws_bytes < need) {

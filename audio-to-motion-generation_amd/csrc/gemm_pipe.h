@@ -200,6 +200,59 @@ struct PipeHalo {
   }
 };
 
+// tap-chunked conv1d / ConvTranspose phase, general layout (mode 5 without Gather::halo; NT =
+// 1-3 taps, any shift cw, clips of T <= 64 rows that tile the 64 rows): per 32-channel chunk the
+// x window is loaded once (as PipeHalo) and stored for every tap j, shifted by j + cw rows within
+// each clip -- gemm_tile's mode-5 store: element e of the thread's 4-row group lands on the row
+// whose source t + j + cw is its t, and the rows whose source leaves the clip receive 0 (written
+// by the element that wraps onto them)
+template <int NT>
+struct PipeTap {
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t off;      // byte offset of x[b][next chunk * 32 + kq][t] (kPipeOOB: rows invalid)
+  int kq, lrow, ch, Ci, sk0;
+  int o5[NT][4];     // per tap: LDS offsets of the thread's 4 elements in a [64][36] stage
+  int ok5;           // per tap and element: carries data (else 0 is stored)
+  __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
+    rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
+    lrow = (tid >> 4) * 4;
+    kq = tid & 15;
+    const int T = g.R2;
+    const int n = row0 + lrow;
+    const int b = n / T, tt = n - b * T;
+    Ci = KK / NT;
+    sk0 = g.sk0;
+    ch = (kbeg / (32 * NT)) * 32 + kq;
+    off = n < R ? (uint32_t)(b * g.sr0 + tt + ch * sk0) * 4u : kPipeOOB;
+    ok5 = 0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ts = tt + e;
+        int td = ts - (t + g.cw);
+        const bool ok = td >= 0 && td < T;
+        td += td < 0 ? T : (td >= T ? -T : 0);
+        o5[t][e] = (lrow + e + (td - ts)) * kPipeLDK + kq;
+        ok5 |= (ok ? 1 : 0) << (t * 4 + e);
+      }
+  }
+  __device__ __forceinline__ void load(float4 (&r)[2], int p) {
+    r[p] = pipe_load(rs, ch + 16 * p < Ci ? off + 4u * 16 * sk0 * p : kPipeOOB);
+    if (p == 1) {
+      ch += 32;
+      off += 4u * 32 * sk0;
+    }
+  }
+  // half p of the chunk's registers, shifted for tap `tap` (compile-time)
+  template <int TAP>
+  __device__ __forceinline__ void store(float* st, const float4 (&r)[2], int p) const {
+    const float v[4] = {r[p].x, r[p].y, r[p].z, r[p].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) st[o5[TAP][e] + 16 * p] = ((ok5 >> (TAP * 4 + e)) & 1) ? v[e] : 0.f;
+  }
+};
+
 __device__ __forceinline__ void pipe_frag(const float* p, float (&f)[8]) {
   const float4 v0 = *reinterpret_cast<const float4*>(p);
   const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
@@ -242,11 +295,12 @@ __device__ __forceinline__ void pipe_step(floatx16& acc, float (&fa0)[8], float 
   A2M_SB();
 }
 
-template <int MB>
+template <int MB, int NT = 0>   // NT > 0: mode 5 in the general (per-tap store) layout
 __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   span_begin(args.ts);
   constexpr int BM = 64, BN = 64, BK = 32, LDK = kPipeLDK;
-  constexpr bool HALO = MB == 5;
+  constexpr bool HALO = MB == 5 && NT == 0;
+  constexpr bool TAPS = MB == 5 && NT > 0;
   constexpr int TA = BM * LDK;
   constexpr int TB = (HALO ? PipeHalo::HR : BN) * LDK;
   __shared__ __attribute__((aligned(16))) float lds[2 * TA + 2 * TB];   // A stages, then B stages
@@ -287,7 +341,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   PipeRows la;
   la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
   using LB = typename std::conditional<
-      MB == 5, PipeHalo,
+      MB == 5, typename std::conditional<TAPS, PipeTap<NT ? NT : 1>, PipeHalo>::type,
       typename std::conditional<MB == 6, PipeNhwc, typename std::conditional<MB == 3, PipeRowsT, PipeRows>::type>::type>::type;
   LB lb;
   lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
@@ -313,7 +367,63 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
     if (!args.partial && tid < BM && m0 + tid < args.M) epr[tid] = epi_row(args.E, m0 + tid + batch * args.E.pstride);
   };
 
-  if constexpr (!HALO) {
+  if constexpr (TAPS) {
+    // per k-tile stages for A and B (as mode 0); B's registers hold a whole chunk (two sets, by
+    // chunk parity): step i stores tile i + 1 (A from set (i + 1) & 1, B tap (i + 1) % NT of chunk
+    // (i + 1) / NT) and loads A tile i + 3, plus chunk (i + 3) / NT when tile i + 3 starts a chunk
+    // -- two k-steps before its first store, after the last store of the chunk that held its set
+    const int brow = brow_i * LDK + lh * 8;
+    la.load(ra[0], 0); la.load(ra[0], 1);
+    lb.load(rb[0], 0); lb.load(rb[0], 1);            // chunk 0 -> set 0
+    epi_consts();
+    la.load(ra[1], 0); la.load(ra[1], 1);
+    if (NT == 1) { lb.load(rb[1], 0); lb.load(rb[1], 1); }   // chunk 1 (tile 1)
+    la.store(As, ra[0], 0); la.store(As, ra[0], 1);
+    lb.template store<0>(Bs, rb[0], 0); lb.template store<0>(Bs, rb[0], 1);
+    la.load(ra[0], 0); la.load(ra[0], 1);            // tile 2
+    if (NT == 2) { lb.load(rb[1], 0); lb.load(rb[1], 1); }   // chunk 1 (tile 2)
+    if (NT == 1) { lb.load(rb[0], 0); lb.load(rb[0], 1); }   // chunk 2 (tile 2)
+    __syncthreads();
+    pipe_frag(As + arow, fa0);
+    pipe_frag(Bs + brow, fb0);
+    auto chunk = [&](auto par, int cc) {
+      constexpr int P = decltype(par)::value;
+      auto tap_step = [&](auto jj) {
+        constexpr int J = decltype(jj)::value;
+        constexpr int QA = ((NT % 2 ? P : 0) + J + 1) & 1;       // A set of tile i + 1 (= of tile i + 3)
+        constexpr int TS = (J + 1) % NT;                          // tap of tile i + 1
+        constexpr int QB = (P + (J + 1) / NT) & 1;                // B set of tile i + 1's chunk
+        constexpr bool LB3 = (J + 3) % NT == 0;                   // tile i + 3 starts a chunk
+        constexpr int QL = (P + (J + 3) / NT) & 1;                // its set
+        const int i = NT * cc + J;
+        const int c = (i & 1) * TA, n = TA - c;
+        float* const nA = As + n;
+        float* const nB = Bs + n;
+        pipe_step(acc, fa0, fb0, As + c + arow, Bs + c + brow, nA + arow, nB + brow, [&](int s) {
+          switch (s) {
+            case 0: la.store(nA, ra[QA], 0); break;
+            case 1: la.store(nA, ra[QA], 1); break;
+            case 2: lb.template store<TS>(nB, rb[QB], 0); break;
+            case 3: lb.template store<TS>(nB, rb[QB], 1); break;
+            case 4: la.load(ra[QA], 0); break;
+            case 5: la.load(ra[QA], 1); break;
+            case 6: if (LB3) lb.load(rb[QL], 0); break;
+            default: if (LB3) lb.load(rb[QL], 1); break;
+          }
+        });
+      };
+      tap_step(std::integral_constant<int, 0>());
+      if constexpr (NT > 1) tap_step(std::integral_constant<int, 1>());
+      if constexpr (NT > 2) tap_step(std::integral_constant<int, 2>());
+    };
+    const int nch = nk / NT;
+    int cc = 0;
+    for (; cc + 1 < nch; cc += 2) {
+      chunk(P0(), cc);
+      chunk(P1(), cc + 1);
+    }
+    if (cc < nch) chunk(P0(), cc);
+  } else if constexpr (!HALO) {
     const int brow = brow_i * LDK + lh * 8;
     la.load(ra[0], 0); la.load(ra[0], 1);
     lb.load(rb[0], 0); lb.load(rb[0], 1);
