@@ -135,8 +135,6 @@ SIGNATURES = {
                                                      ctypes.POINTER(F64), ctypes.POINTER(I64)]),
     'a2m_gemm_timing_read_ex': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
                                                ctypes.POINTER(F64), ctypes.POINTER(I64), ctypes.POINTER(F64)]),
-    'a2m_graph_stack_x6_fwd_f32': (ctypes.c_int, [P, I32, I32, P, P, I32, P, P, P, P, P, P, P, F32, P, P]),
-    'a2m_split_bf16x3_f32': (ctypes.c_int, [P, I64, P, P]),
     'a2m_timing_mark_to_launch_end': (ctypes.c_int, [I32, I64, ctypes.POINTER(ctypes.c_float)]),
     'a2m_timing_mark': (ctypes.c_int, [I32, ctypes.c_void_p]),
     'a2m_timing_mark_elapsed': (ctypes.c_int, [I32, I32, ctypes.POINTER(ctypes.c_float)]),

@@ -493,34 +493,9 @@ def graph_att_proj(w0, att_src, att_dst, cache=None):
     return U
 
 
-def weight_planes(w, cache=None, slot='p'):
-    """[3 * numel] bf16: the exact three-way bf16 split of w (hi, mid, lo planes;
-    a2m_split_bf16x3_f32), cached in `cache[slot]` per weight version."""
-    _check_dev(w)
-    key = _wkey((w,))
-    if cache is not None and cache.get(slot + 'key') == key:
-        return cache[slot]
-    wc = w.contiguous()
-    planes = torch.empty(3 * wc.numel(), dtype=torch.bfloat16, device=w.device)
-    N.check(N.lib.a2m_split_bf16x3_f32(_p(wc), wc.numel(), _p(planes), _stream()))
-    if cache is not None:
-        cache[slot + 'key'] = key
-        cache[slot] = planes
-    return planes
-
-
-# A2M_STACK_X6=1: the graph stack's layer products in bf16x6 on v_mfma_f32_32x32x16_bf16
-# (fp32-class) instead of v_mfma_f32_32x32x2_f32.  Off by default: a 2.7x smaller MFMA phase but
-# the hand stack measured 327-329 vs 314 us (the stack is bound by its VALU / LDS phases, and the
-# split adds VALU work and register spills; DESIGN.md 4)
-_STACK_X6 = os.environ.get('A2M_STACK_X6', '0') != '0'
-
-
-def graph_stack(x, J, nbr_ptr, nbr_idx, layers, slope=0.2, out=None, x6=None):
-    """Fused eval stack of graph layers (a2m_graph_stack_fwd_f32, or a2m_graph_stack_x6_fwd_f32
-    with x6 -- default A2M_STACK_X6, off).  x: [F*J, 64] contiguous; layers: list of
-    (kind, w0, w1, U, bias, ln_w, ln_b[, cache]) with U from graph_att_proj for GAT and `cache`
-    an optional dict that keeps the weights' bf16 planes between calls."""
+def graph_stack(x, J, nbr_ptr, nbr_idx, layers, slope=0.2, out=None):
+    """Fused eval stack of graph layers (a2m_graph_stack_fwd_f32).  x: [F*J, 64] contiguous;
+    layers: list of (kind, w0, w1, U, bias, ln_w, ln_b) with U from graph_att_proj for GAT."""
     _check_dev(x, out)
     assert x.is_contiguous() and x.shape[1] == 64 and x.shape[0] % J == 0 and 0 < len(layers) <= 8
     F = x.shape[0] // J
@@ -529,17 +504,6 @@ def graph_stack(x, J, nbr_ptr, nbr_idx, layers, slope=0.2, out=None, x6=None):
     n = len(layers)
     ptrs = lambda i: (ctypes.c_void_p * n)(*[_p(L[i]) for L in layers])  # noqa: E731
     kinds = (ctypes.c_int32 * n)(*[L[0] for L in layers])
-    if _STACK_X6 if x6 is None else x6:
-        p0, p1 = [], []
-        for L in layers:
-            cache = L[7] if len(L) > 7 else None
-            p0.append(weight_planes(L[1], cache, 'p0'))
-            p1.append(weight_planes(L[2], cache, 'p1') if L[2] is not None else None)
-        arr = lambda ts: (ctypes.c_void_p * n)(*[_p(t) for t in ts])  # noqa: E731
-        N.check(N.lib.a2m_graph_stack_x6_fwd_f32(_p(x), F, J, _p(nbr_ptr), _p(nbr_idx), n, kinds,
-                                                 arr(p0), arr(p1), ptrs(3), ptrs(4), ptrs(5), ptrs(6),
-                                                 slope, _p(out), _stream()))
-        return out
     N.check(N.lib.a2m_graph_stack_fwd_f32(_p(x), F, J, _p(nbr_ptr), _p(nbr_idx), n, kinds,
                                           ptrs(1), ptrs(2), ptrs(3), ptrs(4), ptrs(5), ptrs(6),
                                           slope, _p(out), _stream()))

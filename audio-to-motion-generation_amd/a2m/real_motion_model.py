@@ -100,14 +100,7 @@ class SelfAttention_G(_GraphTopology):
         nj = getattr(self, f'num_{part}_joints')
         pin, pout = getattr(self, f'{part}_proj_in'), getattr(self, f'{part}_proj_out')
         h = torch.empty(B, T, nj * 64, device=x.device)
-        if _PROJ_DENSE and x.stride(2) == 1 and x.stride(1) == T and T <= 64:
-            # A2M_PROJ_DENSE: x first copied to [B*T][C] rows, so the projection's activation
-            # operand is dense k-contiguous rows (loader mode 0) instead of t-runs (mode 3);
-            # the output is the node layout [B, T, J*64] either way
-            xt = F.bct_to_btc(x)
-            F.gemm(nj * 64, B * T, C, pin.weight, C, 1, xt, C, 1, h, 1, nj * 64, bias=pin.bias)
-        else:
-            F.conv1d(x, pin.weight, pin.bias, out=h.permute(0, 2, 1))
+        F.conv1d(x, pin.weight, pin.bias, out=h.permute(0, 2, 1))
         a, b = h.view(B * T * nj, 64), torch.empty(B * T * nj, 64, device=x.device)
         ptr, idx = self.topology(part)
         lns = getattr(self, f'{part}_layer_norms')
@@ -115,13 +108,12 @@ class SelfAttention_G(_GraphTopology):
             layers = []
             for L in range(5):
                 g = getattr(self, f'{part}_gcn{L + 1}')
-                planes = g.__dict__.setdefault('_planes', {})   # bf16x6 weight planes
                 if L % 2 == 0:
                     U = F.graph_att_proj(g.lin.weight, g.att_src, g.att_dst, cache=g._U)
-                    layers.append((0, g.lin.weight, None, U, g.bias, lns[L].weight, lns[L].bias, planes))
+                    layers.append((0, g.lin.weight, None, U, g.bias, lns[L].weight, lns[L].bias))
                 else:
                     layers.append((1, g.lin_rel.weight, g.lin_root.weight, None, g.lin_rel.bias,
-                                   lns[L].weight, lns[L].bias, planes))
+                                   lns[L].weight, lns[L].bias))
             a = F.graph_stack(a, nj, ptr, idx, layers, out=b)
         else:
             for L in range(5):
@@ -137,29 +129,6 @@ class SelfAttention_G(_GraphTopology):
         F.conv1d(a.view(B, T, nj * 64).permute(0, 2, 1), pout.weight, pout.bias, out=rows.permute(0, 2, 1))
         nrm = getattr(self, f'{part}_norm')
         return F.layernorm_to_bct(rows.view(B * T, C), nrm.weight, nrm.bias, T, eps=nrm.eps, out=out_bct)
-
-    def _branches_interleaved(self, feats, out, main, side):
-        parts = (('hand', side, self.body_feats), ('body', main, 0))
-        xs = {'hand': feats, 'body': feats}
-
-        def run(stage):
-            mods = {p: list(getattr(self, f'{p}_{stage}')) for p, _, _ in parts}
-            for i in range(max(len(m) for m in mods.values())):
-                for p, st, _ in parts:
-                    if i < len(mods[p]):
-                        with torch.cuda.stream(st):
-                            xs[p] = mods[p][i](xs[p])
-        run('decoder_pre')
-        for p, st, _ in parts:
-            with torch.cuda.stream(st):
-                xs[p] = self._graph_stack(p, xs[p], None)
-        run('decoder_post')
-        for p, st, f0 in parts:
-            with torch.cuda.stream(st):
-                lg = getattr(self, f'{p}_logits')
-                nf = lg.weight.shape[0]
-                F.conv1d(xs[p], lg.weight, lg.bias, out=out[:, :, f0:f0 + nf].permute(0, 2, 1))
-        main.wait_stream(side)
 
     def _branch(self, part, feats, pose_out, f0):
         self._branch_tail(part, getattr(self, f'{part}_decoder_pre')(feats), pose_out, f0)
@@ -298,37 +267,17 @@ class SelfAttention_G(_GraphTopology):
             # the body and hand decoders are independent after the UNet: the body branch runs
             # on a side stream (forked from / joined to the caller's, so graph capture records
             # both), overlapping its latency-bound small launches with the hand branch's
+            # the hand branch (42-joint graph stack) is the longer one; forked first, on the side
+            # stream (measured 2.96 vs 3.00 ms a step; a high-priority side stream measured 4.8 ms,
+            # each branch on its own side stream or the branches captured layer by layer in
+            # alternation measured neutral or slower: DESIGN.md 6 / 9)
             main = torch.cuda.current_stream(audio.device)
             side = _side_stream(audio.device)
             side.wait_stream(main)
-            if _INTERLEAVE:
-                # A2M_INTERLEAVE: the two branches captured layer by layer in alternation (hand on
-                # the side stream), so the graph's node order interleaves them
-                self._branches_interleaved(feats, out, main, side)
-            elif _TWO_SIDES:
-                # A2M_TWO_SIDES: each branch on its own side stream, both forked from and joined
-                # to the caller's (experiment: how the graph executor places the branches)
-                side2 = _side_stream(audio.device, 1)
-                side2.wait_stream(main)
-                with torch.cuda.stream(side):
-                    self._branch('hand', feats, out, self.body_feats)
-                with torch.cuda.stream(side2):
-                    self._branch('body', feats, out, 0)
-                main.wait_stream(side)
-                main.wait_stream(side2)
-            elif _HAND_FIRST:
-                # the hand branch (42-joint graph stack) is the longer one; forked first, on the
-                # side stream (measured 2.96 vs 3.00 ms a step; a high-priority side stream
-                # (A2M_SIDE_PRIO=1) measured 4.8 ms)
-                with torch.cuda.stream(side):
-                    self._branch('hand', feats, out, self.body_feats)
-                self._branch('body', feats, out, 0)
-            else:
-                with torch.cuda.stream(side):
-                    self._branch('body', feats, out, 0)
+            with torch.cuda.stream(side):
                 self._branch('hand', feats, out, self.body_feats)
-            if not _TWO_SIDES and not _INTERLEAVE:
-                main.wait_stream(side)
+            self._branch('body', feats, out, 0)
+            main.wait_stream(side)
         else:
             self._branch('body', feats, out, 0)
             self._branch('hand', feats, out, self.body_feats)
@@ -378,22 +327,14 @@ def _group_sources(m):
         return (m.conv.weight, m.conv.bias, n.weight, n.bias, n.running_mean, n.running_var)
     return m.weights()   # SelfAttention
 _FUSED_STACK = os.environ.get('A2M_GRAPH_STACK', '1') != '0'   # one launch for the 5 graph layers
-_PROJ_DENSE = os.environ.get('A2M_PROJ_DENSE', '0') != '0'
 _SIDE_STREAMS = {}
 
 
-_HAND_FIRST = os.environ.get('A2M_HAND_FIRST', '1') != '0'
-_SIDE_PRIO = os.environ.get('A2M_SIDE_PRIO', '0') != '0'
-_TWO_SIDES = os.environ.get('A2M_TWO_SIDES', '0') != '0'
-_INTERLEAVE = os.environ.get('A2M_INTERLEAVE', '0') != '0'
-
-
-def _side_stream(device, which=0):
-    key = (device.index or 0, which)
+def _side_stream(device):
+    key = device.index or 0
     s = _SIDE_STREAMS.get(key)
     if s is None:
-        prio = torch.cuda.Stream.priority_range()[1] if _SIDE_PRIO else 0   # highest
-        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device, priority=prio)
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
     return s
 
 

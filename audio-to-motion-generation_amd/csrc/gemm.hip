@@ -355,8 +355,11 @@ static const PlanRule kTunedPlans[] = {
     {1024, 2048, 6144, 64, 2},   // UNet up conv, T 32
     {512, 4096, 3072, 64, 2},    // UNet up conv, T 64
     {512, 2048, 1024, 64, 2},
-    {1024, 1024, 4096, 128, 4},  // the 128 tile kept, 4 splits instead of 8
-    {2048, 1024, 3072, 128, 2},  // UNet convT phase: 2 splits instead of 4 (2.675-2.698 vs 2.703-2.723 ms)
+    // round 5, with the pipelined 64x64 tile (two interleaved rounds each, r05 plan sweep): the
+    // UNet's last two 128x128 launches move to it
+    {1024, 1024, 4096, 64, 2},   // down conv (im2col) + convT phase: 2.347-2.355 vs 2.379 ms
+    {2048, 1024, 3072, 64, 1},   // conv1d k3 at T 16 (halo pipe): 2.342-2.344 vs 2.379 ms
+    {1024, 1024, 2048, 64, 1},   // convT phase (2 taps): 2.335-2.348 vs 2.342-2.370 ms (weak)
     {256, 4096, 2688, 64, 1},    // hand graph-stack output projection: 1 split instead of 2 (weaker
                                  // evidence: mean 2.694 vs 2.705 ms and 2.719 vs 2.753 ms on two noisy
                                  // boxes, seven of ten rounds lower)

@@ -25,9 +25,6 @@ constexpr int GF = 64;          // joint feature dim
 #ifndef STACK_IGLP   // the backend's MFMA / VALU interleaving hint for the k steps (-1: none)
 #define STACK_IGLP 2
 #endif
-#ifndef STACK_X6_PF
-#define STACK_X6_PF 0
-#endif
 #ifndef STACK_WG_PER_CU
 #define STACK_WG_PER_CU 3
 #endif
@@ -316,10 +313,6 @@ struct GraphStack {
   const float* bias[GMAXL];
   const float* ln_w[GMAXL];
   const float* ln_b[GMAXL];
-  // bf16x6 path (a2m_graph_stack_x6_fwd_f32): w0 / w1 as three bf16 planes [3][numel]
-  // (hi, mid, lo: a2m_split_bf16x3_f32), plane stride 4*64*64 (GAT) or 64*64 (GraphConv)
-  const __bf16* w0p[GMAXL];
-  const __bf16* w1p[GMAXL];
   float slope;
 };
 
@@ -443,156 +436,6 @@ __device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)
 #endif
 }
 
-// bf16x6 variant of the k loop: the same aggregation (each neighbour's 8 k-values of a 16-k
-// block gathered once for all heads, the same weights and order), then each 8-value A fragment
-// split exactly into three bf16 planes and multiplied against the pre-split weight planes with
-// the six products of order >= 2^-16 (smallest first) on v_mfma_f32_32x32x16_bf16: fp32-class
-// products (dropped terms < 2^-24 |a b|, as the engine's bf16x6) at 6 x 32 cycles per 16 k
-// instead of 8 x 64 cycles of v_mfma_f32_32x32x2_f32.  A lane's 8 k (16 b + 8 lh + 0..7) are
-// exactly the 32x32x16 operand layout, for the gathered rows and for the weights' rows alike.
-typedef __bf16 sbf16x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ void stack_split_pair(float a, float b, uint32_t* q) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 h2 __attribute__((ext_vector_type(2)));
-  const f2 v = {a, b};
-  const uint32_t hu = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h2));
-  const f2 hf = {__builtin_bit_cast(float, hu << 16), __builtin_bit_cast(float, hu & 0xffff0000u)};
-  const f2 r1 = v - hf;
-  const uint32_t mu = __builtin_bit_cast(uint32_t, __builtin_convertvector(r1, h2));
-  const f2 mf = {__builtin_bit_cast(float, mu << 16), __builtin_bit_cast(float, mu & 0xffff0000u)};
-  const f2 r2 = r1 - mf;
-  q[0] = hu;
-  q[1] = mu;
-  q[2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, h2));
-}
-__device__ __forceinline__ void stack_split8(const float (&v)[8], sbf16x8 (&o)[3]) {
-  uint32_t q[4][3];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) stack_split_pair(v[2 * i], v[2 * i + 1], q[i]);
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    const u4 w = {q[0][c], q[1][c], q[2][c], q[3][c]};
-    o[c] = __builtin_bit_cast(sbf16x8, w);
-  }
-}
-__device__ __forceinline__ constexpr int stack_x6_ia(int j) { return j == 0 ? 2 : j == 1 ? 1 : j == 2 ? 0 : j == 3 ? 1 : 0; }
-__device__ __forceinline__ constexpr int stack_x6_ib(int j) { return j == 0 ? 0 : j == 1 ? 1 : j == 2 ? 2 : j == 3 ? 0 : j == 4 ? 1 : 0; }
-
-template <int DL, bool GAT>
-__device__ __forceinline__ void stack_layer_x6(const float* xs, const float (*al)[GMAXN], const int (&id)[GMAXDEG],
-                                               int node, int d0, const __bf16* W0, const __bf16* W1, int li,
-                                               int lh, floatx16 (&acc)[2]) {
-  constexpr int NS = GAT ? GHEADS : 1;
-  float wq[NS][DL];
-  stack_edge_weights<DL, GAT>(al, id, node, d0, wq);
-  constexpr int PS = GAT ? GHEADS * GF * GF : GF * GF;   // plane stride
-  const int boff = li * GF + lh * 8;
-  auto load_b = [&](int seg, int b, sbf16x8 (&bw)[2][3]) {
-    const __bf16* W = GAT ? W0 + seg * GF * GF : (seg == 0 ? W0 : W1);
-    int o = boff + 16 * b;
-    asm volatile("" : "+v"(o));   // one 32-bit lane offset per segment (not 6 hoisted 64-bit addresses)
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        bw[t][p] = *reinterpret_cast<const sbf16x8*>(W + p * PS + t * 32 * GF + o);
-  };
-  auto mfma6 = [&](const sbf16x8 (&a)[3], const sbf16x8 (&bw)[2][3]) {
-#pragma unroll
-    for (int j = 0; j < 6; ++j)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[stack_x6_ia(j)], bw[t][stack_x6_ib(j)], acc[t], 0, 0, 0);
-  };
-#pragma unroll 1
-  for (int b = 0; b < 4; ++b) {
-    sbf16x8 bA[2][3];
-#if STACK_X6_PF
-    sbf16x8 bB[2][3];
-    load_b(0, b, bA);
-#endif
-    const int off = 16 * b + 8 * lh;
-    // the rows' LDS offsets, recomputed per block: left alone the compiler hoists every
-    // (neighbour, block) address out of the layer loop and spills them (140 VGPRs of spills)
-    int ro[DL];
-#pragma unroll
-    for (int q = 0; q < DL; ++q) {
-      int iq = id[q];
-      asm volatile("" : "+v"(iq));
-      ro[q] = iq * ZP + off;
-    }
-    float a[NS][8];
-#pragma unroll
-    for (int h = 0; h < NS; ++h)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[h][j] = 0.f;
-#pragma unroll
-    for (int q = 0; q < DL; ++q) {
-      const float4 v0 = *reinterpret_cast<const float4*>(xs + ro[q]);
-      const float4 v1 = *reinterpret_cast<const float4*>(xs + ro[q] + 4);
-      const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-      for (int h = 0; h < NS; ++h)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[h][j] += wq[h][q] * v[j];
-      if (q % 2 == 1) __builtin_amdgcn_sched_barrier(0);   // at most two neighbours' slices in flight
-    }
-    sbf16x8 A[3];
-#if STACK_X6_PF   // next segment's weight planes prefetched during this one's MFMAs (+24 VGPRs)
-    if constexpr (GAT) {
-#pragma unroll
-      for (int h = 0; h < GHEADS; ++h) {
-        if (h + 1 < GHEADS) load_b(h + 1, b, (h & 1) ? bA : bB);
-        stack_split8(a[h], A);
-        mfma6(A, (h & 1) ? bB : bA);
-      }
-    } else {
-      load_b(1, b, bB);   // the root weights
-      stack_split8(a[0], A);
-      mfma6(A, bA);
-      const float4 o0 = *reinterpret_cast<const float4*>(xs + node * ZP + off);
-      const float4 o1 = *reinterpret_cast<const float4*>(xs + node * ZP + off + 4);
-      const float o[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-      stack_split8(o, A);
-      mfma6(A, bB);
-    }
-#else
-#pragma unroll
-    for (int h = 0; h < (GAT ? GHEADS : 2); ++h) {
-      __builtin_amdgcn_sched_barrier(0);   // one segment's 24 weight registers live at a time
-      load_b(h, b, bA);
-      if (GAT || h == 0) {
-        stack_split8(a[GAT ? h : 0], A);
-      } else {   // GraphConv root term: the row's own values against the root weights
-        const float4 o0 = *reinterpret_cast<const float4*>(xs + node * ZP + off);
-        const float4 o1 = *reinterpret_cast<const float4*>(xs + node * ZP + off + 4);
-        const float o[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-        stack_split8(o, A);
-      }
-      mfma6(A, bA);
-    }
-#endif
-  }
-}
-
-template <bool GAT>
-__device__ __forceinline__ void stack_layer_dispatch_x6(int dl, const float* xs, const float (*al)[GMAXN],
-                                                        const int (&id)[GMAXDEG], int node, int d0,
-                                                        const __bf16* W0, const __bf16* W1, int li, int lh,
-                                                        floatx16 (&acc)[2]) {
-  switch (dl) {
-    case 1: stack_layer_x6<1, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 2: stack_layer_x6<2, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 3: stack_layer_x6<3, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 4: stack_layer_x6<4, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 5: stack_layer_x6<5, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 6: stack_layer_x6<6, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 7: stack_layer_x6<7, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    default: stack_layer_x6<8, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-  }
-}
-
 template <bool GAT>
 __device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, const float (*al)[GMAXN],
                                                      const int (&id)[GMAXDEG], int node, int d0, const float* W0,
@@ -609,7 +452,6 @@ __device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, co
   }
 }
 
-template <bool X6>
 __global__ __launch_bounds__(256, STACK_WG_PER_CU) void graph_stack_kernel(
     const float* __restrict__ x, int F, int J, const int* __restrict__ nbr_ptr,
     const int* __restrict__ nbr_idx, GraphStack S, float* __restrict__ y) {
@@ -685,7 +527,6 @@ __global__ __launch_bounds__(256, STACK_WG_PER_CU) void graph_stack_kernel(
   int idg[GMAXDEG];   // in-neighbours, then the GAT self loop at slot d0 (weight 0 in GraphConv)
 #pragma unroll
   for (int q = 0; q < GMAXDEG; ++q) idg[q] = q < d0 ? ids[q] : (q == d0 ? node : 0);
-  int nodec = node, d0c = d0;   // (X6: opaque per-layer copies, below)
   // wave-uniform gather bound: the largest in-degree among this wave's rows
   int dw = d0;
 #pragma unroll
@@ -694,14 +535,6 @@ __global__ __launch_bounds__(256, STACK_WG_PER_CU) void graph_stack_kernel(
   for (int L = 0; L < S.nlayers; ++L) {
     const int kind = S.kind[L];
     const bool gat = kind == 0;
-    if constexpr (X6) {
-      // the row's gather ids, re-materialised per layer: otherwise every address and mask derived
-      // from them (logit reads, LDS rows, GraphConv weights) is hoisted out of the layer loop and
-      // held in registers the bf16x6 k loop needs (it spilled 110+ VGPRs)
-#pragma unroll
-      for (int q = 0; q < GMAXDEG; ++q) asm volatile("" : "+v"(idg[q]));
-      asm volatile("" : "+v"(d0c), "+v"(nodec));
-    }
     int dl;                      // wave-uniform number of gather slots this layer
     if (gat) {
       const float* U = S.U[L];
@@ -740,13 +573,8 @@ __global__ __launch_bounds__(256, STACK_WG_PER_CU) void graph_stack_kernel(
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
     dl = __builtin_amdgcn_readfirstlane(dl);
-    if constexpr (X6) {
-      if (gat) stack_layer_dispatch_x6<true>(dl, xs, al, idg, nodec, d0c, S.w0p[L], S.w1p[L], li, lh, acc);
-      else stack_layer_dispatch_x6<false>(max(dl, 1), xs, al, idg, nodec, d0c, S.w0p[L], S.w1p[L], li, lh, acc);
-    } else {
-      if (gat) stack_layer_dispatch<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
-      else stack_layer_dispatch<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
-    }
+    if (gat) stack_layer_dispatch<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
+    else stack_layer_dispatch<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
     // epilogue: out = LReLU(LN(acc * scale + bias)) + x, in place (or to y after the last layer).
     // The wave's 32 x 64 result goes through its private LDS scratch, 8 rows at a time (rows
     // 8p..8p+7 are exactly accumulator entries q = 4p..4p+3), so that each lane then owns 8
@@ -829,44 +657,6 @@ extern "C" int a2m_graph_att_proj_f32(const float* w0, const float* att_src, con
   return A2M_OK;
 }
 
-__global__ void split_bf16x3_kernel(const float* __restrict__ src, int64_t n, uint32_t* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // element pair
-  if (2 * i >= n) return;
-  const float a = src[2 * i], b = 2 * i + 1 < n ? src[2 * i + 1] : 0.f;
-  uint32_t q[3];
-  stack_split_pair(a, b, q);
-  const int64_t half = (n + 1) / 2;   // plane stride in pairs (n even for every stack weight)
-#pragma unroll
-  for (int c = 0; c < 3; ++c) dst[c * half + i] = q[c];
-}
-
-static int graph_stack_launch(bool x6, const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
-                              const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
-                              const float* const* w0, const float* const* w1, const void* const* w0p,
-                              const void* const* w1p, const float* const* U, const float* const* bias,
-                              const float* const* ln_w, const float* const* ln_b, float slope, float* y,
-                              void* stream);
-
-extern "C" int a2m_split_bf16x3_f32(const float* src, int64_t n, void* dst, void* stream) {
-  A2M_CHECK_ARG(src && dst && n >= 0 && n % 2 == 0, "split_bf16x3: bad arguments (n = %lld, even)", (long long)n);
-  if (n == 0) return A2M_OK;
-  hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)cdiv(n / 2, 256)), dim3(256), 0, as_stream(stream), src, n,
-                     static_cast<uint32_t*>(dst));
-  A2M_LAUNCH_CHECK();
-  return A2M_OK;
-}
-
-extern "C" int a2m_graph_stack_x6_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
-                                          const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
-                                          const void* const* w0p, const void* const* w1p,
-                                          const float* const* U, const float* const* bias,
-                                          const float* const* ln_w, const float* const* ln_b,
-                                          float slope, float* y, void* stream) {
-  A2M_CHECK_ARG(w0p && w1p, "graph_stack_x6: null plane pointers");
-  return graph_stack_launch(true, x, F, J, nbr_ptr, nbr_idx, nlayers, kinds, nullptr, nullptr, w0p, w1p, U, bias,
-                            ln_w, ln_b, slope, y, stream);
-}
-
 extern "C" int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
                                        const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
                                        const float* const* w0, const float* const* w1,
@@ -874,16 +664,6 @@ extern "C" int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, con
                                        const float* const* ln_w, const float* const* ln_b,
                                        float slope, float* y, void* stream) {
   A2M_CHECK_ARG(w0 && w1, "graph_stack: null pointer");
-  return graph_stack_launch(false, x, F, J, nbr_ptr, nbr_idx, nlayers, kinds, w0, w1, nullptr, nullptr, U, bias,
-                            ln_w, ln_b, slope, y, stream);
-}
-
-static int graph_stack_launch(bool x6, const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
-                              const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
-                              const float* const* w0, const float* const* w1, const void* const* w0p,
-                              const void* const* w1p, const float* const* U, const float* const* bias,
-                              const float* const* ln_w, const float* const* ln_b, float slope, float* y,
-                              void* stream) {
   A2M_CHECK_ARG(x && y && nbr_ptr && nbr_idx && kinds && U && bias && ln_w && ln_b,
                 "graph_stack: null pointer");
   A2M_CHECK_ARG(J > 0 && J <= GMAXN && F >= 0, "graph_stack: bad J=%d", J);
@@ -894,30 +674,18 @@ static int graph_stack_launch(bool x6, const float* x, int32_t F, int32_t J, con
   S.slope = slope;
   for (int L = 0; L < nlayers; ++L) {
     A2M_CHECK_ARG(kinds[L] == 0 || kinds[L] == 1, "graph_stack: layer %d kind %d", L, kinds[L]);
-    const bool has_w = x6 ? (w0p[L] && (kinds[L] == 0 || w1p[L])) : (w0[L] && (kinds[L] == 0 || w1[L]));
+    const bool has_w = w0[L] && (kinds[L] == 0 || w1[L]);
     A2M_CHECK_ARG(has_w && bias[L] && ln_w[L] && ln_b[L] && (kinds[L] != 0 || U[L] != nullptr),
                   "graph_stack: layer %d parameters missing", L);
-    if (x6)
-      A2M_CHECK_ARG((reinterpret_cast<uintptr_t>(w0p[L]) & 15) == 0 && (reinterpret_cast<uintptr_t>(w1p[L]) & 15) == 0,
-                    "graph_stack_x6: layer %d weight planes not 16-byte aligned", L);
     S.kind[L] = kinds[L];
-    if (x6) {
-      S.w0p[L] = static_cast<const __bf16*>(w0p[L]);
-      S.w1p[L] = static_cast<const __bf16*>(w1p[L]);
-    } else {
-      S.w0[L] = w0[L]; S.w1[L] = w1[L];
-    }
+    S.w0[L] = w0[L]; S.w1[L] = w1[L];
     S.U[L] = U[L];
     S.bias[L] = bias[L]; S.ln_w[L] = ln_w[L]; S.ln_b[L] = ln_b[L];
   }
   if (F == 0) return A2M_OK;
   const int fpb = GMAXN / J;
-  if (x6)
-    hipLaunchKernelGGL(graph_stack_kernel<true>, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
-                       x, F, J, nbr_ptr, nbr_idx, S, y);
-  else
-    hipLaunchKernelGGL(graph_stack_kernel<false>, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
-                       x, F, J, nbr_ptr, nbr_idx, S, y);
+  hipLaunchKernelGGL(graph_stack_kernel, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
+                     x, F, J, nbr_ptr, nbr_idx, S, y);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

@@ -273,18 +273,6 @@ int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t*
                             const float* const* w0, const float* const* w1, const float* const* U,
                             const float* const* bias, const float* const* ln_w,
                             const float* const* ln_b, float slope, float* y, void* stream);
-/* a2m_graph_stack_fwd_f32 with the layers' MFMAs in bf16x6 (fp32-class: the aggregated rows and
- * the weights each split exactly into three bf16 planes, the six products of order >= 2^-16 on
- * v_mfma_f32_32x32x16_bf16, fp32 accumulation).  w0p / w1p: per layer the weight planes
- * [3][numel] (hi, mid, lo; a2m_split_bf16x3_f32 of w0 / w1), 16-byte aligned. */
-int a2m_graph_stack_x6_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
-                               const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
-                               const void* const* w0p, const void* const* w1p, const float* const* U,
-                               const float* const* bias, const float* const* ln_w, const float* const* ln_b,
-                               float slope, float* y, void* stream);
-/* dst[3][n] (bf16 bits) = the exact three-way bf16 split of src[n] (hi = rne(v), mid = rne(v - hi),
- * lo = rne(v - hi - mid)); n even */
-int a2m_split_bf16x3_f32(const float* src, int64_t n, void* dst, void* stream);
 /* ---------------------------------------------------------------- skeleton graph layers
  * One fused GNN step of the body / hand decoders (real_motion_model.py:173-201, 225-253):
  *   y = LeakyReLU(LayerNorm64(L(x))) + x

@@ -146,7 +146,8 @@ def _gat_fn(x, edges, lw, a_s, a_d, bias, heads):
     ei = pyg._add_self_loops(edges, N)
     e = F.leaky_relu(asrc[ei[0]] + adst[ei[1]], 0.2)
     alpha = pyg._segment_softmax(e, ei[1], N)
-    out = torch.zeros_like(xp).index_add(0, ei[1], xp[ei[0]] * alpha.unsqueeze(-1))
+    msg = xp[ei[0]] * alpha.unsqueeze(-1)   # (under autocast: bf16 rows x fp32 weights -> fp32)
+    out = torch.zeros(xp.shape, dtype=msg.dtype).index_add(0, ei[1], msg)
     return out.mean(1) + bias
 
 

@@ -16,6 +16,7 @@ configs[4]  bf16 GEMM operands at the per-GPU batch of the 8-GPU leg (B = 32): G
             the reference's fp32 pose, the G-step gradient against fp32, and a full trainer
             iteration (dropout on).
 """
+import json
 import os
 import tempfile
 
@@ -25,7 +26,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import golden, golden_keys, rel_err
+from conftest import GOLDEN as GOLDEN_DIR, golden, golden_keys, rel_err
 
 pytestmark = pytest.mark.gpu
 DEV = 'cuda'
@@ -213,8 +214,11 @@ def test_bf16_train_step_b32():
     the FORWARD every layer adds ~2^-8 of relative error (encoder 4e-3 per layer, 1.3e-2 after
     the UNet's down path, 0.14 at the pose), and this G-step is ill-conditioned in the pose:
     the fp32 step with the pose perturbed by 1e-3 of its magnitude already has cosine 0.973.
-    So the all-bf16 step sits at cosine ~0.51 (median ~0.56) -- asserted as a regression bound
-    (>= 0.45 / 0.50), not as agreement."""
+    So the all-bf16 step sits at cosine ~0.51 (median ~0.56).  That is the reference's own bf16
+    behaviour: the reference's step restated by the oracle under torch.autocast(cpu, bfloat16)
+    on these inputs (oracle/make_autocast_fixture.py -> tests/golden/bf16_autocast.json) has G
+    cosine 0.484 / median 0.512, D 0.997, and a train-mode pose error of 0.148 (eval mode, running
+    statistics: 0.016).  Asserted: a2m's bf16 step no worse than autocast's, within 0.03."""
     import a2m
     from a2m import autograd as AG
     from a2m.training import GANTrainer, compute_temporal_smoothness_loss_and_jerk
@@ -271,7 +275,9 @@ def test_bf16_train_step_b32():
     assert abs(res['bf16'][2] - res['fp32'][2]) < 1e-2 * abs(res['fp32'][2])
     assert abs(res['bf16'][3] - res['fp32'][3]) < 2e-2 * abs(res['fp32'][3])
     assert cb[0] >= 0.999 and cb[1] >= 0.999, cb
-    assert cg[0] >= 0.45 and cg[1] >= 0.50, cg
+    ref = json.load(open(os.path.join(GOLDEN_DIR, 'bf16_autocast.json')))
+    assert cg[0] >= ref['g_cos_global'] - 0.03 and cg[1] >= ref['g_cos_weight_median'] - 0.03, (cg, ref)
+    assert cd[0] >= ref['d_cos_global'] - 0.01, (cd, ref)
     assert cd[0] > 0.99
     torch.manual_seed(0)
     from a2m.real_motion_model import SelfAttention_D, SelfAttention_G

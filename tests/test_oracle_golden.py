@@ -150,3 +150,27 @@ def test_eval_norm_oracle_vs_reference():
     for K in (52, 48):
         for alpha, tag in ((0.2, 'a02'), (0.1, 'a01')):
             assert np.array_equal(OE.compute_pck(z[f'pck{K}_pred'], z[f'pck{K}_gt'], alpha), z[f'pck{K}_{tag}'])
+
+
+def test_bf16_autocast_fixture_regenerates():
+    """tests/golden/bf16_autocast.json (the reference's bf16 step: oracle G-step + D-step under
+    torch.autocast(cpu, bfloat16), the bound of test_gpu_configs.py::test_bf16_train_step_b32)
+    regenerates from oracle/make_autocast_fixture.py in this process (~15 s).  Tolerance: the
+    step is ill-conditioned, so CPU thread order moves the cosines slightly."""
+    import json
+    import os
+    from oracle import make_autocast_fixture as M
+    with open(os.path.join(M.GOLDEN, 'bf16_autocast.json')) as f:
+        ref = json.load(f)
+    with open(os.path.join(M.GOLDEN, 'state_dict_keys.json')) as f:
+        keys = json.load(f)
+    gsd = {k: torch.from_numpy(np.asarray(v)) for k, v in M.weights.make_state_dict(keys['G'], seed=1234).items()}
+    dsd = {k: torch.from_numpy(np.asarray(v)) for k, v in M.weights.make_state_dict(keys['D'], seed=1235).items()}
+    gen = torch.Generator().manual_seed(21)
+    audio = torch.randn(32, 64, 128, generator=gen) * 2.0 - 3.0
+    pose = torch.from_numpy(M.synth.pose_targets(32, 64, seed=22))
+    f32 = M.step(gsd, dsd, audio, pose, False)
+    b16 = M.step(gsd, dsd, audio, pose, True)
+    cg = M.agree(f32[0], b16[0], keys['G'])
+    assert abs(cg[0] - ref['g_cos_global']) < 0.05 and abs(cg[1] - ref['g_cos_weight_median']) < 0.05
+    assert abs(M.rel(b16[4], f32[4]) - ref['pose_rel_err_train']) < 0.02
