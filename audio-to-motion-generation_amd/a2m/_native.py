@@ -157,7 +157,11 @@ def _load():
                           f'(make -C audio-to-motion-generation_amd)')
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and 'A2M_LIB' in os.environ:
+            continue   # an older library selected for an A/B run (tools/ab_lib*.sh) may lack newer entry points
+        if fn is None:
+            raise ImportError(f'a2m: {LIB_PATH} does not export {name}')
         fn.restype = res
         fn.argtypes = args
     return lib

@@ -592,6 +592,20 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                             (size_t)E.interp_H * sizeof(float) <= 32768),
                 "gemm: fused resample needs batch 1, N a multiple of H = %d <= 8192", E.interp_H);
   a.mcontig = stage_m && E.som == 1 && M > 1 && !interp;
+  // float4 output rows (pipelined tile): n contiguous within 4-aligned groups of one n2 run, every
+  // other stride and base 16-byte aligned; split-K slabs ([M][N]) whenever N % 4 == 0
+  static const int vec4_on = env_int("A2M_GEMM_VEC4", 1);
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool slab_out = p.splits > 1 || interp;
+  // the innermost index that varies with n: n2 (N2 > 1), else n1 (N1 > 1), else n0
+  const int in_lvl = E.N2 > 1 ? 2 : (E.N1 > 1 ? 1 : 0);
+  const int in_stride = in_lvl == 2 ? E.so2 : (in_lvl == 1 ? E.so1 : E.so0);
+  const int in_len = in_lvl == 2 ? E.N2 : (in_lvl == 1 ? E.N1 : 4);
+  const bool outer4 = (in_lvl == 0 || E.so0 % 4 == 0) && (in_lvl != 2 || E.N1 == 1 || E.so1 % 4 == 0) &&
+                      E.som % 4 == 0 && E.bstride % 4 == 0;
+  a.vec4 = vec4_on && !a.mcontig && N % 4 == 0 &&
+           (slab_out || (in_stride == 1 && in_len % 4 == 0 && outer4 && al16(E.out) &&
+                         (!E.res1 || al16(E.res1)) && (!E.res2 || al16(E.res2))));
   static const int ks2 = env_int("A2M_GEMM_KS2", 1);
   // software-pipelined one-wave-per-SIMD tile (gemm_pipe.h; A2M_GEMM_PIPE=0 restores gemm_tile):
   // fp32 64x64, dense weights x dense rows / channels-last rows / halo tap conv, every element

@@ -1,6 +1,9 @@
 // Launches of the software-pipelined 64x64 fp32 tile (gemm_pipe.h), one kernel per B operand mode.
 #include "gemm_pipe.h"
 
+#if A2M_PIPE_STAMPS
+__device__ unsigned long long g_pipe_stamps[kPipeStampBlocks * 6];
+#endif
 namespace a2m {
 void launch_pipe(const GemmArgs& a, int mb, int batch, hipStream_t st) {
   const dim3 grid((unsigned)cdiv(a.N, 64), (unsigned)cdiv(a.M, 64), (unsigned)(batch * a.splits));
@@ -13,3 +16,11 @@ void launch_pipe(const GemmArgs& a, int mb, int batch, hipStream_t st) {
   else hipLaunchKernelGGL(gemm_pipe_kernel<0>, grid, dim3(256), 0, st, a);
 }
 }  // namespace a2m
+
+#if A2M_PIPE_STAMPS
+// diagnostic builds only (tools/build_variant.sh ... -DA2M_PIPE_STAMPS=1): the stamp table
+extern "C" int a2m_debug_pipe_stamps(unsigned long long* out, int n) {
+  if (n > kPipeStampBlocks * 6) n = kPipeStampBlocks * 6;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pipe_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif

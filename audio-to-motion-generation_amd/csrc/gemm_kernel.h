@@ -39,6 +39,8 @@ struct GemmArgs {
   int splits, kchunk;
   float* partial;
   int xcd_group;   // >0: XCD-aware block remap with this many M-tiles per group; 0: identity
+  int vec4;        // (pipelined tile) output rows contiguous along n in 16-byte groups: the tile is
+                   // staged through LDS and written as float4 rows (host: gemm.hip)
   int mcontig;     // output has unit m stride: the tile is staged through LDS and written
                    // along m (split-K slabs then are [N][M])
   unsigned long long* ts;   // measurement only (a2m_gemm_timing_*; null otherwise): this launch's

@@ -28,6 +28,19 @@
 #ifndef A2M_PIPE_ABL
 #define A2M_PIPE_ABL 0
 #endif
+// Diagnostic builds only: A2M_PIPE_STAMPS = 1 records per block the shader clock at kernel entry,
+// after the prologue's barrier, after the k loop and after the epilogue, plus the constant-rate
+// clock at entry and exit, into g_pipe_stamps (read by a2m_debug_pipe_stamps, gemm_f32_pipe.hip)
+#ifndef A2M_PIPE_STAMPS
+#define A2M_PIPE_STAMPS 0
+#endif
+#if A2M_PIPE_STAMPS
+constexpr int kPipeStampBlocks = 4096;
+extern __device__ unsigned long long g_pipe_stamps[kPipeStampBlocks * 6];
+#define A2M_PSTAMP(i, v) do { if (threadIdx.x == 0) { const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); if (lin < kPipeStampBlocks) g_pipe_stamps[lin * 6 + (i)] = (v); } } while (0)
+#else
+#define A2M_PSTAMP(i, v) do { } while (0)
+#endif
 
 namespace a2m {
 
@@ -260,6 +273,52 @@ __device__ __forceinline__ void pipe_frag(const float* p, float (&f)[8]) {
   f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
 }
 
+// Epilogue for outputs whose n index is contiguous in 16-byte groups (args.vec4): the 64 x 64
+// accumulator tile goes to LDS as C[m][n] (pitch 68), then each thread finishes 4 float4 runs
+// of one row: the row's epilogue constants once, the residual / accumulate operands as float4
+// loads, one global_store_dwordx4 per 4 outputs (16 scalar stores per lane before: the
+// epilogue's store issue was ~7k cycles, the largest fixed cost of a one-block-per-CU launch).
+// Split-K slabs ([M][N] rows) take the same path.
+__device__ __forceinline__ void pipe_epilogue_vec4(const GemmArgs& args, const floatx16& acc, float* lds,
+                                                   const EpiRow* epr, bool slab, int zz, int batch, int m0,
+                                                   int n0, int tid, int wm, int wn, int li, int lh) {
+  constexpr int LDC = 68;
+#pragma unroll
+  for (int q = 0; q < 16; ++q)
+    lds[(wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh) * LDC + wn * 32 + li] = acc[q];
+  __syncthreads();
+  const Epilogue& E = args.E;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int idx = tid + 256 * j;
+    const int ml = idx >> 4, nl = (idx & 15) * 4;
+    const int m = m0 + ml, n = n0 + nl;
+    if (m >= args.M || n >= args.N) continue;
+    float4 v = *reinterpret_cast<const float4*>(lds + ml * LDC + nl);
+    if (slab) {
+      *reinterpret_cast<float4*>(args.partial + (int64_t)zz * args.M * args.N + (int64_t)m * args.N + n) = v;
+      continue;
+    }
+    const EpiRow r = epr[ml];
+    const int64_t off = (int64_t)batch * E.bstride + epi_addr(E, m, n);
+    v.x = epi_value_p(E, v.x, r); v.y = epi_value_p(E, v.y, r);
+    v.z = epi_value_p(E, v.z, r); v.w = epi_value_p(E, v.w, r);
+    if (E.res1) {
+      const float4 a = *reinterpret_cast<const float4*>(E.res1 + off);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    if (E.res2) {
+      const float4 a = *reinterpret_cast<const float4*>(E.res2 + off);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    if (E.accumulate) {
+      const float4 a = *reinterpret_cast<const float4*>(E.out + off);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    *reinterpret_cast<float4*>(E.out + off) = v;
+  }
+}
+
 #define A2M_SB() __builtin_amdgcn_sched_barrier(0)
 
 // One k-step.  ca / cb: this lane's fragment rows of tile i (A, B) at half 0 (the half-1
@@ -297,6 +356,8 @@ __device__ __forceinline__ void pipe_step(floatx16& acc, float (&fa0)[8], float 
 
 template <int MB, int NT = 0>   // NT > 0: mode 5 in the general (per-tap store) layout
 __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
+  A2M_PSTAMP(4, __builtin_amdgcn_s_memrealtime());
+  A2M_PSTAMP(0, __builtin_amdgcn_s_memtime());
   span_begin(args.ts);
   constexpr int BM = 64, BN = 64, BK = 32, LDK = kPipeLDK;
   constexpr bool HALO = MB == 5 && NT == 0;
@@ -384,6 +445,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
     if (NT == 2) { lb.load(rb[1], 0); lb.load(rb[1], 1); }   // chunk 1 (tile 2)
     if (NT == 1) { lb.load(rb[0], 0); lb.load(rb[0], 1); }   // chunk 2 (tile 2)
     __syncthreads();
+    A2M_PSTAMP(1, __builtin_amdgcn_s_memtime());
     pipe_frag(As + arow, fa0);
     pipe_frag(Bs + brow, fb0);
     auto chunk = [&](auto par, int cc) {
@@ -435,6 +497,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
     la.load(ra[0], 0); la.load(ra[0], 1);
     lb.load(rb[0], 0); lb.load(rb[0], 1);
     __syncthreads();
+    A2M_PSTAMP(1, __builtin_amdgcn_s_memtime());
     pipe_frag(As + arow, fa0);
     pipe_frag(Bs + brow, fb0);
     // step i (parity P = i & 1): stores of tile i + 1 from set (P + 1) & 1, then the loads of
@@ -483,6 +546,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
     lb.store(Bs, rx, 0); lb.store(Bs, rx, 1);
     la.load(ra[0], 0); la.load(ra[0], 1);
     __syncthreads();
+    A2M_PSTAMP(1, __builtin_amdgcn_s_memtime());
     pipe_frag(As + arow, fa0);
     pipe_frag(Bs + brow - LDK, fb0);   // tile 0 = tap 0: shift -1
     const int nch = nk / 3;
@@ -545,11 +609,19 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
     }
     if (cc < nch) chunk(P0(), cc);
   }
+  A2M_PSTAMP(2, __builtin_amdgcn_s_memtime());
   __syncthreads();   // the m-contiguous epilogue reuses the stages
   floatx16 accs[1][1];
   accs[0][0] = acc;
-  tile_epilogue<BM, BN, 1, 1>(args, accs, lds, epr, args.partial != nullptr, zz, batch, m0, n0, tid, wm, wn, li, lh);
+  if (args.vec4) pipe_epilogue_vec4(args, acc, lds, epr, args.partial != nullptr, zz, batch, m0, n0, tid, wm, wn, li, lh);
+  else tile_epilogue<BM, BN, 1, 1>(args, accs, lds, epr, args.partial != nullptr, zz, batch, m0, n0, tid, wm, wn, li, lh);
   span_end(args.ts);
+#if A2M_PIPE_STAMPS
+  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  A2M_PSTAMP(3, __builtin_amdgcn_s_memtime());
+  A2M_PSTAMP(5, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 #undef A2M_SB
