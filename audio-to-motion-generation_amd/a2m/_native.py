@@ -120,6 +120,7 @@ SIGNATURES = {
     'a2m_window_gather_f32': (ctypes.c_int, [P, I64, I32, P, I32, I32, I32, P, P, P, P]),
     'a2m_gemm_timing_begin': (ctypes.c_int, []),
     'a2m_gemm_plan_override': (ctypes.c_int, [I32, I32]),
+    'a2m_gemm_pipe_override': (ctypes.c_int, [I32]),
     'a2m_set_gemm_precision': (ctypes.c_int, [I32]),
     'a2m_get_gemm_precision': (I32, []),
     'a2m_gemm_timing_end': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),

@@ -6,7 +6,7 @@
 #include <vector>
 
 #include "gemm_kernel.h"
-#include "gemm_pipe.h"
+#include "gemm_pipe_bf16.h"
 
 namespace a2m {
 
@@ -321,6 +321,7 @@ static int gemm_xcd_group() {
 }
 
 static int g_override_tile = 0, g_override_split = 0;   // a2m_gemm_plan_override (tuning)
+static int g_pipe_override = -1;   // a2m_gemm_pipe_override: -1 A2M_GEMM_PIPE, 0 gemm_tile, 1 pipelined
 
 struct PlanRule {
   int M, N, K, tile, splits;
@@ -372,6 +373,24 @@ static const PlanRule* tuned_plan(int M, int N, int K, int prec) {
   return nullptr;
 }
 
+// bf16 (prec 1) throughput per CU by resident blocks, flop / us: staging- and latency-bound
+// rather than MFMA-bound (16x the f32 MFMA rate), so it grows with the blocks a CU holds far more
+// than the f32 tile's.  A2M_GEMM_BF16_THR="t1,t2,t3,t4[,t128_1,t128_2]" (kflop / us, experiments)
+static double bf16_thr(int tile, int c) {
+  static const std::vector<double> t = [] {
+    // fitted in the replayed bf16 bench step (r05 sweeps, two interleaved rounds each: 1.658 ms
+    // against 1.831 ms with round 4's 4 x the f32 table, {1360, 1712, 1740, 1760, 1856, 2000}e3)
+    std::vector<double> v = {530e3, 750e3, 900e3, 1060e3, 1500e3, 2000e3};
+    if (const char* e = std::getenv("A2M_GEMM_BF16_THR")) {
+      double x[6];
+      const int n = std::sscanf(e, "%lf,%lf,%lf,%lf,%lf,%lf", &x[0], &x[1], &x[2], &x[3], &x[4], &x[5]);
+      for (int i = 0; i < n; ++i) v[i] = x[i] * 1e3;
+    }
+    return v;
+  }();
+  return tile == 128 ? t[4 + (c > 1)] : t[std::min(std::max(c, 1), 4) - 1];
+}
+
 static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int tile, int kchunk,
                            int splits, int prec, bool conv_rows = false) {
   static const double thr64[4] = {340e3, 428e3, 435e3, 440e3};   // flop / us per CU
@@ -395,7 +414,7 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   // choices are the fastest measured (encoder 300.0 us; 87: 303.2 us; tools/enc_plan_ab.py)
   static const double rows6 = env_int("A2M_GEMM_MODE6_THR", 100) / 100.0;
   if (conv_rows && tile == 64 && prec == 0) thr *= rows6;
-  if (prec == 1) thr *= 4.0;  // staging-bound rather than MFMA-bound (16x MFMA rate); rough
+  if (prec == 1) thr = bf16_thr(tile, c) * (gathered && tile == 64 ? 0.84 : 1.0);
   const double block_flops = 2.0 * tile * tile * (double)kchunk;
   const double fixed = prec == 2 ? (tile == 128 ? 15.0 : 2.0)
                                  : (tile == 128 ? (gathered ? 16.0 : 10.0) : 3.0);
@@ -610,7 +629,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   // software-pipelined one-wave-per-SIMD tile (gemm_pipe.h; A2M_GEMM_PIPE=0 restores gemm_tile):
   // fp32 64x64, dense weights x dense rows / channels-last rows / halo tap conv, every element
   // offset below 2^29 floats (raw buffer loads)
-  static const int pipe_on = env_int("A2M_GEMM_PIPE", 1);
+  static const int pipe_env = env_int("A2M_GEMM_PIPE", 1);
+  const int pipe_on = g_pipe_override >= 0 ? g_pipe_override : pipe_env;
   auto below = [](int64_t v) { return v >= 0 && v < ((int64_t)1 << 29); };
   bool pipe_ext = below((int64_t)(M - 1) * A.sr0 + K);
   if (mb == 0) pipe_ext = pipe_ext && below((int64_t)(N - 1) * B.sr0 + K);
@@ -625,6 +645,12 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                            (mb == 0 || mb == 6 || rows3 ||
                             (mb == 5 && (a.B.halo || (B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 &&
                                                       64 % B.R2 == 0)))) && pipe_ext;
+  // the bf16-operand pipelined tile (gemm_pipe_bf16.h): the same operand modes, 64-channel
+  // k-tiles (mode 6: Ci % 64 == 0), no halo layout (mode 5 takes the per-tap stores)
+  const bool pipe_bf16 = pipe_on && prec == 1 && p.bm == 64 && ma == 0 &&
+                         (mb == 0 || (mb == 6 && B.nhwc % 64 == 0) || rows3 ||
+                          (mb == 5 && B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 && 64 % B.R2 == 0)) &&
+                         pipe_ext;
   if (p.splits > 1 || interp) {
     const size_t need = split_ws_bytes(p, M, N, batch);
     if (ws == nullptr || ws_bytes < need) {
@@ -636,7 +662,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   static const int log_launches = env_int("A2M_GEMM_LOG", 0);
   if (log_launches)
     std::fprintf(stderr, "a2m gemm M=%d N=%d K=%d batch=%d tile=%d bk=%d splits=%d%s modes=%d,%d som=%d so=%d,%d,%d N12=%d,%d\n",
-                 M, N, K, batch, p.bm, p.bk, p.splits, pipe_launch ? " (pipe)" : "", ma, mb, E.som, E.so0, E.so1,
+                 M, N, K, batch, p.bm, p.bk, p.splits, pipe_launch || pipe_bf16 ? " (pipe)" : "", ma, mb, E.som, E.so0, E.so1,
                  E.so2, E.N1, E.N2);
   a.ts = nullptr;
   if (g_timing) {
@@ -653,7 +679,8 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     }
   }
   if (prec == 1) {
-    if (p.bm == 128) launch_tile<128, 128, 64, 1>(a, ma, mb, batch, stream);
+    if (pipe_bf16) launch_pipe_bf16(a, mb, batch, stream);
+    else if (p.bm == 128) launch_tile<128, 128, 64, 1>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 64, 1>(a, ma, mb, batch, stream);
   } else if (prec == 2) {
     if (p.bm == 128) launch_tile<128, 128, 32, 2>(a, ma, mb, batch, stream);
@@ -703,6 +730,12 @@ int a2m_gemm_plan_override(int32_t tile, int32_t splits) {
                 "gemm_plan_override: tile %d splits %d", tile, splits);
   a2m::g_override_tile = tile;
   a2m::g_override_split = splits;
+  return A2M_OK;
+}
+
+int a2m_gemm_pipe_override(int32_t mode) {
+  A2M_CHECK_ARG(mode >= -1 && mode <= 1, "gemm_pipe_override: %d (-1 env, 0 off, 1 on)", mode);
+  a2m::g_pipe_override = mode;
   return A2M_OK;
 }
 

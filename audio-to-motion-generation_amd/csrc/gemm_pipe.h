@@ -321,6 +321,30 @@ __device__ __forceinline__ void pipe_epilogue_vec4(const GemmArgs& args, const f
 
 #define A2M_SB() __builtin_amdgcn_sched_barrier(0)
 
+// block -> (n-tile, m-tile, batch * split), XCD-grouped as in gemm_tile (block-uniform: SGPRs)
+__device__ __forceinline__ void pipe_block(const GemmArgs& args, int& bx, int& by, int& bz) {
+  bx = blockIdx.x; by = blockIdx.y; bz = blockIdx.z;
+  if (args.xcd_group > 0) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int q = total / 8, r = total % 8, x = L % 8;
+    const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
+    bz = t / (gx * gy);
+    const int rem = t - bz * gx * gy;
+    const int gm = args.xcd_group;
+    const int group = rem / (gm * gx);
+    const int first_m = group * gm;
+    const int gsz = min(gy - first_m, gm);
+    const int in = rem - group * gm * gx;
+    by = first_m + in % gsz;
+    bx = in / gsz;
+  }
+  bx = __builtin_amdgcn_readfirstlane(bx);
+  by = __builtin_amdgcn_readfirstlane(by);
+  bz = __builtin_amdgcn_readfirstlane(bz);
+}
+
 // One k-step.  ca / cb: this lane's fragment rows of tile i (A, B) at half 0 (the half-1
 // fragments are 16 floats further); na / nb: those of tile i + 1.  f0 holds tile i's half-0
 // fragments on entry and tile i + 1's on exit.  work(s), s = 0..7, is the operand work placed
@@ -371,27 +395,8 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
 
-  // block -> (n-tile, m-tile, batch * split), XCD-grouped as in gemm_tile
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (args.xcd_group > 0) {
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int total = gx * gy * gridDim.z;
-    const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const int q = total / 8, r = total % 8, x = L % 8;
-    const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
-    bz = t / (gx * gy);
-    const int rem = t - bz * gx * gy;
-    const int gm = args.xcd_group;
-    const int group = rem / (gm * gx);
-    const int first_m = group * gm;
-    const int gsz = min(gy - first_m, gm);
-    const int in = rem - group * gm * gx;
-    by = first_m + in % gsz;
-    bx = in / gsz;
-  }
-  bx = __builtin_amdgcn_readfirstlane(bx);
-  by = __builtin_amdgcn_readfirstlane(by);
-  bz = __builtin_amdgcn_readfirstlane(bz);
+  int bx, by, bz;
+  pipe_block(args, bx, by, bz);
   const int zz = bz;
   const int batch = zz / args.splits, split = zz % args.splits;
   const int m0 = by * BM, n0 = bx * BN;
@@ -623,8 +628,6 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   A2M_PSTAMP(5, __builtin_amdgcn_s_memrealtime());
 #endif
 }
-
-#undef A2M_SB
 
 void launch_pipe(const GemmArgs& a, int mb, int batch, hipStream_t st);
 

@@ -512,7 +512,7 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
     tf_exec = it['flops'] / (ms_exec * 1e-3) / 1e12
     tf_disp = it['flops'] / (ms_disp * 1e-3) / 1e12
     tf_ser = gt.flops / ((gt.ms_tile + gt.ms_reduce) * 1e-3) / 1e12
-    traffic = load_traffic('gemm_kernel') if peak == FP32_MFMA_PEAK_TFLOPS else None
+    traffic = load_traffic('gemm_engine') if peak == FP32_MFMA_PEAK_TFLOPS else None
     if tr:
         ms_fam = tr['family_us'] / 1e3
         tf = it['flops'] / (ms_fam * 1e-3) / 1e12
@@ -531,6 +531,8 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
             'achieved': round(tf, 2), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(tf / peak, 4),
             'traffic': traffic['bytes_per_launch'] if traffic else None,
+            'traffic_unit': 'HBM bytes per engine tile launch (the family\'s bytes per step / its tile launches)',
+            'traffic_bytes_per_step': traffic.get('bytes_per_step') if traffic else None,
             'traffic_source': traffic['source'] if traffic else None,
             'basis': basis,
             'family_ms_per_step': round(ms_fam, 4),

@@ -504,6 +504,10 @@ int a2m_gemm_timing_begin(void);
 /* Tuning hook: force the engine's tile (64 | 128) and split-K count for subsequent launches
  * (0 = the planner's choice); workspace sizing follows.  Process-global, not for production. */
 int a2m_gemm_plan_override(int32_t tile, int32_t splits);
+/* Test / tuning hook: which 64x64 tile kernel eligible launches take -- 1 the software-pipelined
+ * tile (gemm_pipe.h / gemm_pipe_bf16.h), 0 gemm_tile, -1 the A2M_GEMM_PIPE environment default
+ * (1).  Both give bitwise-equal results; process-global, not for production. */
+int a2m_gemm_pipe_override(int32_t mode);
 /* Operand precision of every GEMM-engine launch (convs, linears, attention products and their
  * backward) issued after the call: 0 = fp32 (default; the parity configuration), 1 = bf16
  * operands with fp32 accumulation (BASELINE configs[4], torch.autocast(bfloat16)-equivalent:

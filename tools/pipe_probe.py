@@ -1,6 +1,6 @@
 """Per-launch A/B of the software-pipelined tile (gemm_pipe.h) against gemm_tile on the step's
 one-wave-per-SIMD shapes (diagnostic).  Run twice, A2M_GEMM_PIPE=1 / 0:
-    python tools/pipe_probe.py"""
+    python tools/pipe_probe.py [bf16]"""
 import os
 import sys
 
@@ -9,11 +9,18 @@ sys.path.insert(0, os.path.join(REPO, 'audio-to-motion-generation_amd'))
 sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
+BF16 = 'bf16' in sys.argv[1:]
+sys.argv[1:] = [a for a in sys.argv[1:] if a != 'bf16']   # tools.conv_ab reads the rest as shapes
+
 from a2m import functional as F  # noqa: E402
 from tools.conv_ab import graph_time  # noqa: E402
 
 dev = torch.device('cuda')
 tag = 'pipe' if os.environ.get('A2M_GEMM_PIPE', '1') != '0' else 'tile'
+if BF16:
+    import a2m
+    a2m.set_gemm_precision('bf16')
+    tag += '-bf16'
 torch.manual_seed(0)
 for M, N, K in [(256, 4096, 768), (256, 4096, 256), (256, 4096, 512), (2688, 4096, 256), (256, 4096, 2688),
                 (512, 2048, 1024), (1024, 2048, 2048)]:

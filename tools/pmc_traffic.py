@@ -21,7 +21,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from replay_filter import load, replayed  # noqa: E402
 
-FAMILIES = ('gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'logmel_kernel',
+FAMILIES = ('gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'logmel_kernel',
             'graph_stack_kernel', 'graph_layer_kernel', 'graph_att_proj_kernel', 'attn_fused_eval_kernel',
             'attn_core_wide_kernel', 'conv2d_c1_kernel', 'im2col2d_kernel', 'im2col1d_kernel',
             'channel_attention_kernel', 'softmax_rows_kernel', 'layernorm_kernel')
@@ -51,6 +51,7 @@ def main():
     ap.add_argument('write_dir')
     ap.add_argument('--out', default='profiles/traffic_latest.json')
     ap.add_argument('--tag', default='')
+    ap.add_argument('--steps', type=int, default=3, help='replayed steps in the PMC runs (tools/step_pmc.py R)')
     a = ap.parse_args()
     fetch, write = read_counter(a.fetch_dir, 'FETCH_SIZE'), read_counter(a.write_dir, 'WRITE_SIZE')
     out = {}
@@ -64,6 +65,19 @@ def main():
         out[fam] = {'bytes_per_launch': round(rd + wr), 'read_bytes_per_launch': round(rd),
                     'write_bytes_per_launch': round(wr), 'dispatches': [nf, nw],
                     'source': f'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes {a.tag}, replayed steps only; FETCH x2 (gfx950), KB x1024'}
+    # the implicit-GEMM engine as one family (bench.py's roofline): tile kernels of both kinds and
+    # every split-K reduce; bytes per step over the replayed steps, and per tile launch
+    eng = [f for f in ('gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel') if f in out]
+    if eng:
+        steps = a.steps
+        rd = sum(out[f]['read_bytes_per_launch'] * out[f]['dispatches'][0] for f in eng)
+        wr = sum(out[f]['write_bytes_per_launch'] * out[f]['dispatches'][1] for f in eng)
+        tiles = sum(out[f]['dispatches'][0] for f in eng if f != 'splitk_reduce_kernel')
+        out['gemm_engine'] = {'bytes_per_step': round((rd + wr) / steps), 'read_bytes_per_step': round(rd / steps),
+                              'write_bytes_per_step': round(wr / steps),
+                              'bytes_per_launch': round((rd + wr) / max(tiles, 1)),
+                              'tile_launches_per_step': tiles / steps, 'families': eng,
+                              'source': out[eng[0]]['source'] + f'; {steps} replayed steps'}
     os.makedirs(os.path.dirname(a.out) or '.', exist_ok=True)
     with open(a.out, 'w') as f:
         json.dump(out, f, indent=1)

@@ -1,7 +1,8 @@
 """Per-step kernel breakdown of the graph-replayed bench steps in a rocprofv3 kernel trace of
 tools/step_pmc.py (dispatches after the marker only, tools/replay_filter.py), and the GEMM
 engine's in-step roofline figure from it: algorithmic FLOPs per step (bench.py
-g_forward GEMM count, passed in) / summed gemm_kernel durations per step.
+g_forward GEMM count, passed in) / summed GEMM-engine durations per step (both tile kernels and the
+split-K reduces, as bench.py's roofline).
 
     python tools/replay_breakdown.py TRACE_DIR_or_kernel_trace.csv STEPS [--gflop 184.4] [--out f.txt]
 """
@@ -36,9 +37,11 @@ def main():
     span = (int(rows[-1]['End_Timestamp']) - int(rows[0]['Start_Timestamp'])) / 1e3
     lines = [f'{len(rows)} dispatches after the marker = {n} replayed steps; first-to-last span '
              f'{span / n:.1f} us/step; kernel-time sum {tot / n:.1f} us/step']
-    gemm = sum(v[1] for k, v in agg.items() if 'gemm_kernel' in k) / n
-    gcalls = sum(v[0] for k, v in agg.items() if 'gemm_kernel' in k) / n
-    lines.append(f'gemm_kernel: {gcalls:.1f} launches/step, {gemm:.1f} us/step')
+    def engine(k):
+        return 'gemm_kernel' in k or 'gemm_pipe_kernel' in k or 'splitk_reduce' in k
+    gemm = sum(v[1] for k, v in agg.items() if engine(k)) / n
+    gcalls = sum(v[0] for k, v in agg.items() if engine(k)) / n
+    lines.append(f'GEMM engine (gemm_kernel + gemm_pipe_kernel + splitk_reduce): {gcalls:.1f} launches/step, {gemm:.1f} us/step')
     if a.gflop:
         tf = a.gflop * 1e9 / (gemm * 1e-6) / 1e12
         lines.append(f'gemm roofline: {a.gflop:.1f} GFLOP / {gemm:.1f} us = {tf:.1f} TF = {tf / a.peak:.4f} of {a.peak}')
