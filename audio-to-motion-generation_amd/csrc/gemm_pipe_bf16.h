@@ -27,6 +27,18 @@
 
 namespace a2m {
 
+// Diagnostic builds only: A2M_PIPE_HALF_A = 1 skips half of the A (weight) loads (results
+// wrong; times what a bf16 weight copy would save)
+#ifndef A2M_PIPE_HALF_A
+#define A2M_PIPE_HALF_A 0
+#endif
+
+// operand register sets of the dense / channels-last / row-contiguous loops: a tile is loaded
+// A2M_PIPE_H_DEPTH k-steps before it is stored
+#ifndef A2M_PIPE_H_DEPTH
+#define A2M_PIPE_H_DEPTH 2
+#endif
+
 constexpr int kHK = 72;                 // [row][k] pitch of a 64-k bf16 stage, in halves
 constexpr int kHStage = 64 * kHK / 2;   // one operand stage, in floats
 
@@ -335,7 +347,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
           constexpr int s = decltype(sc)::value;
           if constexpr (s < 4) la.store(nA, ra[QA], s);
           else if constexpr (s < 6) lb.template store<TS>(nB, rb[QB], s - 4);
-          else if constexpr (s >= 8 && s < 12) la.load(ra[QA], s - 8);
+          else if constexpr (s >= 8 && s < 12) { if (!(A2M_PIPE_HALF_A && (s & 1))) la.load(ra[QA], s - 8); }
           else if constexpr (s >= 12) { if (LB3) lb.load(rb[QL], s - 12); }
         });
       };
@@ -351,40 +363,46 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
     }
     if (cc < nch) chunk(P0(), cc);
   } else {
-    load4(la, ra[0]);
-    load4(lb, rb[0]);
+    // D register sets, tile t in set t % D: step i stores tile i + 1 from set (i + 1) % D, then
+    // loads tile i + 1 + D into it; the loop is unrolled by D so the set indices are static
+    constexpr int D = A2M_PIPE_H_DEPTH;
+    float4 xa[D][4], xb[D][4];
+    load4(la, xa[0]);
+    load4(lb, xb[0]);
     epi_consts();
-    load4(la, ra[1]);
-    load4(lb, rb[1]);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) la.store(As, ra[0], s);
+    for (int d = 1; d < D; ++d) { load4(la, xa[d]); load4(lb, xb[d]); }
 #pragma unroll
-    for (int s = 0; s < LB::NST; ++s) lb.store(Bs, rb[0], s);
-    load4(la, ra[0]);
-    load4(lb, rb[0]);
+    for (int s = 0; s < 4; ++s) la.store(As, xa[0], s);
+#pragma unroll
+    for (int s = 0; s < LB::NST; ++s) lb.store(Bs, xb[0], s);
+    load4(la, xa[0]);
+    load4(lb, xb[0]);
     __syncthreads();
     first_frags();
-    // step i (parity P = i & 1): stores of tile i + 1 from set (P + 1) & 1, then the loads of
-    // tile i + 3 into that set
     auto step = [&](auto par, int i) {
-      constexpr int Q = (decltype(par)::value + 1) & 1;
+      constexpr int Q = (decltype(par)::value + 1) % D;
       const int c = (i & 1) * kHStage, n = kHStage - c;
       float* const nA = As + n;
       float* const nB = Bs + n;
       pipe_step_h(acc, fa0, fb0, H(As + c) + arow, H(Bs + c) + brow, H(nA) + arow, H(nB) + brow, [&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        if constexpr (s < 4) la.store(nA, ra[Q], s);
-        else if constexpr (s < 4 + LB::NST) lb.store(nB, rb[Q], s - 4);
-        else if constexpr (s >= 8 && s < 12) la.load(ra[Q], s - 8);
-        else if constexpr (s >= 12) lb.load(rb[Q], s - 12);
+        if constexpr (s < 4) la.store(nA, xa[Q], s);
+        else if constexpr (s < 4 + LB::NST) lb.store(nB, xb[Q], s - 4);
+        else if constexpr (s >= 8 && s < 12) { if (!(A2M_PIPE_HALF_A && (s & 1))) la.load(xa[Q], s - 8); }
+        else if constexpr (s >= 12) lb.load(xb[Q], s - 12);
       });
     };
     int i = 0;
-    for (; i + 1 < nk; i += 2) {
-      step(P0(), i);
-      step(P1(), i + 1);
+    for (; i + D - 1 < nk; i += D) {
+      step(HS<0>(), i);
+      if constexpr (D > 1) step(HS<1>(), i + 1);
+      if constexpr (D > 2) step(HS<2>(), i + 2);
+      if constexpr (D > 3) step(HS<3>(), i + 3);
     }
-    if (i < nk) step(P0(), i);
+    if (i < nk) step(HS<0>(), i);
+    if constexpr (D > 2) { if (i + 1 < nk) step(HS<1>(), i + 1); }
+    if constexpr (D > 3) { if (i + 2 < nk) step(HS<2>(), i + 2); }
   }
   __syncthreads();   // the epilogue reuses the stages
   floatx16 accs[1][1];
