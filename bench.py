@@ -533,6 +533,7 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
             'traffic': traffic['bytes_per_launch'] if traffic else None,
             'traffic_unit': 'HBM bytes per engine tile launch (the family\'s bytes per step / its tile launches)',
             'traffic_bytes_per_step': traffic.get('bytes_per_step') if traffic else None,
+            'traffic_over_dense_operands': traffic.get('traffic_over_dense') if traffic else None,
             'traffic_source': traffic['source'] if traffic else None,
             'basis': basis,
             'family_ms_per_step': round(ms_fam, 4),

@@ -52,6 +52,8 @@ def main():
     ap.add_argument('--out', default='profiles/traffic_latest.json')
     ap.add_argument('--tag', default='')
     ap.add_argument('--steps', type=int, default=3, help='replayed steps in the PMC runs (tools/step_pmc.py R)')
+    ap.add_argument('--plans', default=None, help='A2M_GEMM_LOG=1 tools/plan_log.py output of the same build: '
+                    'the step\'s dense operand + output bytes, 4 (M K + K N + M N) per launch')
     a = ap.parse_args()
     fetch, write = read_counter(a.fetch_dir, 'FETCH_SIZE'), read_counter(a.write_dir, 'WRITE_SIZE')
     out = {}
@@ -78,6 +80,18 @@ def main():
                               'bytes_per_launch': round((rd + wr) / max(tiles, 1)),
                               'tile_launches_per_step': tiles / steps, 'families': eng,
                               'source': out[eng[0]]['source'] + f'; {steps} replayed steps'}
+    if a.plans and 'gemm_engine' in out:
+        import re
+        txt = open(a.plans).read().split('--- second step')[-1]
+        dense = 0
+        for m in re.finditer(r'M=(\d+) N=(\d+) K=(\d+) batch=(\d+)', txt):
+            M, N, K, b = map(int, m.groups())
+            dense += 4 * b * (M * K + K * N + M * N)
+        e = out['gemm_engine']
+        e['dense_operand_bytes_per_step'] = dense
+        e['traffic_over_dense'] = round(e['bytes_per_step'] / dense, 3) if dense else None
+        e['dense_basis'] = ('4 (M K + K N + M N) bytes per engine launch of one eager step (plan log): the '
+                            'implicit B operand of a conv counted as its K x N im2col matrix')
     os.makedirs(os.path.dirname(a.out) or '.', exist_ok=True)
     with open(a.out, 'w') as f:
         json.dump(out, f, indent=1)

@@ -20,7 +20,8 @@ python tools/replay_breakdown.py $OUT/trace $R --gflop $GF --out $OUT/breakdown.
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $REPO/$OUT/fetch -o run -- python tools/step_pmc.py 3 "$@" > $OUT/fetch.log 2>&1 || { echo fetch failed; tail -5 $OUT/fetch.log; exit 3; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $REPO/$OUT/write -o run -- python tools/step_pmc.py 3 "$@" > $OUT/write.log 2>&1 || { echo write failed; tail -5 $OUT/write.log; exit 4; }
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $REPO/$OUT/mfma -o run -- python tools/step_pmc.py 3 "$@" > $OUT/mfma.log 2>&1 || { echo mfma failed; tail -5 $OUT/mfma.log; exit 5; }
-python tools/pmc_traffic.py $OUT/fetch $OUT/write --steps 3 --out $OUT/traffic.json --tag "$TAG (tools/step_pmc.sh)" > /dev/null || exit 6
+A2M_GEMM_LOG=1 timeout -k 10 120 python tools/plan_log.py "$@" > /dev/null 2> $OUT/plans.txt || { echo plan log failed; exit 9; }
+python tools/pmc_traffic.py $OUT/fetch $OUT/write --steps 3 --plans $OUT/plans.txt --out $OUT/traffic.json --tag "$TAG (tools/step_pmc.sh)" > /dev/null || exit 6
 python tools/pmc_mfma.py $OUT/mfma $OUT/trace --out $OUT/mfma.json > /dev/null || exit 7
 find $OUT -name "*counter_collection.csv" -size +20M -delete
 exit 0
