@@ -1,6 +1,6 @@
 """Times the fused eval graph stack (a2m_graph_stack_fwd_f32: GAT, GraphConv, GAT, GraphConv,
-GAT) at the bench shapes: hand (J=42) and body (J=10) over B*T = 4096 frames (the kernel
-A2M_STACK_X6 selects; weight planes cached outside the timed loop).
+GAT) at the bench shapes: hand (J=42) and body (J=10) over B*T = 4096 frames, each alone on the
+chip.
     python tools/stack_bench.py [hand|body] [iters]"""
 import os
 import sys
