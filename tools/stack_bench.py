@@ -48,4 +48,4 @@ for name, J, lo in (('hand', 42, 10), ('body', 10, 0)):
     e1.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / iters
     gf = FR * J * 64 * 64 * 2 * (3 * 4 + 2 * 2) / 1e9
-    print(f'{name} stack: {us:.1f} us/launch, {gf:.2f} GFLOP of MFMA work, {gf / us * 1e-3:.1f} TF', flush=True)
+    print(f'{name} stack: {us:.1f} us/launch, {gf:.2f} GFLOP of MFMA work, {gf / us * 1e3:.1f} TF', flush=True)
