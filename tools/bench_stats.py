@@ -1,7 +1,7 @@
 """Cross-check of the bench line's roofline against a rocprofv3 --kernel-trace --stats run of the
-same bench command (tools/gpu_round.sh): the gemm_kernel family's average launch duration over
-every launch of the run (the timed replays dominate: 200 steps x 36 launches) against the line's
-roofline.ms_per_launch (the in-step span stamps), and the top kernels of the summary.
+same bench command (tools/gpu_round.sh): the engine family's average launch duration (tile kernels
+and split-K reduces) over every launch of the run (the timed replays dominate: 200 steps x 47
+launches) against the line's roofline (its replayed-step kernel trace), and the top kernels.
 
     python tools/bench_stats.py PROF_DIR BENCH_JSON_LINE_FILE [--out file.txt]
 """
@@ -21,17 +21,22 @@ def main():
     fn = glob.glob(os.path.join(a.prof_dir, '**', '*kernel_stats.csv'), recursive=True)[0]
     rows = list(csv.DictReader(open(fn, newline='')))
     line = json.loads([x for x in open(a.bench_json) if x.startswith('{')][-1])
-    calls = sum(int(r['Calls']) for r in rows if 'gemm_kernel' in r['Name'])
-    ns = sum(float(r['TotalDurationNs']) for r in rows if 'gemm_kernel' in r['Name'])
+    def engine(n):
+        return 'gemm_kernel' in n or 'gemm_pipe' in n or 'splitk_reduce' in n
+    calls = sum(int(r['Calls']) for r in rows if engine(r['Name']))
+    ns = sum(float(r['TotalDurationNs']) for r in rows if engine(r['Name']))
     rp = line['roofline']
     avg_ms = ns / calls / 1e6
-    gfl = rp['gflop_per_launch']
-    out = [f'rocprofv3 --kernel-trace --stats of `python bench.py --no-cpu-baseline` ({os.path.basename(fn)})',
+    n_launch = rp.get('trace_launches_per_step') or (rp['launches_per_step'] + rp.get('reduces_per_step', 0))
+    line_avg = rp['family_ms_per_step'] / n_launch
+    gfl = rp['gflop_per_step'] / n_launch
+    out = [f'rocprofv3 --kernel-trace --stats of `python bench.py --no-cpu-baseline --no-trace` ({os.path.basename(fn)})',
            f'bench line: {line["ms_per_step"]} ms/step, roofline {rp["achieved"]} TF = {rp["frac"]} '
-           f'({rp["ms_per_launch"]} ms per gemm_kernel launch, {gfl} GFLOP per launch)',
-           f'rocprof gemm_kernel: {calls} launches, average {avg_ms:.4f} ms -> '
-           f'{gfl / avg_ms:.2f} TF = {gfl / avg_ms / rp["peak"]:.4f} of {rp["peak"]}; '
-           f'line / rocprof average = {rp["ms_per_launch"] / avg_ms:.4f}',
+           f'({rp["family_ms_per_step"]} ms of engine per step over {n_launch} launches = {line_avg:.4f} ms per '
+           f'launch, {gfl:.3f} GFLOP per launch on average)',
+           f'rocprof engine family (gemm_kernel / gemm_pipe_kernel / splitk_reduce*) over the whole command: '
+           f'{calls} launches, average {avg_ms:.4f} ms -> {gfl / avg_ms:.2f} TF = {gfl / avg_ms / rp["peak"]:.4f} of '
+           f'{rp["peak"]}; line / rocprof average = {line_avg / avg_ms:.4f}',
            '', 'Calls  TotalDurationNs  AverageNs  Percentage  Name']
     for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:30]:
         out.append(f'{r["Calls"]:>6} {float(r["TotalDurationNs"]):>15.0f} {float(r["AverageNs"]):>10.0f} '
