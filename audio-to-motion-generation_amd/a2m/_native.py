@@ -74,6 +74,10 @@ SIGNATURES = {
                                             U64, I32, F32, P, I64, I64, P, P, P, SZ, P]),
     'a2m_bn_train_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, I32, P, P, P, P, F32, I32,
                                             U64, I32, F32, P, P, P, P, P, SZ, P]),
+    'a2m_bn_eval_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, P, P, F32, I32, F32, P, I64, I64,
+                                           P, P, P]),
+    'a2m_bn_eval_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32,
+                                           P, P, P, P, P, SZ, P]),
     'a2m_bn_sync_stats_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, F32, I32, U64, P, P, SZ, P]),
     'a2m_bn_sync_apply_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, I64, P, P, P, P, F32, F32, F32,
                                              I32, U64, I32, F32, P, I64, I64, P, P, P]),

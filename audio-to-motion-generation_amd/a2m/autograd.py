@@ -8,8 +8,8 @@ Semantics follow the reference modules in training mode:
   GNN stack      proj_in -> 5 x {layer, LN, LeakyReLU, +res} -> Dropout -> proj_out -> LN
 Dropout masks are a counter-based hash of (seed, element); every call draws a fresh seed
 from a2m.autograd.next_seed() (seeded from torch.initial_seed(), or manual_seed()).
-BatchNorm in eval mode with gradients enabled is not supported (the reference never needs
-it: evaluation runs under torch.no_grad()).
+BatchNorm in eval mode with gradients enabled normalises with the running statistics (fixed in
+the backward), as nn.BatchNorm*d.eval() does.
 """
 import torch
 
@@ -45,8 +45,8 @@ class _ConvBNAct(torch.autograd.Function):
             raw = F.conv2d(x.contiguous(), w, b, cfg['stride'], cfg['pad'])
         else:
             raw = F.conv1d(x, w, b, cfg['stride'], cfg['pad'])
-        out, mean, rstd = F.bn_train(raw, gamma, beta, cfg['rm'], cfg['rv'], cfg['momentum'], cfg['eps'],
-                                     cfg['p'], cfg['mode'], cfg['seed'], cfg['act'], cfg['slope'])
+        out, mean, rstd = _bn_fwd(raw, gamma, beta, cfg, cfg['p'], cfg['mode'], cfg['seed'], cfg['act'],
+                                  cfg['slope'])
         ctx.save_for_backward(x, w, raw, gamma, beta, mean, rstd)
         ctx.cfg = cfg
         ctx.has_bias = b is not None
@@ -56,8 +56,8 @@ class _ConvBNAct(torch.autograd.Function):
     def backward(ctx, dout):
         x, w, raw, gamma, beta, mean, rstd = ctx.saved_tensors
         c = ctx.cfg
-        draw, dg, db, dbias = F.bn_train_bwd(dout.contiguous(), raw, gamma, beta, mean, rstd, c['p'],
-                                             c['mode'], c['seed'], c['act'], c['slope'], want_bias=ctx.has_bias)
+        draw, dg, db, dbias = _bn_bwd(dout.contiguous(), raw, gamma, beta, mean, rstd, c, c['p'], c['mode'],
+                                      c['seed'], c['act'], c['slope'], ctx.has_bias)
         dx = F.conv_dgrad(draw, w, x.shape, c['stride'], c['pad']) if _need(ctx, 0) else None
         dw = F.conv_wgrad(draw, x, w.shape, c['stride'], c['pad']) if _need(ctx, 1) else None
         return dx, dw, dbias, dg, db, None
@@ -92,13 +92,33 @@ class _deferred_batch_counters:
         return False
 
 
+def _bn_fwd(raw, gamma, beta, cfg, p, mode, seed, act, slope):
+    """BatchNorm (+ dropout) + activation of a conv output: batch statistics in training mode,
+    the running statistics (fixed, not updated; no dropout) in eval mode."""
+    if cfg['eval']:
+        return F.bn_eval(raw, gamma, beta, cfg['rm'], cfg['rv'], cfg['eps'], act, slope)
+    return F.bn_train(raw, gamma, beta, cfg['rm'], cfg['rv'], cfg['momentum'], cfg['eps'], p, mode, seed, act,
+                      slope)
+
+
+def _bn_bwd(dout, raw, gamma, beta, mean, rstd, cfg, p, mode, seed, act, slope, want_bias):
+    if cfg['eval']:
+        return F.bn_eval_bwd(dout, raw, gamma, beta, mean, rstd, act, slope, want_bias=want_bias)
+    return F.bn_train_bwd(dout, raw, gamma, beta, mean, rstd, p, mode, seed, act, slope, want_bias=want_bias)
+
+
 def _bn_cfg(norm, two_d, stride, pad, p, mode, act):
+    """Per-call BatchNorm settings.  A module in eval mode with gradients (e.g. attribution or
+    fine-tuning through a frozen G) normalises with its running statistics, as nn.BatchNorm*d
+    does in eval mode: no statistics update, no batch counter, and dropout is off (p = 0)."""
     if not norm.training:
-        raise NotImplementedError('BatchNorm in eval mode with gradients: run evaluation under torch.no_grad()')
+        return dict(two_d=two_d, stride=stride, pad=pad, rm=norm.running_mean, rv=norm.running_var,
+                    momentum=0.0, eps=norm.eps, p=0.0, mode=F.DROP_NONE, seed=0, act=act, slope=0.2,
+                    eval=True)
     _count_batch(norm)
     return dict(two_d=two_d, stride=stride, pad=pad, rm=norm.running_mean, rv=norm.running_var,
                 momentum=norm.momentum if norm.momentum is not None else 0.1, eps=norm.eps, p=p,
-                mode=mode, seed=next_seed() if p > 0 else 0, act=act, slope=0.2)
+                mode=mode, seed=next_seed() if p > 0 else 0, act=act, slope=0.2, eval=False)
 
 
 def conv_norm_act(m, x, out=None):
@@ -128,8 +148,7 @@ class _ConvTBN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, cfg):
         raw = F.convt1d(x.contiguous(), w, b, cfg['stride'], cfg['pad'], cfg['out_pad'])
-        out, mean, rstd = F.bn_train(raw, gamma, beta, cfg['rm'], cfg['rv'], cfg['momentum'], cfg['eps'],
-                                     0.0, F.DROP_NONE, 0, F.ACT_RELU)
+        out, mean, rstd = _bn_fwd(raw, gamma, beta, cfg, 0.0, F.DROP_NONE, 0, F.ACT_RELU, 0.2)
         ctx.save_for_backward(x, w, raw, gamma, beta, mean, rstd)
         ctx.cfg = cfg
         ctx.has_bias = b is not None
@@ -139,8 +158,8 @@ class _ConvTBN(torch.autograd.Function):
     def backward(ctx, dout):
         x, w, raw, gamma, beta, mean, rstd = ctx.saved_tensors
         c = ctx.cfg
-        draw, dg, db, dbias = F.bn_train_bwd(dout.contiguous(), raw, gamma, beta, mean, rstd, 0.0, F.DROP_NONE,
-                                             0, F.ACT_RELU, want_bias=ctx.has_bias)
+        draw, dg, db, dbias = _bn_bwd(dout.contiguous(), raw, gamma, beta, mean, rstd, c, 0.0, F.DROP_NONE, 0,
+                                      F.ACT_RELU, 0.2, ctx.has_bias)
         # ConvTranspose1d's dgrad is a plain conv with its own [Ci][Co][k] weight; its wgrad is
         # the conv wgrad with the operand roles exchanged.
         dx = F.conv1d(draw, w, None, c['stride'], c['pad']) if _need(ctx, 0) else None

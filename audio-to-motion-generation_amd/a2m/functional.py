@@ -648,6 +648,36 @@ def bn_train(x, gamma, beta, rmean, rvar, momentum, eps, p, mode, seed, act, slo
     return out, mean, rstd
 
 
+def bn_eval(x, gamma, beta, rmean, rvar, eps, act, slope=0.2, out=None):
+    """Eval-mode BatchNorm (running statistics, not updated) fused with the activation, for a
+    forward with gradients; returns (out, mean, rstd) for bn_eval_bwd."""
+    _check_dev(x, gamma, beta, rmean, rvar, out)
+    B, C, L, xsb, xsc = _bcl(x)
+    if out is None:
+        out = torch.empty(x.shape, device=x.device)
+    _, _, _, ysb, ysc = _bcl(out)
+    mean = torch.empty(C, device=x.device)
+    rstd = torch.empty(C, device=x.device)
+    N.check(N.lib.a2m_bn_eval_fwd_f32(_p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(rmean), _p(rvar),
+                                      eps, act, slope, _p(out), ysb, ysc, _p(mean), _p(rstd), _stream()))
+    return out, mean, rstd
+
+
+def bn_eval_bwd(dy, x, gamma, beta, mean, rstd, act, slope=0.2, want_bias=True):
+    """Backward of bn_eval: (dx, dgamma, dbeta, dbias) with the statistics held fixed."""
+    _check_dev(dy, x)
+    B, C, L, xsb, xsc = _bcl(x)
+    _, _, _, dsb, dsc = _bcl(dy)
+    dx = torch.empty(x.shape, device=x.device)
+    dg = torch.empty(C, device=x.device) if gamma is not None else None
+    db = torch.empty(C, device=x.device) if beta is not None else None
+    dbias = torch.empty(C, device=x.device) if want_bias else None
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_eval_bwd_f32(
+        _p(dy), dsb, dsc, _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(mean), _p(rstd), act, slope,
+        _p(dx), _p(dg), _p(db), _p(dbias), wp, wn, _stream()))
+    return dx, dg, db, dbias
+
+
 def bn_train_bwd(dy, x, gamma, beta, mean, rstd, p, mode, seed, act, slope=0.2, want_bias=True):
     _check_dev(dy, x)
     B, C, L, xsb, xsc = _bcl(x)

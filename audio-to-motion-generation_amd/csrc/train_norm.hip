@@ -265,6 +265,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(BNBwdArgs a, co
   if (threadIdx.x == 0) dpart[(int64_t)c * f.slices + s] = sd;
 }
 
+// Eval-mode BatchNorm with gradients (nn.BatchNorm*d in .eval(), model_layers.py:51-118): the
+// running statistics normalise and are not updated; the kernels above run with mean = running
+// mean and rstd = 1 / sqrt(running var + eps), and the backward drops the batch-statistics terms
+// (the apply divides the (sum g, sum g xhat) pair by n_div = +inf: exactly 0, so dz = gamma rstd g)
+__global__ void bn_eval_consts_kernel(const float* rmean, const float* rvar, int C, float eps,
+                                      float* mean, float* rstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    mean[c] = rmean[c];
+    rstd[c] = (float)(1.0 / sqrt((double)rvar[c] + (double)eps));
+  }
+}
+
 // SyncBN helpers: per-channel float64 (sum, sum2) pairs over the slices (all-reduced by the
 // host between the stats and apply phases), and the finalize / conversion steps on them.
 __global__ void reduce_pairs_kernel(const double* part, int C, int slices, double* sums,
@@ -476,6 +489,57 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
   a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
   a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
   a.n_div = (float)N;
+  hipStream_t st = as_stream(stream);
+  double* part = static_cast<double*>(ws);
+  double* dpart = part + 2 * (size_t)C * S;
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_apply_fused_kernel, dim3(C * S), dim3(256), 0, st, a, part, dgamma, dbeta,
+                     dx, dpart);
+  A2M_LAUNCH_CHECK();
+  if (dbias) {
+    hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, dpart, C,
+                       S, dbias);
+    A2M_LAUNCH_CHECK();
+  }
+  return A2M_OK;
+}
+
+int a2m_bn_eval_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
+                        const float* gamma, const float* beta, const float* running_mean,
+                        const float* running_var, float eps, int32_t act, float slope, float* y,
+                        int64_t ys_b, int64_t ys_c, float* save_mean, float* save_rstd, void* stream) {
+  A2M_CHECK_ARG(x && y && running_mean && running_var && save_mean && save_rstd && B > 0 && C > 0 && L > 0,
+                "bn_eval_fwd: bad args");
+  const int S = bn_slices((int64_t)B * L);
+  A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)B * L);
+  BNArgs a{x, xs_b, xs_c, B, C, L, S, 0.f, DROP_NONE, 0};
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(bn_eval_consts_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, running_mean,
+                     running_var, C, eps, save_mean, save_rstd);
+  A2M_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(C * S), dim3(256), 0, st, a, save_mean, save_rstd, gamma, beta,
+                     act, slope, y, ys_b, ys_c);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_bn_eval_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x, int64_t xs_b,
+                        int64_t xs_c, int32_t B, int32_t C, int32_t L, const float* gamma,
+                        const float* beta, const float* save_mean, const float* save_rstd, int32_t act,
+                        float slope, float* dx, float* dgamma, float* dbeta, float* dbias, void* ws,
+                        size_t ws_bytes, void* stream) {
+  A2M_CHECK_ARG(dy && x && dx && save_mean && save_rstd && B > 0 && C > 0 && L > 0, "bn_eval_bwd: bad args");
+  const int64_t N = (int64_t)B * L;
+  const int S = bn_slices(N);
+  A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
+  const size_t need = sizeof(double) * 3 * (size_t)C * S;
+  if (!ws || ws_bytes < need) { set_error("bn_eval_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
+  BNBwdArgs a;
+  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, 0.f, DROP_NONE, 0};
+  a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
+  a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
+  a.n_div = __builtin_inff();   // fixed statistics: no mean(g) / mean(g xhat) terms
   hipStream_t st = as_stream(stream);
   double* part = static_cast<double*>(ws);
   double* dpart = part + 2 * (size_t)C * S;

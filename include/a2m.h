@@ -336,6 +336,21 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
                          const float* save_rstd, float drop_p, int32_t drop_mode, uint64_t seed,
                          int32_t act, float slope, float* dx, float* dgamma, float* dbeta,
                          float* dbias, void* ws, size_t ws_bytes, void* stream);
+/* Eval-mode BatchNorm with gradients (nn.BatchNorm*d after .eval(), model_layers.py:51-118, e.g.
+ * fine-tuning or input attribution through a frozen G): normalises with the running statistics,
+ * which it does not update, fused with the activation; save_mean / save_rstd receive the running
+ * mean and 1 / sqrt(running_var + eps) for the backward.  No dropout (eval). */
+int a2m_bn_eval_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
+                        const float* gamma, const float* beta, const float* running_mean,
+                        const float* running_var, float eps, int32_t act, float slope, float* y,
+                        int64_t ys_b, int64_t ys_c, float* save_mean, float* save_rstd, void* stream);
+/* Its backward: dx = gamma * rstd * act'(.) * dy (fixed statistics: no batch-mean terms),
+ * dgamma = sum g * xhat, dbeta = sum g, dbias = sum dx, g = act'(.) * dy. */
+int a2m_bn_eval_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x, int64_t xs_b,
+                        int64_t xs_c, int32_t B, int32_t C, int32_t L, const float* gamma,
+                        const float* beta, const float* save_mean, const float* save_rstd, int32_t act,
+                        float slope, float* dx, float* dgamma, float* dbeta, float* dbias, void* ws,
+                        size_t ws_bytes, void* stream);
 /* SyncBatchNorm phases for data-parallel training (per-layer all-reduce of the
  * BatchNorm statistics so DP over ranks normalises like the single-device batch,
  * version5_model_train.py:342-414 at B = 64).  The fused bn_train_fwd/bwd above split at their

@@ -64,6 +64,77 @@ def test_conv_norm_act_train(two_d):
                   'beta': (m.norm.bias.grad, ref.norm.bias.grad)})
 
 
+@pytest.mark.parametrize('two_d', [False, True])
+def test_conv_norm_act_eval_mode_gradients(two_d):
+    """nn.BatchNorm in eval mode with gradients (model_layers.py:51-118 after .eval(); e.g. input
+    attribution through a frozen G): running statistics normalise and stay unchanged, and the
+    backward holds them fixed -- against torch-CPU autograd of the same eval-mode layer."""
+    from a2m.model_layers import ConvNormRelu
+    torch.manual_seed(0)
+    args = (3, 8) if two_d else (6, 10)
+    kind = '2d' if two_d else '1d'
+    m = ConvNormRelu(*args, type=kind, leaky=True, downsample=True)
+    ref = ConvNormRelu(*args, type=kind, leaky=True, downsample=True)
+    ref.load_state_dict(m.state_dict())
+    with torch.no_grad():
+        for mod in (m, ref):
+            mod.norm.running_mean.copy_(_r(args[1], seed=5, scale=0.3))
+            mod.norm.running_var.copy_(_r(args[1], seed=6).abs() + 0.5)
+            mod.norm.weight.copy_(_r(args[1], seed=7).abs() + 0.5)
+            mod.norm.bias.copy_(_r(args[1], seed=8, scale=0.2))
+    m.to(DEV).eval()
+    ref.eval()
+    rm0 = m.norm.running_mean.clone()
+    x = _r(4, 3, 12, 20, seed=1) if two_d else _r(3, 6, 17, seed=1)
+    xd, xc = _leaf(x)
+    yd = m(xd)
+    conv = TF.conv2d if two_d else TF.conv1d
+    yc = TF.leaky_relu(TF.batch_norm(conv(xc, ref.conv.weight, ref.conv.bias, stride=2, padding=1),
+                                     ref.norm.running_mean, ref.norm.running_var, ref.norm.weight,
+                                     ref.norm.bias, False, 0.1, 1e-5), 0.2)
+    assert rel_err(yd.detach().cpu(), yc.detach()) < TOL
+    assert torch.equal(m.norm.running_mean, rm0)
+    gy = _r(*yc.shape, seed=2)
+    yd.backward(gy.to(DEV))
+    yc.backward(gy)
+    _check_grads({'x': (xd.grad, xc.grad), 'w': (m.conv.weight.grad, ref.conv.weight.grad),
+                  'bias': (m.conv.bias.grad, ref.conv.bias.grad),
+                  'gamma': (m.norm.weight.grad, ref.norm.weight.grad),
+                  'beta': (m.norm.bias.grad, ref.norm.bias.grad)})
+
+
+def test_generator_eval_mode_input_gradient():
+    """SelfAttention_G in eval mode with gradients enabled (every BatchNorm on its running
+    statistics): the forward equals the no-grad eval forward, and d(pose)/d(mel) matches the
+    fp32 CPU oracle's autograd in eval mode."""
+    from a2m.real_motion_model import SelfAttention_G
+    from oracle import model as OM
+    torch.manual_seed(3)
+    g = SelfAttention_G(time_steps=64, p=0.2)
+    for mod in g.modules():
+        if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
+            with torch.no_grad():
+                mod.running_mean.copy_(torch.randn(mod.num_features) * 0.1)
+                mod.running_var.copy_(torch.rand(mod.num_features) + 0.5)
+        if hasattr(mod, 'gamma'):
+            torch.nn.init.constant_(mod.gamma, 0.3)
+    sd = {k: v.clone() for k, v in g.state_dict().items()}
+    g = g.to(DEV).eval()
+    mel = _r(2, 64, 128, seed=4) * 2.0 - 3.0
+    with torch.no_grad():
+        ref_pose = g(mel.to(DEV))[0].cpu()
+    md = mel.clone().to(DEV).requires_grad_(True)
+    pose = g(md)[0]
+    assert rel_err(pose.detach().cpu(), ref_pose) < TOL
+    gy = _r(*pose.shape, seed=5)
+    pose.backward(gy.to(DEV))
+    mc = mel.clone().requires_grad_(True)
+    pc, _ = OM.generator(sd, mc, train=False)
+    assert rel_err(pose.detach().cpu(), pc.detach()) < TOL
+    pc.backward(gy)
+    assert rel_err(md.grad.cpu(), mc.grad) < 1e-3, rel_err(md.grad.cpu(), mc.grad)
+
+
 def test_convt_bn_relu_train():
     from a2m.model_layers import ConvTranspose1D
     torch.manual_seed(0)
