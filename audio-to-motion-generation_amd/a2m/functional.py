@@ -386,6 +386,9 @@ def stacked_qkv(wq, bq, wk, bk, wv, bv, cache=None):
 
 
 _ATTN_EVAL_FUSED = __import__('os').environ.get('A2M_ATTN_EVAL_FUSED', '1') != '0'
+# bf16 operand mode: the fused eval attention with its projection on the bf16 MFMA
+# (A2M_ATTN_EVAL_BF16=0: the engine's bf16 QKV GEMM + the attention core, as in round 4)
+_ATTN_EVAL_BF16 = os.environ.get('A2M_ATTN_EVAL_BF16', '1') != '0'
 
 
 def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=None, cache=None):
@@ -402,7 +405,8 @@ def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=No
         assert res.stride() == out.stride()
     wqkv, bqkv = stacked_qkv(wq, bq, wk, bk, wv, bv, cache)
     if save is None and _ATTN_EVAL_FUSED and N.lib.a2m_self_attention_eval_fits(C, T) and \
-            x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 and N.lib.a2m_get_gemm_precision() == 0:
+            x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 and \
+            N.lib.a2m_get_gemm_precision() in ((0, 1) if _ATTN_EVAL_BF16 else (0,)):
         # inference: q/k/v projections fused into the attention core, one launch
         N.check(N.lib.a2m_self_attention_eval_f32(_p(x), x.stride(0), B, C, T, _p(wqkv), _p(bqkv), _p(gamma),
                                                   _p(res), _p(out), out.stride(0), _stream()))

@@ -168,6 +168,24 @@ constexpr int FK = 32;        // projection k-tile (channels)
 constexpr int FKP = FK + 4;   // staged tile pitch
 constexpr int FCOLS = 128;    // projection output columns: Q 32 | K 32 | V 64
 
+// bf16 operand mode (precision 1): the projection's products on v_mfma_f32_32x32x16_bf16 --
+// each lane's 8 staged k of a 16-k half rounded to bf16 in registers (the fp32 fragment layout is
+// the bf16 MFMA's), one MFMA per half instead of eight -- as the engine's bf16 QKV GEMM rounds
+// them; scores, softmax and PV stay fp32 as in every mode.
+__device__ __forceinline__ bf16x8 attn_pack8(const float (&v)[8]) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  uint32_t u[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f2 p = {v[2 * j], v[2 * j + 1]};
+    u[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p, h2));
+  }
+  return __builtin_bit_cast(bf16x8, u4{u[0], u[1], u[2], u[3]});
+}
+
+template <bool BF16>
 __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
     const float* __restrict__ x, int64_t x_bs, int C, int T, const float* __restrict__ wqkv,
     const float* __restrict__ bqkv, const float* __restrict__ gamma, const float* __restrict__ res,
@@ -260,10 +278,29 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
     constexpr int Q = (decltype(par)::value + 1) & 1;
     float* const cur = lds + (i & 1) * STG;
     float* const nxt = lds + ((i + 1) & 1) * STG;
-    pipe_step(acc, fa0, fb0, cur + arow, cur + brow, nxt + arow, nxt + brow, [&](int s) {
-      if (s < 4) store_piece(nxt, rg[Q], s);
-      else if (s < 7) load_piece(rg[Q], s - 4);
-    });
+    if constexpr (BF16) {
+      // pipe_step's LDS protocol with one bf16 MFMA per half: tile i's second-half fragments,
+      // the first half's MFMA, tile i + 1's stores and tile i + 3's loads, the barrier, the second
+      // half's MFMA, tile i + 1's first-half fragments
+      float fa1[8], fb1[8];
+      pipe_frag(cur + arow + 16, fa1);
+      pipe_frag(cur + brow + 16, fb1);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(attn_pack8(fa0), attn_pack8(fb0), acc, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) store_piece(nxt, rg[Q], s);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) load_piece(rg[Q], s);
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(attn_pack8(fa1), attn_pack8(fb1), acc, 0, 0, 0);
+      pipe_frag(nxt + arow, fa0);
+      pipe_frag(nxt + brow, fb0);
+    } else {
+      pipe_step(acc, fa0, fb0, cur + arow, cur + brow, nxt + arow, nxt + brow, [&](int s) {
+        if (s < 4) store_piece(nxt, rg[Q], s);
+        else if (s < 7) load_piece(rg[Q], s - 4);
+      });
+    }
   };
   for (int kt = 0; kt < nk; kt += 2) {
     step(std::integral_constant<int, 0>(), kt);
@@ -603,8 +640,12 @@ int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const flo
                     const float* bqkv, const float* gamma, const float* res, float* y,
                     hipStream_t st, int G, int64_t x_gs, int64_t res_gs, int64_t y_gs) {
   dim3 grid((unsigned)cdiv(C, ACH), (unsigned)(B * G));
-  hipLaunchKernelGGL(attn_fused_eval_kernel, grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
-                     res, y, B, x_gs, res_gs, y_gs);
+  if (a2m_get_gemm_precision() == 1)
+    hipLaunchKernelGGL(attn_fused_eval_kernel<true>, grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
+                       res, y, B, x_gs, res_gs, y_gs);
+  else
+    hipLaunchKernelGGL(attn_fused_eval_kernel<false>, grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
+                       res, y, B, x_gs, res_gs, y_gs);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

@@ -314,6 +314,7 @@ struct GraphStack {
   const float* ln_w[GMAXL];
   const float* ln_b[GMAXL];
   float slope;
+  int bf16;   // 1: layer products with bf16 operands (precision 1)
 };
 
 // The k loop of one layer for a wave whose rows have at most DL gather slots (compile-time, so
@@ -436,6 +437,91 @@ __device__ __forceinline__ void stack_layer_k(const float* xs, const float (*al)
 #endif
 }
 
+// bf16 operand mode (a2m_set_gemm_precision(1), configs[4]): the layer products on
+// v_mfma_f32_32x32x16_bf16 -- the aggregated rows and the weights rounded to bf16 (RNE) in
+// registers, fp32 accumulation -- as torch.autocast runs the reference's GATConv / GraphConv
+// linears in bf16.  Per 16-k chunk each lane aggregates its row's 8 consecutive features (two
+// float4 gathers per neighbour, all heads at once) and issues one MFMA per (segment, t): 1/16 of
+// the fp32 k loop's matrix-pipe time.
+typedef __bf16 sbf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ sbf16x8 stack_pack8(const float (&v)[8]) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+  uint32_t u[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f2 p = {v[2 * j], v[2 * j + 1]};
+    u[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p, h2));
+  }
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(sbf16x8, u4{u[0], u[1], u[2], u[3]});
+}
+
+template <int DL, bool GAT>
+__device__ __forceinline__ void stack_layer_kh(const float* xs, const float (*al)[GMAXN], const int (&id)[GMAXDEG],
+                                               int node, int d0, const float* W0, const float* W1, int li,
+                                               int lh, floatx16 (&acc)[2]) {
+  constexpr int NS = GAT ? GHEADS : 1;
+  constexpr int NSEG = GAT ? GHEADS : 2;
+  float wq[NS][DL];
+  stack_edge_weights<DL, GAT>(al, id, node, d0, wq);
+#pragma unroll 1
+  for (int kc = 0; kc < GF / 16; ++kc) {
+    const int off = 16 * kc + 8 * lh;   // this lane's 8 consecutive k of the chunk
+    float a[NSEG][8];
+#pragma unroll
+    for (int h = 0; h < NSEG; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[h][e] = 0.f;
+#pragma unroll
+    for (int q = 0; q < DL; ++q) {
+      const float4 v0 = *reinterpret_cast<const float4*>(xs + id[q] * ZP + off);
+      const float4 v1 = *reinterpret_cast<const float4*>(xs + id[q] * ZP + off + 4);
+      const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int h = 0; h < NS; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[h][e] += wq[h][q] * v[e];
+    }
+    if (!GAT) {   // GraphConv's root term: the node's own features
+      const float4 o0 = *reinterpret_cast<const float4*>(xs + node * ZP + off);
+      const float4 o1 = *reinterpret_cast<const float4*>(xs + node * ZP + off + 4);
+      const float o[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[1][e] = o[e];
+    }
+#pragma unroll
+    for (int h = 0; h < NSEG; ++h) {
+      const sbf16x8 af = stack_pack8(a[h]);
+      const float* W = GAT ? W0 + h * GF * GF : (h == 0 ? W0 : W1);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float* wr = W + (t * 32 + li) * GF + off;
+        const float4 b0 = *reinterpret_cast<const float4*>(wr);
+        const float4 b1 = *reinterpret_cast<const float4*>(wr + 4);
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, stack_pack8(bv), acc[t], 0, 0, 0);
+      }
+    }
+  }
+}
+
+template <bool GAT>
+__device__ __forceinline__ void stack_layer_dispatch_h(int dl, const float* xs, const float (*al)[GMAXN],
+                                                       const int (&id)[GMAXDEG], int node, int d0, const float* W0,
+                                                       const float* W1, int li, int lh, floatx16 (&acc)[2]) {
+  switch (dl) {
+    case 1: stack_layer_kh<1, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 2: stack_layer_kh<2, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 3: stack_layer_kh<3, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 4: stack_layer_kh<4, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 5: stack_layer_kh<5, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 6: stack_layer_kh<6, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 7: stack_layer_kh<7, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    default: stack_layer_kh<8, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+  }
+}
+
 template <bool GAT>
 __device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, const float (*al)[GMAXN],
                                                      const int (&id)[GMAXDEG], int node, int d0, const float* W0,
@@ -452,7 +538,11 @@ __device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, co
   }
 }
 
-__global__ __launch_bounds__(256, STACK_WG_PER_CU) void graph_stack_kernel(
+#ifndef STACK_WG_PER_CU_BF16   // three workgroups per CU as the fp32 stack (hand 228.7 us alone
+#define STACK_WG_PER_CU_BF16 3   // against 250 us at two, where its registers need no spills)
+#endif
+template <bool BF16>
+__global__ __launch_bounds__(256, BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU) void graph_stack_kernel(
     const float* __restrict__ x, int F, int J, const int* __restrict__ nbr_ptr,
     const int* __restrict__ nbr_idx, GraphStack S, float* __restrict__ y) {
   __shared__ __attribute__((aligned(16))) float xs[GMAXN * ZP];        // node-indexed tile
@@ -573,8 +663,14 @@ __global__ __launch_bounds__(256, STACK_WG_PER_CU) void graph_stack_kernel(
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
     dl = __builtin_amdgcn_readfirstlane(dl);
-    if (gat) stack_layer_dispatch<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
-    else stack_layer_dispatch<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
+    if constexpr (BF16) {
+      if (gat) stack_layer_dispatch_h<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
+      else stack_layer_dispatch_h<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
+    } else if (gat) {
+      stack_layer_dispatch<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
+    } else {
+      stack_layer_dispatch<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
+    }
     // epilogue: out = LReLU(LN(acc * scale + bias)) + x, in place (or to y after the last layer).
     // The wave's 32 x 64 result goes through its private LDS scratch, 8 rows at a time (rows
     // 8p..8p+7 are exactly accumulator entries q = 4p..4p+3), so that each lane then owns 8
@@ -672,6 +768,9 @@ extern "C" int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, con
   GraphStack S{};
   S.nlayers = nlayers;
   S.slope = slope;
+  // bf16 operand mode: the layer products on the bf16 MFMA (A2M_STACK_BF16=0: the fp32 stack)
+  static const int stack_bf16 = std::getenv("A2M_STACK_BF16") ? std::atoi(std::getenv("A2M_STACK_BF16")) : 1;
+  S.bf16 = stack_bf16 && a2m_get_gemm_precision() == 1;
   for (int L = 0; L < nlayers; ++L) {
     A2M_CHECK_ARG(kinds[L] == 0 || kinds[L] == 1, "graph_stack: layer %d kind %d", L, kinds[L]);
     const bool has_w = w0[L] && (kinds[L] == 0 || w1[L]);
@@ -684,8 +783,12 @@ extern "C" int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, con
   }
   if (F == 0) return A2M_OK;
   const int fpb = GMAXN / J;
-  hipLaunchKernelGGL(graph_stack_kernel, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
-                     x, F, J, nbr_ptr, nbr_idx, S, y);
+  if (S.bf16)
+    hipLaunchKernelGGL(graph_stack_kernel<true>, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
+                       x, F, J, nbr_ptr, nbr_idx, S, y);
+  else
+    hipLaunchKernelGGL(graph_stack_kernel<false>, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
+                       x, F, J, nbr_ptr, nbr_idx, S, y);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

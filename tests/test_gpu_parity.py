@@ -416,6 +416,49 @@ def test_graph_stack_vs_oracle(part, J, lo):
     assert e < TOL, e
 
 
+@pytest.mark.parametrize('part,J,lo', [('body', 10, 0), ('hand', 42, 10)])
+def test_graph_stack_bf16_mode(part, J, lo):
+    """The stack in bf16 operand mode (configs[4]: the layer products on the bf16 MFMA, as
+    torch.autocast runs GATConv / GraphConv's linears in bf16) against the fp32 oracle at a
+    bf16-level tolerance, and against the fp32 kernel."""
+    import a2m
+    from a2m import functional as F
+    from a2m import skeleton as S
+    from oracle import model as OM
+    Fr = 29
+    x = _rand(Fr * J, 64, seed=80)
+    ei = S.edge_index(lo, J)
+    edges = OM.expand_edges(ei, J, Fr)
+    ptr, idx = S.in_neighbour_csr(ei, J)
+    dv = lambda t: t.to(DEV)  # noqa: E731
+    ref, layers = x, []
+    for L in range(5):
+        lnw, lnb = _rand(64, seed=90 + L).abs() + .5, _rand(64, seed=95 + L, scale=0.1)
+        if L % 2 == 0:
+            lw, asrc, adst, bias = _rand(256, 64, seed=100 + L, scale=0.15), \
+                _rand(1, 4, 64, seed=110 + L, scale=0.3), _rand(1, 4, 64, seed=120 + L, scale=0.3), \
+                _rand(64, seed=130 + L, scale=0.1)
+            g = OM._gat_fn(ref, edges, lw, asrc, adst, bias, 4)
+            U = F.graph_att_proj(dv(lw), dv(asrc), dv(adst))
+            layers.append((0, dv(lw), None, U, dv(bias), dv(lnw), dv(lnb)))
+        else:
+            wr, br, wo = _rand(64, 64, seed=140 + L, scale=0.12), _rand(64, seed=150 + L, scale=0.1), \
+                _rand(64, 64, seed=160 + L, scale=0.12)
+            g = OM.graph_conv(OM.Ctx({'g.lin_rel.weight': wr, 'g.lin_rel.bias': br,
+                                      'g.lin_root.weight': wo}), 'g', ref, edges)
+            layers.append((1, dv(wr), dv(wo), None, dv(br), dv(lnw), dv(lnb)))
+        ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(g, (64,), lnw, lnb), 0.2) + ref
+    out32 = F.graph_stack(dv(x), J, dv(ptr), dv(idx), layers).cpu()
+    prev = a2m.set_gemm_precision('bf16')
+    try:
+        out16 = F.graph_stack(dv(x), J, dv(ptr), dv(idx), layers).cpu()
+    finally:
+        a2m.set_gemm_precision(prev)
+    e16, e32 = rel_err(out16, ref), rel_err(out32, ref)
+    print(f'{part}: bf16 stack vs oracle {e16:.2e}, fp32 stack {e32:.2e}')
+    assert e32 < TOL and 1e-6 < e16 < 3e-2, (e16, e32)
+
+
 def test_pose_losses_vs_reference():
     from a2m import functional as F
     z = golden('losses.npz')

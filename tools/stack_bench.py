@@ -1,7 +1,7 @@
 """Times the fused eval graph stack (a2m_graph_stack_fwd_f32: GAT, GraphConv, GAT, GraphConv,
 GAT) at the bench shapes: hand (J=42) and body (J=10) over B*T = 4096 frames, each alone on the
 chip.
-    python tools/stack_bench.py [hand|body] [iters]"""
+    python tools/stack_bench.py [hand|body|both] [iters] [bf16]"""
 import os
 import sys
 
@@ -14,8 +14,12 @@ from a2m import skeleton as S  # noqa: E402
 
 dev = torch.device('cuda')
 FR = 4096
-which = sys.argv[1] if len(sys.argv) > 1 else 'both'
-iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+argv = [a for a in sys.argv[1:] if a != 'bf16']
+if 'bf16' in sys.argv[1:]:   # the bf16 operand mode's stack (layer products on the bf16 MFMA)
+    import a2m
+    a2m.set_gemm_precision('bf16')
+which = argv[0] if len(argv) > 0 else 'both'
+iters = int(argv[1]) if len(argv) > 1 else 20
 g = torch.Generator(device='cpu').manual_seed(0)
 
 
