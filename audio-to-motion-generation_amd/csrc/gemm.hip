@@ -379,8 +379,10 @@ static const PlanRule* tuned_plan(int M, int N, int K, int prec) {
 static double bf16_thr(int tile, int c) {
   static const std::vector<double> t = [] {
     // fitted in the replayed bf16 bench step (r05 sweeps, two interleaved rounds each: 1.658 ms
-    // against 1.831 ms with round 4's 4 x the f32 table, {1360, 1712, 1740, 1760, 1856, 2000}e3)
-    std::vector<double> v = {530e3, 750e3, 900e3, 1060e3, 1500e3, 2000e3};
+    // against 1.831 ms with round 4's 4 x the f32 table, {1360, 1712, 1740, 1760, 1856, 2000}e3,
+    // at {530, 750, 900, 1060, 1500, 2000}e3; refitted with the bf16 pipelined tile, whose 64x64
+    // launches run faster: 1.416-1.422 ms against 1.447-1.449)
+    std::vector<double> v = {600e3, 850e3, 1000e3, 1150e3, 1500e3, 2000e3};
     if (const char* e = std::getenv("A2M_GEMM_BF16_THR")) {
       double x[6];
       const int n = std::sscanf(e, "%lf,%lf,%lf,%lf,%lf,%lf", &x[0], &x[1], &x[2], &x[3], &x[4], &x[5]);

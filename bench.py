@@ -498,7 +498,7 @@ def mfma_peak(dtype):
 
 def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
     """`roofline` for the dominant family, the implicit-GEMM engine: every tile-kernel launch
-    (gemm_kernel / gemm_pipe_kernel) AND every split-K reduce of one step.  `achieved` =
+    (gemm_kernel / gemm_pipe_kernel / gemm_pipe_bf16_kernel) AND every split-K reduce of one step.  `achieved` =
     algorithmic FLOPs per step (2*M*N*K summed over the step's engine launches) / the family's
     summed kernel-trace durations per step (`traced_family`: rocprofv3 --kernel-trace of the
     replayed bench graph, the figure a kernel-trace breakdown gives); without a trace, the span
@@ -527,7 +527,7 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
                  'tile kernel and split-K reduce in the replayed step graph, plus the measured per-launch '
                  'dispatch overhead')
     return {'bound': 'mfma',
-            'kernel': 'implicit-GEMM engine family (gemm_kernel, gemm_pipe_kernel, splitk_reduce*): every launch of one step',
+            'kernel': 'implicit-GEMM engine family (gemm_kernel, gemm_pipe_kernel, gemm_pipe_bf16_kernel, splitk_reduce*): every launch of one step',
             'achieved': round(tf, 2), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(tf / peak, 4),
             'traffic': traffic['bytes_per_launch'] if traffic else None,
@@ -550,7 +550,7 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
                                  'ms_per_step': round(gt.ms_tile + gt.ms_reduce, 4)}}
 
 
-GEMM_FAMILY = ('gemm_kernel', 'gemm_pipe_kernel', 'splitk_reduce')   # the engine's kernels
+GEMM_FAMILY = ('gemm_kernel', 'gemm_pipe_kernel', 'gemm_pipe_bf16_kernel', 'splitk_reduce')   # the engine's kernels
 
 
 def trace_child(args):
@@ -637,7 +637,7 @@ def traced_family(args, flops_per_step, reps=10, keep_dir=None):
         tot = sum(v[1] for v in agg.values()) / reps
         lines = [f'{len(rows)} dispatches after the marker = {reps} replayed steps (device sync after each); '
                  f'kernel-time sum {tot:.1f} us/step',
-                 f'engine family (gemm_kernel + gemm_pipe_kernel + splitk_reduce*): {len(fam) / reps:.1f} launches/step, '
+                 f'engine family (gemm_kernel + gemm_pipe_kernel / gemm_pipe_bf16_kernel + splitk_reduce*): {len(fam) / reps:.1f} launches/step, '
                  f'{fam_us:.1f} us/step ({red_us:.1f} us of split-K reduces)',
                  f'engine roofline: {flops_per_step / 1e9:.1f} GFLOP / {fam_us:.1f} us = '
                  f'{flops_per_step / (fam_us * 1e-6) / 1e12:.1f} TF']

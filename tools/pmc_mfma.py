@@ -18,7 +18,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from replay_filter import load, replayed  # noqa: E402
 
-FAMILIES = ('gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel', 'graph_stack_kernel', 'logmel2048_kernel', 'graph_layer_kernel',
+FAMILIES = ('gemm_pipe_bf16_kernel', 'gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel', 'graph_stack_kernel', 'logmel2048_kernel', 'graph_layer_kernel',
             'attn_fused_eval_kernel', 'attn_core', 'im2col', 'channel_att', 'layernorm_kernel')
 
 
@@ -53,7 +53,7 @@ def main():
                   'busy_frac': busy / (1024.0 * cyc) if cyc else None,
                   'trace_avg_us': dur[f][1] / max(dur[f][0], 1) / 1e3 if f in dur else None}
     # the GEMM engine as one family (bench.py's roofline): both tile kernels and the split-K reduces
-    eng = [f for f in ('gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel') if f in per]
+    eng = [f for f in ('gemm_pipe_bf16_kernel', 'gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel') if f in per]
     if eng:
         cyc = sum(per[f].get('GRBM_GUI_ACTIVE', 0.0) for f in eng) / 8.0
         busy = sum(per[f].get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0) for f in eng)

@@ -21,7 +21,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from replay_filter import load, replayed  # noqa: E402
 
-FAMILIES = ('gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'logmel_kernel',
+FAMILIES = ('gemm_pipe_bf16_kernel', 'gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel', 'logmel2048_kernel', 'logmel_kernel',
             'graph_stack_kernel', 'graph_layer_kernel', 'graph_att_proj_kernel', 'attn_fused_eval_kernel',
             'attn_core_wide_kernel', 'conv2d_c1_kernel', 'im2col2d_kernel', 'im2col1d_kernel',
             'channel_attention_kernel', 'softmax_rows_kernel', 'layernorm_kernel')
@@ -69,7 +69,7 @@ def main():
                     'source': f'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes {a.tag}, replayed steps only; FETCH x2 (gfx950), KB x1024'}
     # the implicit-GEMM engine as one family (bench.py's roofline): tile kernels of both kinds and
     # every split-K reduce; bytes per step over the replayed steps, and per tile launch
-    eng = [f for f in ('gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel') if f in out]
+    eng = [f for f in ('gemm_pipe_bf16_kernel', 'gemm_pipe_kernel', 'gemm_kernel', 'splitk_reduce_kernel') if f in out]
     if eng:
         steps = a.steps
         rd = sum(out[f]['read_bytes_per_launch'] * out[f]['dispatches'][0] for f in eng)

@@ -38,7 +38,7 @@ def main():
     lines = [f'{len(rows)} dispatches after the marker = {n} replayed steps; first-to-last span '
              f'{span / n:.1f} us/step; kernel-time sum {tot / n:.1f} us/step']
     def engine(k):
-        return 'gemm_kernel' in k or 'gemm_pipe_kernel' in k or 'splitk_reduce' in k
+        return 'gemm_kernel' in k or 'gemm_pipe' in k or 'splitk_reduce' in k
     gemm = sum(v[1] for k, v in agg.items() if engine(k)) / n
     gcalls = sum(v[0] for k, v in agg.items() if engine(k)) / n
     lines.append(f'GEMM engine (gemm_kernel + gemm_pipe_kernel + splitk_reduce): {gcalls:.1f} launches/step, {gemm:.1f} us/step')
