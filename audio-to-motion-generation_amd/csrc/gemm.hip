@@ -653,6 +653,10 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                          (mb == 0 || (mb == 6 && B.nhwc % 64 == 0) || rows3 ||
                           (mb == 5 && B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 && 64 % B.R2 == 0)) &&
                          pipe_ext;
+  // ... and its halo layout for the 3-tap pad-1 convs over clips of T >= 16 (the window stored
+  // once per chunk instead of once per tap); gemm_tile's bf16 tile takes the per-tap stores
+  if (pipe_bf16 && halo_on && mb == 5 && B.tapconv == 3 && B.cw == -1 && B.R2 >= 16 && 64 % B.R2 == 0)
+    a.B.halo = 1;
   if (p.splits > 1 || interp) {
     const size_t need = split_ws_bytes(p, M, N, batch);
     if (ws == nullptr || ws_bytes < need) {

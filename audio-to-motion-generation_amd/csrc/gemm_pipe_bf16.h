@@ -229,6 +229,52 @@ struct PipeTapH {
   }
 };
 
+// tap-chunked conv1d in the halo layout (mode 5, Gather::halo: 3 taps, pad 1, clips T >= 16 that
+// tile the 64 rows; PipeHalo's bf16 twin): the chunk's 64-channel x window is loaded and stored
+// ONCE (k-pair map), row n of the tile at halo row (n / T) (T + 2) + 1 + n % T of a chunk-parity
+// stage whose rows before and after each clip are zero; tap j reads it shifted by j - 1 rows
+struct PipeHaloH {
+  static constexpr int HR = 64 + 2 * 4;   // halo stage rows (at most four clips)
+  static constexpr int NST = 2;
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t off;      // byte offset of x[b][next chunk * 64 + kp][t] (kPipeOOB: rows invalid)
+  int kp, lrow, ch, Ci, sk0;
+  int h5[4];         // half offsets of the thread's 4 rows in a halo stage
+  __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
+    rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
+    lrow = (tid >> 4) * 4;
+    kp = (tid & 15) * 2;
+    const int T = g.R2;
+    const int n = row0 + lrow;
+    const int b = n / T, tt = n - b * T;
+    Ci = KK / 3;
+    sk0 = g.sk0;
+    ch = (kbeg / 192) * 64 + kp;
+    off = n < R ? (uint32_t)(b * g.sr0 + tt + ch * sk0) * 4u : kPipeOOB;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int nn = lrow + e;
+      h5[e] = ((nn / T) * (T + 2) + 1 + nn % T) * kHK + kp;
+    }
+  }
+  __device__ __forceinline__ void load(float4 (&r)[4], int p) {
+    const int dk = (p & 1) + 32 * (p >> 1);
+    r[p] = pipe_load(rs, ch + dk < Ci ? off + 4u * dk * sk0 : kPipeOOB);
+    if (p == 3) {
+      ch += 64;
+      off += 4u * 64 * sk0;
+    }
+  }
+  // k pair kp + 32 s of the window's 4 rows
+  __device__ __forceinline__ void store(float* st, const float4 (&r)[4], int s) const {
+    uint32_t* w = reinterpret_cast<uint32_t*>(st);
+    w[(h5[0] + 32 * s) >> 1] = hpack2(r[2 * s].x, r[2 * s + 1].x);
+    w[(h5[1] + 32 * s) >> 1] = hpack2(r[2 * s].y, r[2 * s + 1].y);
+    w[(h5[2] + 32 * s) >> 1] = hpack2(r[2 * s].z, r[2 * s + 1].z);
+    w[(h5[3] + 32 * s) >> 1] = hpack2(r[2 * s].w, r[2 * s + 1].w);
+  }
+};
+
 // One 64-k step.  ca / cb: this lane's fragment rows of tile i (A, B), na / nb: those of tile
 // i + 1 (halves).  fa0 / fb0 hold tile i's K16 chunks 0-1 on entry and tile i + 1's on exit.
 // work(HS<s>), s = 0..15: 0-7 behind the first two MFMAs (the stores of tile i + 1: they must
@@ -267,8 +313,11 @@ template <int MB, int NT = 0>   // MB 5: NT = taps (1-3)
 __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
   span_begin(args.ts);
   constexpr int BM = 64;
-  constexpr bool TAPS = MB == 5;
-  __shared__ __attribute__((aligned(16))) float lds[4 * kHStage];   // A stages, then B stages
+  constexpr bool HALO = MB == 5 && NT == 0;
+  constexpr bool TAPS = MB == 5 && NT > 0;
+  constexpr int TBH = PipeHaloH::HR * kHK / 2;   // a halo B stage, in floats
+  constexpr int TB = HALO ? TBH : kHStage;
+  __shared__ __attribute__((aligned(16))) float lds[2 * kHStage + 2 * TB];   // A stages, then B stages
   __shared__ EpiRow epr[BM];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -286,7 +335,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
   PipeRowsH la;
   la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
   using LB = typename std::conditional<
-      TAPS, PipeTapH<NT ? NT : 1>,
+      MB == 5, typename std::conditional<TAPS, PipeTapH<NT ? NT : 1>, PipeHaloH>::type,
       typename std::conditional<MB == 6, PipeNhwcH,
                                 typename std::conditional<MB == 3, PipeRowsTH, PipeRowsH>::type>::type>::type;
   LB lb;
@@ -356,6 +405,74 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
       if constexpr (NT > 2) tap_step(std::integral_constant<int, 2>());
     };
     const int nch = nk / NT;
+    int cc = 0;
+    for (; cc + 1 < nch; cc += 2) {
+      chunk(P0(), cc);
+      chunk(P1(), cc + 1);
+    }
+    if (cc < nch) chunk(P0(), cc);
+  } else if constexpr (HALO) {
+    // A in k-tile parity stages, B in chunk parity stages (one per 3 k-tiles); the next chunk's
+    // x window is loaded at the chunk's tap 0 and stored at its tap 2 (gemm_pipe.h's schedule)
+    const int T = args.B.R2;
+    for (int idx = tid; idx < 2 * (64 / T) * 2 * (kHK / 2); idx += 256) {   // zero rows around each clip
+      const int col = idx % (kHK / 2), q = idx / (kHK / 2);
+      const int which = q & 1, clip = (q >> 1) % (64 / T), stage = (q >> 1) / (64 / T);
+      Bs[stage * TB + (clip * (T + 2) + (which ? T + 1 : 0)) * (kHK / 2) + col] = 0.f;
+    }
+    const int bsh = 2 * ((wn * 32 + li) / T) + 1;                   // halo rows above this lane's B row
+    const int hrow = (wn * 32 + li + bsh) * kHK + lh * 8;           // tap 1 (shift 0), halves
+    float4 rx[4];                                                   // a chunk's x window
+    load4(la, ra[0]);
+    load4(lb, rx);
+    epi_consts();
+    load4(la, ra[1]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) la.store(As, ra[0], s);
+    lb.store(Bs, rx, 0); lb.store(Bs, rx, 1);
+    load4(la, ra[0]);
+    __syncthreads();
+    fa0[0] = hld(H(As) + arow); fa0[1] = hld(H(As) + arow + 16);
+    fb0[0] = hld(H(Bs) + hrow - kHK); fb0[1] = hld(H(Bs) + hrow - kHK + 16);   // tile 0 = tap 0
+    const int nch = nk / 3;
+    // chunk cc (parity P): tap j stores A(3 cc + j + 1) from set (P + j + 1) & 1 and loads
+    // A(3 cc + j + 3) into it
+    auto chunk = [&](auto par, int cc) {
+      constexpr int P = decltype(par)::value;
+      constexpr int Q0 = (P + 1) & 1, Q1 = P, Q2 = (P + 1) & 1;
+      const int i0 = 3 * cc;
+      float* const bc = Bs + (cc & 1) * TB;          // this chunk's B stage
+      float* const bn = Bs + ((cc & 1) ^ 1) * TB;    // the next chunk's
+      {   // tap 0 (+ the next chunk's x window loads)
+        const int c = (i0 & 1) * kHStage, n = kHStage - c;
+        float* const nA = As + n;
+        pipe_step_h(acc, fa0, fb0, H(As + c) + arow, H(bc) + hrow - kHK, H(nA) + arow, H(bc) + hrow, [&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          if constexpr (s < 4) la.store(nA, ra[Q0], s);
+          else if constexpr (s >= 8 && s < 12) la.load(ra[Q0], s - 8);
+          else if constexpr (s >= 12) lb.load(rx, s - 12);
+        });
+      }
+      {   // tap 1
+        const int c = ((i0 + 1) & 1) * kHStage, n = kHStage - c;
+        float* const nA = As + n;
+        pipe_step_h(acc, fa0, fb0, H(As + c) + arow, H(bc) + hrow, H(nA) + arow, H(bc) + hrow + kHK, [&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          if constexpr (s < 4) la.store(nA, ra[Q1], s);
+          else if constexpr (s >= 8 && s < 12) la.load(ra[Q1], s - 8);
+        });
+      }
+      {   // tap 2 (+ the next chunk's x window stores)
+        const int c = ((i0 + 2) & 1) * kHStage, n = kHStage - c;
+        float* const nA = As + n;
+        pipe_step_h(acc, fa0, fb0, H(As + c) + arow, H(bc) + hrow + kHK, H(nA) + arow, H(bn) + hrow - kHK, [&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          if constexpr (s < 4) la.store(nA, ra[Q2], s);
+          else if constexpr (s < 6) lb.store(bn, rx, s - 4);
+          else if constexpr (s >= 8 && s < 12) la.load(ra[Q2], s - 8);
+        });
+      }
+    };
     int cc = 0;
     for (; cc + 1 < nch; cc += 2) {
       chunk(P0(), cc);
