@@ -53,6 +53,40 @@ def test_bf16_conv1d_gathered_operands(Ci, Co, T, k, s, p):
     assert rel_err(y.cpu().double(), ref) < 1e-5
 
 
+@pytest.mark.parametrize('C,T,res', [(256, 64, True), (128, 48, False)])
+def test_bf16_fused_eval_attention_exact_on_bf16_operands(C, T, res):
+    """The fused eval attention in bf16 mode (its QKV projection on the bf16 MFMA) on x and
+    weights that are already bf16 values: against an fp64 SelfAttention of the same values
+    (scores, softmax and PV are fp32 in every mode), and against the engine's bf16 QKV GEMM +
+    attention core path (A2M_ATTN_EVAL_BF16=0's route)."""
+    import a2m
+    from a2m import functional as F
+    g = torch.Generator().manual_seed(C + T)
+    B = 6
+    x = _r16(torch.randn(B, C, T, generator=g))
+    ws = [_r16(torch.randn(o, C, generator=g) * C ** -0.5) for o in (C // 8, C // 8, C)]
+    bs = [torch.randn(o, generator=g) * 0.1 for o in (C // 8, C // 8, C)]
+    gamma = torch.tensor([0.7])
+    r = torch.randn(B, C, T, generator=g) if res else None
+    q = torch.einsum('oc,bct->bot', ws[0].double(), x.double()) + bs[0].double()[:, None]
+    k = torch.einsum('oc,bct->bot', ws[1].double(), x.double()) + bs[1].double()[:, None]
+    v = torch.einsum('oc,bct->bot', ws[2].double(), x.double()) + bs[2].double()[:, None]
+    att = torch.softmax(torch.einsum('bci,bcj->bij', q, k), dim=-1)
+    ref = 0.7 * torch.einsum('bcj,bij->bci', v, att) + x.double() + (r.double() if res else 0.0)
+    dv = lambda t: None if t is None else t.to(DEV)  # noqa: E731
+    args = [dv(ws[0]), dv(bs[0]), dv(ws[1]), dv(bs[1]), dv(ws[2]), dv(bs[2]), dv(gamma)]
+    with a2m.gemm_precision('bf16'):
+        fused = F.self_attention(dv(x), *args, res=dv(r), cache={}).cpu()
+        prev = F._ATTN_EVAL_BF16
+        F._ATTN_EVAL_BF16 = False
+        try:
+            packed = F.self_attention(dv(x), *args, res=dv(r), cache={}).cpu()
+        finally:
+            F._ATTN_EVAL_BF16 = prev
+    assert rel_err(fused.double(), ref) < 1e-5, rel_err(fused.double(), ref)
+    assert rel_err(fused, packed) < 1e-5, rel_err(fused, packed)
+
+
 def test_bf16_generator_eval_close_to_fp32(g_state):
     """G eval (B=2, T=64 fixture) with bf16 GEMM operands vs the reference's fp32 output.
     Measured bound: bf16 rounding (2^-9 relative per operand) through the 40-odd GEMMs of G."""
