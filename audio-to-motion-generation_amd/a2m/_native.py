@@ -106,6 +106,8 @@ SIGNATURES = {
                                                      SZ, P]),
     'a2m_graph_layer_bwd_f32': (ctypes.c_int, [P, P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32, P, P,
                                                P, P, P, P, P, P, P, SZ, P]),
+    'a2m_graph_layer_bwd_saved_f32': (ctypes.c_int, [P, P, P, I32, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32,
+                                                     P, P, P, P, P, P, P, P, P, SZ, P]),
     'a2m_interp_time_bwd_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, I32, P]),
     'a2m_pose_losses_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, P, P, P, SZ, P]),
     'a2m_pose_losses_w_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, F32, F32, P, P, P, SZ, P]),

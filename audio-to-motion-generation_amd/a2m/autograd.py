@@ -11,6 +11,8 @@ from a2m.autograd.next_seed() (seeded from torch.initial_seed(), or manual_seed(
 BatchNorm in eval mode with gradients enabled normalises with the running statistics (fixed in
 the backward), as nn.BatchNorm*d.eval() does.
 """
+import os
+
 import torch
 
 from . import functional as F
@@ -283,23 +285,30 @@ class _LayerNormBCT(torch.autograd.Function):
         return dx, dw, db, None
 
 
+# A2M_GRAPH_SAVE_PRE=0: the graph-layer backward recomputes the pre-LayerNorm output instead of
+# reading the forward's copy (one [nodes][64] tensor per layer kept for the backward)
+_GRAPH_SAVE_PRE = os.environ.get('A2M_GRAPH_SAVE_PRE', '1') != '0'
+
+
 class _GraphLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w0, w1, att_src, att_dst, bias, ln_w, ln_b, topo):
         J, kind, ptr, idx, norm_res = topo
-        y = F.graph_layer(x.contiguous(), J, kind, ptr, idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
-                          norm_res=norm_res)
-        ctx.save_for_backward(x, w0, w1, att_src, att_dst, bias, ln_w, ln_b)
+        x = x.contiguous()
+        pre = torch.empty_like(x) if norm_res and _GRAPH_SAVE_PRE else None
+        y = F.graph_layer(x, J, kind, ptr, idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
+                          norm_res=norm_res, pre_ln=pre)
+        ctx.save_for_backward(x, w0, w1, att_src, att_dst, bias, ln_w, ln_b, pre)
         ctx.topo = topo
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w0, w1, att_src, att_dst, bias, ln_w, ln_b = ctx.saved_tensors
+        x, w0, w1, att_src, att_dst, bias, ln_w, ln_b, pre = ctx.saved_tensors
         J, kind, ptr, idx, norm_res = ctx.topo
         dx, dw0, dw1, das, dad, dbias, dlw, dlb = F.graph_layer_bwd(
-            x.contiguous(), dy, J, kind, ptr, idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
-            norm_res=norm_res)
+            x, dy, J, kind, ptr, idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
+            norm_res=norm_res, pre_ln=pre)
         return dx, dw0, dw1, das, dad, dbias, dlw, dlb, None
 
 

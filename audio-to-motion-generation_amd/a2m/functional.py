@@ -847,8 +847,10 @@ def channel_attention_bwd(dy, x, w1, b1, w2, b2):
 
 
 def graph_layer_bwd(x, dy, J, kind, nbr_ptr, nbr_idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
-                    slope=0.2, norm_res=True):
-    _check_dev(x, dy)
+                    slope=0.2, norm_res=True, pre_ln=None):
+    """pre_ln: the forward's saved pre-LayerNorm output (graph_layer(..., pre_ln=)); None = the
+    backward recomputes it."""
+    _check_dev(x, dy, pre_ln)
     dy = dy.contiguous()
     F = x.shape[0] // J
     dx = torch.empty_like(x)
@@ -859,8 +861,8 @@ def graph_layer_bwd(x, dy, J, kind, nbr_ptr, nbr_idx, w0, w1, att_src, att_dst, 
     dbias = torch.empty_like(bias)
     dlw = torch.empty_like(ln_w) if norm_res else None
     dlb = torch.empty_like(ln_b) if norm_res else None
-    _with_ws(x.device, lambda wp, wn: N.lib.a2m_graph_layer_bwd_f32(
-        _p(x), _p(dy), F, J, kind, int(norm_res), _p(nbr_ptr), _p(nbr_idx), _p(w0), _p(w1), _p(att_src),
+    _with_ws(x.device, lambda wp, wn: N.lib.a2m_graph_layer_bwd_saved_f32(
+        _p(x), _p(dy), _p(pre_ln), F, J, kind, int(norm_res), _p(nbr_ptr), _p(nbr_idx), _p(w0), _p(w1), _p(att_src),
         _p(att_dst), _p(bias), _p(ln_w), _p(ln_b), slope, _p(dx), _p(dw0), _p(dw1), _p(das), _p(dad),
         _p(dbias), _p(dlw), _p(dlb), wp, wn, _stream()))
     return dx, dw0, dw1, das, dad, dbias, dlw, dlb

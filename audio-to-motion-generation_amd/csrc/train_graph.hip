@@ -33,6 +33,20 @@ constexpr int BNT = 512, BRG = BNT / 16, BRPT = BMAXN / BRG;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+// A2M_GBWD_STAMPS (diagnostic build, tools/build_variant.sh): thread 0 of every workgroup stamps
+// the wall clock after each phase's barrier (tools/graph_bwd_phases.py reads them back)
+#ifdef A2M_GBWD_STAMPS
+constexpr int kGbStamps = 32, kGbBlocks = 4096;
+__device__ unsigned long long g_gb_stamps[kGbBlocks * kGbStamps];
+#define GB_STAMP(i)                                                              \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < kGbBlocks)                              \
+      g_gb_stamps[blockIdx.x * kGbStamps + (i)] = (unsigned long long)wall_clock64(); \
+  } while (0)
+#else
+#define GB_STAMP(i) do {} while (0)
+#endif
+
 // acc += A[rows][64] (LDS, pitch BZP) . W^T over output columns c0 + (0..31), where
 // B(n=j, k=c) = Wt(j, c) given by functor
 template <class WF>
@@ -67,8 +81,8 @@ __device__ __forceinline__ void zero_acc(floatx16& acc) {
 }
 
 __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
-    const float* __restrict__ x, const float* __restrict__ dy, int F, int J, int kind, int norm_res,
-    const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_idx, const float* __restrict__ w0,
+    const float* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ pre_ln, int F,
+    int J, int kind, int norm_res, const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_idx, const float* __restrict__ w0,
     const float* __restrict__ w1, const float* __restrict__ Ug, const float* __restrict__ bias,
     const float* __restrict__ ln_w, const float* __restrict__ ln_b, float slope,
     float* __restrict__ dx, float* __restrict__ ybuf, float* __restrict__ dout,
@@ -96,21 +110,36 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
   const int rblk = wave & 3, c0 = (wave >> 2) * 32;   // MFMA rows / columns of this wave
   const int arow = rblk * 32 + li;
   const int ywidth = kind == 0 ? BH * BF : BF;
+  GB_STAMP(0);
 
-  {  // node tile: all loads of this thread in flight before the LDS writes
+  // the forward's saved pre-LayerNorm output o (bias included) replaces the recompute
+  const bool saved = pre_ln != nullptr;
+  const bool load_o = saved && norm_res;
+  {  // node tile (and o): all loads of this thread in flight before the LDS writes
     constexpr int NL = BMAXN * (BF / 4) / BNT;
-    float4 v[NL];
+    float4 v[NL], u[NL];
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int i = tid + j * BNT, n = i / (BF / 4), q = i % (BF / 4);
       v[j] = n < NB ? *reinterpret_cast<const float4*>(x + (node0 + n) * BF + q * 4)
                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      u[j] = load_o && n < NB ? *reinterpret_cast<const float4*>(pre_ln + (node0 + n) * BF + q * 4)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       const int i = tid + j * BNT, n = i / (BF / 4), q = i % (BF / 4);
       *reinterpret_cast<float4*>(xs + n * BZP + q * 4) = v[j];
+      if (load_o) *reinterpret_cast<float4*>(bufA + n * BZP + q * 4) = u[j];
     }
+  }
+  // this thread's rows of dy, in flight across the prologue / recompute
+  float4 dyr[BRPT];
+#pragma unroll
+  for (int r = 0; r < BRPT; ++r) {
+    const int n = nr0 + BRG * r;
+    dyr[r] = n < NB ? *reinterpret_cast<const float4*>(dy + (node0 + n) * BF + cg * 4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (kind == 0)
     for (int i = tid; i < 2 * BH * BF; i += blockDim.x) (&U[0][0])[i] = Ug[i];
@@ -125,6 +154,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
     ndeg[n] = d;
   }
   __syncthreads();
+  GB_STAMP(1);
   if (kind == 0) {
     // reverse-edge slots, once per block (the per-head adjoint loops index them directly
     // instead of searching the neighbour list of every neighbour)
@@ -147,6 +177,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
       al[n][q] = s;
     }
     __syncthreads();
+    GB_STAMP(2);
   }
 
   auto edge_softmax = [&](int h) {
@@ -173,9 +204,10 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
   };
 
   // ---------------------------------------------------------------- forward recompute
+  // (without the saved o: Y_h / agg -> ybuf for the weight gradients, o -> bufA)
   floatx16 acc;
   zero_acc(acc);
-  const int nseg = kind == 0 ? BH : 2;
+  const int nseg = saved ? 0 : (kind == 0 ? BH : 2);
   for (int seg = 0; seg < nseg; ++seg) {
     const float* Wseg = kind == 0 ? w0 + (int64_t)seg * BF * BF : (seg == 0 ? w0 : w1);
     const float* A = bufA;
@@ -207,8 +239,11 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
     mfma_rows64(acc, A, arow, c0, lh, li, [&](int j, int c) { return Wseg[j * BF + c]; });
     __syncthreads();
   }
-  acc_to_lds(acc, bufA, rblk, c0, lh, li, kind == 0 ? 1.f / BH : 1.f);  // o (bias added below)
-  __syncthreads();
+  if (!saved) {
+    acc_to_lds(acc, bufA, rblk, c0, lh, li, kind == 0 ? 1.f / BH : 1.f);  // o (bias added below)
+    __syncthreads();
+  }
+  GB_STAMP(3);
 
   // ---------------------------------------------------------------- LN / act / residual bwd
   float dxa[BRPT][4];
@@ -218,11 +253,9 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
   for (int r = 0; r < BRPT; ++r) {
     const int n = nr0 + BRG * r;
     float o[4], g4[4];
-    const float4 dy4 = n < NB ? *reinterpret_cast<const float4*>(dy + (node0 + n) * BF + cg * 4)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float dyv[4] = {dy4.x, dy4.y, dy4.z, dy4.w};
+    const float dyv[4] = {dyr[r].x, dyr[r].y, dyr[r].z, dyr[r].w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = bufA[n * BZP + cg * 4 + q] + bias[cg * 4 + q];
+    for (int q = 0; q < 4; ++q) o[q] = saved ? bufA[n * BZP + cg * 4 + q] : bufA[n * BZP + cg * 4 + q] + bias[cg * 4 + q];
     float dov[4];
     if (norm_res) {
       float s = o[0] + o[1] + o[2] + o[3];
@@ -264,11 +297,12 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) pb[q] += dov[q];
     *reinterpret_cast<float4*>(bufB + n * BZP + cg * 4) = make_float4(dov[0], dov[1], dov[2], dov[3]);
-    if (n < NB)
+    if (n < NB && dout)
       *reinterpret_cast<float4*>(dout + (node0 + n) * BF + cg * 4) =
           make_float4(dov[0] * oscale, dov[1] * oscale, dov[2] * oscale, dov[3] * oscale);
   }
   __syncthreads();
+  GB_STAMP(4);
 
   float dU = 0.f;  // per-thread item tid of the dU partial [8][64]
   if (kind == 0) {
@@ -280,6 +314,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
       mfma_rows64(acc, bufB, arow, c0, lh, li, [&](int j, int c) { return Wh[c * BF + j]; });
       acc_to_lds(acc, bufA, rblk, c0, lh, li, 1.f / BH);
       __syncthreads();
+      GB_STAMP(5 + 5 * h + 0);
       // dalpha[n][q] = dY_h[n] . x[nbl[n][q]]  (16 lanes per node)
       for (int i = tid; i < BMAXN * 16; i += blockDim.x) {
         const int n = i >> 4, c4 = i & 15;
@@ -301,6 +336,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
         }
       }
       __syncthreads();
+      GB_STAMP(5 + 5 * h + 1);
       // softmax + LeakyReLU backward: ds (pre-activation logit grads), da_dst
       for (int n = tid; n < NB; n += blockDim.x) {
         const int d = ndeg[n];
@@ -319,6 +355,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
         dalh[h][1][n] = sum;
       }
       __syncthreads();
+      GB_STAMP(5 + 5 * h + 2);
       // da_src[j] = sum over the targets i that have j as a source (symmetric graph)
       for (int j = tid; j < NB; j += blockDim.x) {
         float s = 0.f;
@@ -330,6 +367,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
         dalh[h][0][j] = s;
       }
       __syncthreads();
+      GB_STAMP(5 + 5 * h + 3);
       // dx += aggregation adjoint + logit adjoint;  dU partials
 #pragma unroll
       for (int r = 0; r < BRPT; ++r) {
@@ -353,8 +391,20 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           dxa[r][q] += a[q] + dal[n][0] * U[h][cg * 4 + q] + dal[n][1] * U[BH + h][cg * 4 + q];
+        if (saved) {
+          // Z_h[n] = sum_i alpha_inh dout_i (the aggregation adjoint of dout): dW_h = sum_n Z_h[n] x_n^T
+          float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int q = 0; q < BDEG; ++q) {
+            const float4 dv = *reinterpret_cast<const float4*>(bufB + nbl[n][q] * BZP + cg * 4);
+            z.x += al4[q] * dv.x; z.y += al4[q] * dv.y; z.z += al4[q] * dv.z; z.w += al4[q] * dv.w;
+          }
+          *reinterpret_cast<float4*>(ybuf + (node0 + n) * ywidth + h * BF + cg * 4) =
+              make_float4(z.x * oscale, z.y * oscale, z.z * oscale, z.w * oscale);
+        }
       }
       __syncthreads();
+      GB_STAMP(5 + 5 * h + 4);
     }
     // dU partials, all heads in one pass over the block's nodes (thread tid: item tid of
     // [8][64], q = which * 4 + h)
@@ -373,8 +423,10 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
     zero_acc(acc);
     mfma_rows64(acc, bufB, arow, c0, lh, li, [&](int j, int c) { return w1[c * BF + j]; });
     __syncthreads();
+    GB_STAMP(5);
     acc_to_lds(acc, xs, rblk, c0, lh, li, 1.f);
     __syncthreads();
+    GB_STAMP(6);
 #pragma unroll
     for (int r = 0; r < BRPT; ++r) {
       const int n = nr0 + BRG * r;
@@ -392,6 +444,16 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
         if (q < dn) { a[0] += gv[q].x; a[1] += gv[q].y; a[2] += gv[q].z; a[3] += gv[q].w; }
 #pragma unroll
       for (int q = 0; q < 4; ++q) dxa[r][q] += a[q];
+      if (saved) {  // Z[n] = sum_{i ~ n} do_i: dW_rel = sum_n Z[n] x_n^T
+        float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q)
+          if (q < dn) {
+            const float4 dv = *reinterpret_cast<const float4*>(bufB + nbl[n][q] * BZP + cg * 4);
+            z.x += dv.x; z.y += dv.y; z.z += dv.z; z.w += dv.w;
+          }
+        *reinterpret_cast<float4*>(ybuf + (node0 + n) * BF + cg * 4) = z;
+      }
     }
   }
 
@@ -410,6 +472,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
     red[nr0][2 * BF + cg * 4 + q] = plb[q];
   }
   __syncthreads();
+  GB_STAMP(25);
   float* pp = part + (int64_t)blockIdx.x * BPART;
   for (int c = tid; c < 3 * BF; c += blockDim.x) {
     float s = 0.f;
@@ -417,6 +480,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
     pp[c] = s;
   }
   if (kind == 0) pp[3 * BF + tid] = dU;
+  GB_STAMP(26);
 }
 
 // dU -> att gradients and the extra dW terms: U_q[k] = sum_c W_h[c][k] att_q[c]
@@ -449,15 +513,26 @@ __global__ void graph_att_proj_kernel2(const float* w0, const float* att_src, co
 
 using namespace a2m;
 
-extern "C" int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t F, int32_t J,
-                                       int32_t kind, int32_t norm_res, const int32_t* nbr_ptr,
-                                       const int32_t* nbr_idx, const float* w0, const float* w1,
-                                       const float* att_src, const float* att_dst,
-                                       const float* bias, const float* ln_w, const float* ln_b,
-                                       float slope, float* dx, float* dw0, float* dw1,
-                                       float* datt_src, float* datt_dst, float* dbias,
-                                       float* dln_w, float* dln_b, void* ws, size_t ws_bytes,
-                                       void* stream) {
+#ifdef A2M_GBWD_STAMPS
+extern "C" int a2m_debug_gbwd_stamps(unsigned long long* host, size_t n) {
+  const size_t cap = (size_t)kGbBlocks * kGbStamps;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gb_stamps), sizeof(unsigned long long) * (n < cap ? n : cap)) ==
+         hipSuccess ? A2M_OK : A2M_EHIP;
+}
+#endif
+
+// pre_ln (nullable): the forward's saved pre-LayerNorm output (a2m_graph_layer_fwd_f32's pre_ln,
+// written when norm_res).  With it the kernel skips the forward recompute and the weight
+// gradients contract the aggregation adjoint of dout with x instead of dout with the aggregated
+// inputs (same sums, another order); without it, the recompute path.
+extern "C" int a2m_graph_layer_bwd_saved_f32(const float* x, const float* dy, const float* pre_ln, int32_t F,
+                                             int32_t J, int32_t kind, int32_t norm_res, const int32_t* nbr_ptr,
+                                             const int32_t* nbr_idx, const float* w0, const float* w1,
+                                             const float* att_src, const float* att_dst, const float* bias,
+                                             const float* ln_w, const float* ln_b, float slope, float* dx,
+                                             float* dw0, float* dw1, float* datt_src, float* datt_dst,
+                                             float* dbias, float* dln_w, float* dln_b, void* ws, size_t ws_bytes,
+                                             void* stream) {
   A2M_CHECK_ARG(x && dy && dx && nbr_ptr && nbr_idx && w0 && bias && dw0 && dbias,
                 "graph_layer_bwd: null pointer");
   A2M_CHECK_ARG(J > 0 && J <= BMAXN && F > 0, "graph_layer_bwd: bad shape");
@@ -493,8 +568,11 @@ extern "C" int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t 
     hipLaunchKernelGGL(graph_att_proj_kernel2, dim3(1), dim3(2 * BH * BF), 0, st, w0, att_src, att_dst, Ug);
     A2M_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(graph_layer_bwd_kernel, dim3(blocks), dim3(BNT), 0, st, x, dy, F, J, kind, norm_res,
-                     nbr_ptr, nbr_idx, w0, w1, Ug, bias, ln_w, ln_b, slope, dx, ybuf, dob, part);
+  // the saved path of the GAT needs no dout rows (its weight gradient contracts Z with x)
+  const bool saved = pre_ln != nullptr;
+  hipLaunchKernelGGL(graph_layer_bwd_kernel, dim3(blocks), dim3(BNT), 0, st, x, dy, pre_ln, F, J, kind, norm_res,
+                     nbr_ptr, nbr_idx, w0, w1, Ug, bias, ln_w, ln_b, slope, dx, ybuf,
+                     saved && kind == 0 ? nullptr : dob, part);
   A2M_LAUNCH_CHECK();
   const int cols = kind == 0 ? BPART : 3 * BF;
   // dbias | dln_w | dln_b straight into the caller's vectors, the attention partials into redv
@@ -506,20 +584,37 @@ extern "C" int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t 
   outs.n = cols > 3 * BF ? 4 : 3;
   int rc = reduce_cols(part, blocks, BPART, cols, outs, 0, st);
   if (rc) return rc;
-  // weight gradients: sum over all nodes of do (x) Y
+  // weight gradients: sum over all nodes of do (x) Y  (saved path: of Z (x) x)
   if (kind == 0) {
-    // dW_h[c][k] = sum_n dout[n][c] Y[n][h*64 + k]   (batch over heads)
-    rc = gemm(dense_kr(dob, BF, 0), dense_kr(ybuf, yw, BF), epi_dense(dw0, BF, (int64_t)BF * BF), BF, BF,
-              (int)Nn, BH, gws, gbytes, st);
+    // dW_h[c][k] = sum_n dout[n][c] Y[n][h*64 + k] = sum_n Z[n][h*64 + c] x[n][k]  (batch over heads)
+    rc = saved ? gemm(dense_kr(ybuf, yw, BF), dense_kr(x, BF, 0), epi_dense(dw0, BF, (int64_t)BF * BF), BF, BF,
+                      (int)Nn, BH, gws, gbytes, st)
+               : gemm(dense_kr(dob, BF, 0), dense_kr(ybuf, yw, BF), epi_dense(dw0, BF, (int64_t)BF * BF), BF, BF,
+                      (int)Nn, BH, gws, gbytes, st);
     if (rc) return rc;
     hipLaunchKernelGGL(graph_att_bwd_kernel, dim3((unsigned)cdiv(BH * BF * BF, 256)), dim3(256), 0, st, w0,
                        att_src, att_dst, redv + 3 * BF, dw0, datt_src, datt_dst);
     A2M_LAUNCH_CHECK();
   } else {
-    rc = gemm(dense_kr(dob, BF), dense_kr(ybuf, BF), epi_dense(dw0, BF), BF, BF, (int)Nn, 1, gws, gbytes, st);
+    rc = saved ? gemm(dense_kr(ybuf, BF), dense_kr(x, BF), epi_dense(dw0, BF), BF, BF, (int)Nn, 1, gws, gbytes, st)
+               : gemm(dense_kr(dob, BF), dense_kr(ybuf, BF), epi_dense(dw0, BF), BF, BF, (int)Nn, 1, gws, gbytes, st);
     if (rc) return rc;
     rc = gemm(dense_kr(dob, BF), dense_kr(x, BF), epi_dense(dw1, BF), BF, BF, (int)Nn, 1, gws, gbytes, st);
     if (rc) return rc;
   }
   return A2M_OK;
+}
+
+extern "C" int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t F, int32_t J,
+                                       int32_t kind, int32_t norm_res, const int32_t* nbr_ptr,
+                                       const int32_t* nbr_idx, const float* w0, const float* w1,
+                                       const float* att_src, const float* att_dst,
+                                       const float* bias, const float* ln_w, const float* ln_b,
+                                       float slope, float* dx, float* dw0, float* dw1,
+                                       float* datt_src, float* datt_dst, float* dbias,
+                                       float* dln_w, float* dln_b, void* ws, size_t ws_bytes,
+                                       void* stream) {
+  return a2m_graph_layer_bwd_saved_f32(x, dy, nullptr, F, J, kind, norm_res, nbr_ptr, nbr_idx, w0, w1, att_src,
+                                       att_dst, bias, ln_w, ln_b, slope, dx, dw0, dw1, datt_src, datt_dst, dbias,
+                                       dln_w, dln_b, ws, ws_bytes, stream);
 }

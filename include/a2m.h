@@ -426,6 +426,16 @@ int a2m_graph_layer_bwd_f32(const float* x, const float* dy, int32_t F, int32_t 
                             const float* ln_b, float slope, float* dx, float* dw0, float* dw1,
                             float* datt_src, float* datt_dst, float* dbias, float* dln_w,
                             float* dln_b, void* ws, size_t ws_bytes, void* stream);
+/* The same with the forward's saved pre-LayerNorm output (a2m_graph_layer_fwd_f32's pre_ln,
+   norm_res layers; NULL = recompute): no forward recompute in the backward kernel, and the
+   weight gradients contract the aggregation adjoint of dout with x (same sums, another order). */
+int a2m_graph_layer_bwd_saved_f32(const float* x, const float* dy, const float* pre_ln, int32_t F,
+                                  int32_t J, int32_t kind, int32_t norm_res, const int32_t* nbr_ptr,
+                                  const int32_t* nbr_idx, const float* w0, const float* w1,
+                                  const float* att_src, const float* att_dst, const float* bias,
+                                  const float* ln_w, const float* ln_b, float slope, float* dx,
+                                  float* dw0, float* dw1, float* datt_src, float* datt_dst, float* dbias,
+                                  float* dln_w, float* dln_b, void* ws, size_t ws_bytes, void* stream);
 
 /* F.interpolate (time) backward: dx [B][C][H][W] (zeros where the forward read nothing). */
 int a2m_interp_time_bwd_f32(const float* dy, int32_t B, int32_t C, int32_t H, int32_t W,

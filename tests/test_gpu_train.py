@@ -203,13 +203,17 @@ def test_channel_attention_train(B, C, T):
                   'b2': (m.fc[2].bias.grad, sd['c.fc.2.bias'].grad)})
 
 
-@pytest.mark.parametrize('kind,J,lo,norm_res', [(0, 10, 0, True), (0, 42, 10, True), (1, 42, 10, True),
-                                                (1, 10, 0, True), (0, 42, 10, False)])
-def test_graph_layer_train(kind, J, lo, norm_res):
+@pytest.mark.parametrize('save_pre', [True, False], ids=['saved', 'recompute'])
+@pytest.mark.parametrize('kind,J,lo,norm_res,Fr', [(0, 10, 0, True, 7), (0, 42, 10, True, 7), (1, 42, 10, True, 7),
+                                                   (1, 10, 0, True, 7), (0, 42, 10, False, 7),
+                                                   (0, 42, 10, True, 29), (1, 10, 0, True, 29)])
+def test_graph_layer_train(kind, J, lo, norm_res, Fr, save_pre, monkeypatch):
+    """Both backward paths: the forward's saved pre-LayerNorm output (the weight gradients as
+    Z (x) x, Z the aggregation adjoint of dout) and the in-kernel recompute (dout (x) Y)."""
     from a2m import autograd as AG
     from a2m import skeleton as S
     from oracle import model as OM
-    Fr = 7
+    monkeypatch.setattr(AG, '_GRAPH_SAVE_PRE', save_pre)
     ei = S.edge_index(lo, J)
     ptr, idx = [t.to(DEV) for t in S.in_neighbour_csr(ei, J)]
     edges = OM.expand_edges(ei, J, Fr)

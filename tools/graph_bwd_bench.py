@@ -24,13 +24,24 @@ for name, J, lo, kind in (('hand gat', 42, 10, 0), ('hand gconv', 42, 10, 1), ('
         a_s = a_d = None
     b = torch.zeros(64, device=dev)
     lw, lb = torch.ones(64, device=dev), torch.zeros(64, device=dev)
-    run = lambda: F.graph_layer_bwd(x, dy, J, kind, ptr, idx, w0, w1, a_s, a_d, b, lw, lb)  # noqa: E731
-    for _ in range(3):
-        run()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    pre = torch.empty_like(x)
+    F.graph_layer(x, J, kind, ptr, idx, w0, w1, a_s, a_d, b, lw, lb, pre_ln=pre)
+    for mode, p in (('recompute', None), ('saved o', pre)):
+        run = lambda: F.graph_layer_bwd(x, dy, J, kind, ptr, idx, w0, w1, a_s, a_d, b, lw, lb, pre_ln=p)  # noqa: E731
+        for _ in range(3):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            run()
+        e1.record()
+        e1.synchronize()
+        print(f'{name:12s} backward, {mode:9s} (kernel + weight-gradient GEMMs): {e0.elapsed_time(e1) * 100:.1f} us',
+              flush=True)
+    fw = lambda: F.graph_layer(x, J, kind, ptr, idx, w0, w1, a_s, a_d, b, lw, lb, pre_ln=pre)  # noqa: E731
     e0.record()
     for _ in range(10):
-        run()
+        fw()
     e1.record()
     e1.synchronize()
-    print(f'{name:12s} backward (kernel + weight-gradient GEMMs): {e0.elapsed_time(e1) * 100:.1f} us', flush=True)
+    print(f'{name:12s} forward writing pre_ln: {e0.elapsed_time(e1) * 100:.1f} us', flush=True)

@@ -1,0 +1,5 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_train.py > gpurun_out/train_tests.txt 2>&1 || { tail -20 gpurun_out/train_tests.txt; exit 3; }
+tail -2 gpurun_out/train_tests.txt
+TRAIN_STEPS=20 TRAIN_WARMUP=3 bash tools/ab_train_env.sh 2 "" A2M_GRAPH_SAVE_PRE=0 A2M_GRAPH_SAVE_PRE=1
