@@ -30,6 +30,8 @@ constexpr int BPART = 3 * BF + 2 * BH * BF;  // dbias | dln_w | dln_b | dU[8][64
 // work at one workgroup per CU): MFMA wave w owns rows 32 (w & 3).. and columns 32 (w >> 2)..;
 // the row-wise phases use 16 lanes per node row, BRG = 32 row groups of BRPT rows each.
 constexpr int BNT = 512, BRG = BNT / 16, BRPT = BMAXN / BRG;
+static_assert(BNT == 2 * BH * BF, "one thread per GAT projection element in the prologue");
+static_assert(BNT >= 2 * BMAXN, "one thread per CSR entry in the prologue");
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -66,6 +68,27 @@ __device__ __forceinline__ void mfma_rows64(floatx16& acc, const float* A, int a
   }
 }
 
+// the same product with the B fragments preloaded: w[8 kc + s] = W^T(c0 + li, 16 kc + 8 lh + s)
+// (load_wt: W row-major [64][64], B(n = j, k = c) = W[c][j])
+__device__ __forceinline__ void load_wt(float (&w)[32], const float* __restrict__ W, int c0, int lh, int li) {
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) w[kc * 8 + s] = W[(kc * 16 + lh * 8 + s) * BF + c0 + li];
+}
+
+__device__ __forceinline__ void mfma_rows64_w(floatx16& acc, const float* A, int arow, int lh, const float (&w)[32]) {
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc) {
+    const float* p = A + arow * BZP + kc * 16 + lh * 8;
+    const float4 a0 = *reinterpret_cast<const float4*>(p);
+    const float4 a1 = *reinterpret_cast<const float4*>(p + 4);
+    const float af[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], w[kc * 8 + s], acc, 0, 0, 0);
+  }
+}
+
 __device__ __forceinline__ void acc_to_lds(const floatx16& acc, float* dst, int rblk, int c0, int lh,
                                            int li, float scale) {
 #pragma unroll
@@ -96,10 +119,11 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
   __shared__ float dsb[BMAXN][BDEG];
   __shared__ float dal[BMAXN][2];
   __shared__ float dalh[BH][2][BMAXN];  // every head's (da_src, da_dst), for the dU pass
-  __shared__ unsigned char nbl[BMAXN][BDEG];
-  __shared__ unsigned char rev[BMAXN][BDEG];  // GAT: slot of n in nbl[nbl[n][q]] (0xff: none)
+  __shared__ __attribute__((aligned(8))) unsigned char nbl[BMAXN][BDEG];
+  __shared__ __attribute__((aligned(8))) unsigned char rev[BMAXN][BDEG];  // GAT: slot of n in nbl[nbl[n][q]] (0xff: none)
   __shared__ unsigned char ndeg[BMAXN];
   __shared__ float red[BRG][3 * BF];
+  __shared__ int csr[2 * BMAXN];   // the in-neighbour CSR (row pointers, then sources)
 
   const int fpb = BMAXN / J;
   const int NBmax = fpb * J;
@@ -115,25 +139,34 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
   // the forward's saved pre-LayerNorm output o (bias included) replaces the recompute
   const bool saved = pre_ln != nullptr;
   const bool load_o = saved && norm_res;
-  {  // node tile (and o): all loads of this thread in flight before the LDS writes
-    constexpr int NL = BMAXN * (BF / 4) / BNT;
-    float4 v[NL], u[NL];
+  // ---- prologue: every global load of the block issued before the first LDS write (oldest
+  // first: what the first barrier needs, then the weight fragments and dy rows that stay in flight)
+  const int ne = min(nbr_ptr[J], 2 * BMAXN - (J + 1));
+  constexpr int NL = BMAXN * (BF / 4) / BNT;
+  float4 v[NL], u[NL];
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int i = tid + j * BNT, n = i / (BF / 4), q = i % (BF / 4);
-      v[j] = n < NB ? *reinterpret_cast<const float4*>(x + (node0 + n) * BF + q * 4)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
-      u[j] = load_o && n < NB ? *reinterpret_cast<const float4*>(pre_ln + (node0 + n) * BF + q * 4)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int i = tid + j * BNT, n = i / (BF / 4), q = i % (BF / 4);
-      *reinterpret_cast<float4*>(xs + n * BZP + q * 4) = v[j];
-      if (load_o) *reinterpret_cast<float4*>(bufA + n * BZP + q * 4) = u[j];
-    }
+  for (int j = 0; j < NL; ++j) {
+    const int i = tid + j * BNT, n = i / (BF / 4), q = i % (BF / 4);
+    v[j] = n < NB ? *reinterpret_cast<const float4*>(x + (node0 + n) * BF + q * 4)
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    u[j] = load_o && n < NB ? *reinterpret_cast<const float4*>(pre_ln + (node0 + n) * BF + q * 4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // this thread's rows of dy, in flight across the prologue / recompute
+  const float uval = kind == 0 ? Ug[tid] : 0.f;   // 512 threads = the [8][64] projections
+  const int csr_v = tid <= J ? nbr_ptr[tid] : (tid < J + 1 + ne ? nbr_idx[tid - (J + 1)] : 0);
+  // B fragments of the backward MFMAs (GAT: head 0, the next head's one head ahead; GraphConv:
+  // W_rel and W_root)
+  float wcur[32], wnxt[32];
+  load_wt(wcur, w0, c0, lh, li);
+  if (kind != 0) load_wt(wnxt, w1, c0, lh, li);
+  // this thread's columns of the bias / LayerNorm parameters and its rows of dy, in flight across
+  // the prologue / recompute
+  const float4 bias4 = saved ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(bias + cg * 4);
+  const float4 lnw4 = norm_res ? *reinterpret_cast<const float4*>(ln_w + cg * 4) : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 lnb4 = norm_res ? *reinterpret_cast<const float4*>(ln_b + cg * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float biasv[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
+  const float lnwv[4] = {lnw4.x, lnw4.y, lnw4.z, lnw4.w};
+  const float lnbv[4] = {lnb4.x, lnb4.y, lnb4.z, lnb4.w};
   float4 dyr[BRPT];
 #pragma unroll
   for (int r = 0; r < BRPT; ++r) {
@@ -141,13 +174,20 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
     dyr[r] = n < NB ? *reinterpret_cast<const float4*>(dy + (node0 + n) * BF + cg * 4)
                     : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (kind == 0)
-    for (int i = tid; i < 2 * BH * BF; i += blockDim.x) (&U[0][0])[i] = Ug[i];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int i = tid + j * BNT, n = i / (BF / 4), q = i % (BF / 4);
+    *reinterpret_cast<float4*>(xs + n * BZP + q * 4) = v[j];
+    if (load_o) *reinterpret_cast<float4*>(bufA + n * BZP + q * 4) = u[j];
+  }
+  if (kind == 0) (&U[0][0])[tid] = uval;
+  if (tid < J + 1 + ne) csr[tid] = csr_v;
+  __syncthreads();
   for (int n = tid; n < BMAXN; n += blockDim.x) {
     int d = 0;
     if (n < NB) {
       const int f0 = (n / J) * J, ln = n % J;
-      for (int e = nbr_ptr[ln]; e < nbr_ptr[ln + 1] && d < BDEG; ++e) nbl[n][d++] = f0 + nbr_idx[e];
+      for (int e = csr[ln]; e < csr[ln + 1] && d < BDEG; ++e) nbl[n][d++] = f0 + csr[J + 1 + e];
       if (kind == 0 && d < BDEG) nbl[n][d++] = n;
     }
     for (int q = d; q < BDEG; ++q) nbl[n][q] = 0;  // unpredicated gathers read row 0, weight 0
@@ -158,22 +198,29 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
   if (kind == 0) {
     // reverse-edge slots, once per block (the per-head adjoint loops index them directly
     // instead of searching the neighbour list of every neighbour)
-    for (int n = tid; n < NB; n += blockDim.x) {
-      const int d = ndeg[n];
-      for (int q = 0; q < BDEG; ++q) {
-        unsigned char r = 0xff;
-        if (q < d) {
-          const int i = nbl[n][q];
-          for (int p = ndeg[i] - 1; p >= 0; --p)
-            if (nbl[i][p] == n) r = (unsigned char)p;  // first match, as the search did
-        }
-        rev[n][q] = r;
+    // (one thread per (n, q); neighbour i's list read as one 8-byte word)
+    for (int it = tid; it < NB * BDEG; it += blockDim.x) {
+      const int n = it / BDEG, q = it % BDEG;
+      unsigned char r = 0xff;
+      if (q < ndeg[n]) {
+        const int i = nbl[n][q], di = ndeg[i];
+        const uint2 nb = *reinterpret_cast<const uint2*>(&nbl[i][0]);
+#pragma unroll
+        for (int p = BDEG - 1; p >= 0; --p)
+          if (p < di && (((p < 4 ? nb.x : nb.y) >> (8 * (p & 3))) & 0xff) == (unsigned)n)
+            r = (unsigned char)p;  // first match, as the search did
       }
+      rev[n][q] = r;
     }
     for (int i = tid; i < NB * 2 * BH; i += blockDim.x) {
       const int n = i >> 3, q = i & 7;
-      float s = 0.f;
-      for (int k = 0; k < BF; ++k) s += xs[n * BZP + k] * U[q][k];
+      float s = 0.f;   // k in order, as the forward's logits (graph.hip)
+#pragma unroll 4
+      for (int k = 0; k < BF; k += 4) {
+        const float4 xv = *reinterpret_cast<const float4*>(xs + n * BZP + k);
+        const float4 uv = *reinterpret_cast<const float4*>(&U[q][k]);
+        s += xv.x * uv.x; s += xv.y * uv.y; s += xv.z * uv.z; s += xv.w * uv.w;
+      }
       al[n][q] = s;
     }
     __syncthreads();
@@ -255,7 +302,7 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
     float o[4], g4[4];
     const float dyv[4] = {dyr[r].x, dyr[r].y, dyr[r].z, dyr[r].w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = saved ? bufA[n * BZP + cg * 4 + q] : bufA[n * BZP + cg * 4 + q] + bias[cg * 4 + q];
+    for (int q = 0; q < 4; ++q) o[q] = saved ? bufA[n * BZP + cg * 4 + q] : bufA[n * BZP + cg * 4 + q] + biasv[q];
     float dov[4];
     if (norm_res) {
       float s = o[0] + o[1] + o[2] + o[3];
@@ -269,13 +316,12 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
       float sg = 0.f, sgx = 0.f, oh[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int c = cg * 4 + q;
         oh[q] = (o[q] - mean) * rstd;
-        const float u = oh[q] * ln_w[c] + ln_b[c];
+        const float u = oh[q] * lnwv[q] + lnbv[q];
         const float du = n < NB ? dyv[q] * (u > 0.f ? 1.f : slope) : 0.f;
         plw[q] += du * oh[q];
         plb[q] += du;
-        g4[q] = du * ln_w[c];
+        g4[q] = du * lnwv[q];
         sg += g4[q];
         sgx += g4[q] * oh[q];
       }
@@ -310,65 +356,66 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
       edge_softmax(h);
       // dY_h = do W_h / 4  -> bufA
       zero_acc(acc);
-      const float* Wh = w0 + (int64_t)h * BF * BF;
-      mfma_rows64(acc, bufB, arow, c0, lh, li, [&](int j, int c) { return Wh[c * BF + j]; });
+      if (h + 1 < BH) load_wt(wnxt, w0 + (int64_t)(h + 1) * BF * BF, c0, lh, li);
+      mfma_rows64_w(acc, bufB, arow, lh, wcur);
       acc_to_lds(acc, bufA, rblk, c0, lh, li, 1.f / BH);
+#pragma unroll
+      for (int s = 0; s < 32; ++s) wcur[s] = wnxt[s];
       __syncthreads();
       GB_STAMP(5 + 5 * h + 0);
-      // dalpha[n][q] = dY_h[n] . x[nbl[n][q]]  (16 lanes per node)
+      // dalpha[n][q] = dY_h[n] . x[nbl[n][q]]  (16 lanes per node), then on every lane of the
+      // node's group (identical row sums) the softmax + LeakyReLU backward: ds (pre-activation
+      // logit grads, -> dsb) and da_dst
       for (int i = tid; i < BMAXN * 16; i += blockDim.x) {
         const int n = i >> 4, c4 = i & 15;
         const int d = ndeg[n];
         const float4 g = *reinterpret_cast<const float4*>(bufA + n * BZP + c4 * 4);
+        const uint2 nb = *reinterpret_cast<const uint2*>(&nbl[n][0]);
+        int ids[BDEG];
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q) ids[q] = ((q < 4 ? nb.x : nb.y) >> (8 * (q & 3))) & 0xff;
         float4 xv[BDEG];
 #pragma unroll
         for (int q = 0; q < BDEG; ++q)
-          xv[q] = *reinterpret_cast<const float4*>(xs + nbl[n][q] * BZP + c4 * 4);
+          xv[q] = *reinterpret_cast<const float4*>(xs + ids[q] * BZP + c4 * 4);
         float v[BDEG];
 #pragma unroll
         for (int q = 0; q < BDEG; ++q)
           v[q] = q < d ? g.x * xv[q].x + g.y * xv[q].y + g.z * xv[q].z + g.w * xv[q].w : 0.f;
 #pragma unroll
         for (int q = 0; q < BDEG; ++q) v[q] = row16_sum(v[q]);
-        if (c4 == 0) {
+        if (n < NB) {
+          const float ad = al[n][BH + h];
+          float e[BDEG], sv[BDEG];
 #pragma unroll
-          for (int q = 0; q < BDEG; ++q) dsb[n][q] = v[q];
+          for (int q = 0; q < BDEG; ++q) {
+            e[q] = ew[n][q];
+            sv[q] = al[ids[q]][h] + ad;
+          }
+          float sdot = 0.f;
+#pragma unroll
+          for (int q = 0; q < BDEG; ++q)
+            if (q < d) sdot += e[q] * v[q];
+          float sum = 0.f;
+#pragma unroll
+          for (int q = 0; q < BDEG; ++q)
+            if (q < d) {
+              const float de = e[q] * (v[q] - sdot);
+              v[q] = de * (sv[q] > 0.f ? 1.f : 0.2f);
+              sum += v[q];
+            }
+          if (c4 == 0) {
+#pragma unroll
+            for (int q = 0; q < BDEG; ++q)
+              if (q < d) dsb[n][q] = v[q];
+            dal[n][1] = sum;
+            dalh[h][1][n] = sum;
+          }
         }
       }
       __syncthreads();
       GB_STAMP(5 + 5 * h + 1);
-      // softmax + LeakyReLU backward: ds (pre-activation logit grads), da_dst
-      for (int n = tid; n < NB; n += blockDim.x) {
-        const int d = ndeg[n];
-        const float ad = al[n][BH + h];
-        float sdot = 0.f;
-        for (int q = 0; q < d; ++q) sdot += ew[n][q] * dsb[n][q];
-        float sum = 0.f;
-        for (int q = 0; q < d; ++q) {
-          const float s = al[nbl[n][q]][h] + ad;
-          const float de = ew[n][q] * (dsb[n][q] - sdot);
-          const float ds = de * (s > 0.f ? 1.f : 0.2f);
-          dsb[n][q] = ds;
-          sum += ds;
-        }
-        dal[n][1] = sum;
-        dalh[h][1][n] = sum;
-      }
-      __syncthreads();
-      GB_STAMP(5 + 5 * h + 2);
-      // da_src[j] = sum over the targets i that have j as a source (symmetric graph)
-      for (int j = tid; j < NB; j += blockDim.x) {
-        float s = 0.f;
-        for (int q = 0; q < ndeg[j]; ++q) {
-          const int p = rev[j][q];
-          if (p != 0xff) s += dsb[nbl[j][q]][p];
-        }
-        dal[j][0] = s;
-        dalh[h][0][j] = s;
-      }
-      __syncthreads();
-      GB_STAMP(5 + 5 * h + 3);
-      // dx += aggregation adjoint + logit adjoint;  dU partials
+      // dx += aggregation adjoint + logit adjoint (with da_src);  dU partials
 #pragma unroll
       for (int r = 0; r < BRPT; ++r) {
         const int n = nr0 + BRG * r;
@@ -376,13 +423,26 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
         float a[4] = {0.f, 0.f, 0.f, 0.f};
         float4 gv[BDEG];
         float al4[BDEG];
+        const uint2 nb = *reinterpret_cast<const uint2*>(&nbl[n][0]);
+        const uint2 rv = *reinterpret_cast<const uint2*>(&rev[n][0]);
+        int ids[BDEG], ps[BDEG];
 #pragma unroll
         for (int q = 0; q < BDEG; ++q) {
-          const int i = nbl[n][q];
-          const int p = rev[n][q];
-          gv[q] = *reinterpret_cast<const float4*>(bufA + i * BZP + cg * 4);
-          al4[q] = p != 0xff ? ew[i][p] : 0.f;  // 0xff past the degree
+          ids[q] = ((q < 4 ? nb.x : nb.y) >> (8 * (q & 3))) & 0xff;
+          ps[q] = ((q < 4 ? rv.x : rv.y) >> (8 * (q & 3))) & 0xff;
         }
+        // da_src[n] = sum of ds over the edges out of n (j = n's targets, symmetric graph)
+        const int dn = ndeg[n];
+        float das = 0.f;
+#pragma unroll
+        for (int q = 0; q < BDEG; ++q) {
+          gv[q] = *reinterpret_cast<const float4*>(bufA + ids[q] * BZP + cg * 4);
+          const bool e = ps[q] != 0xff;   // 0xff past the degree
+          al4[q] = e ? ew[ids[q]][ps[q] & 7] : 0.f;
+          const float dsv = e ? dsb[ids[q]][ps[q] & 7] : 0.f;
+          if (q < dn && e) das += dsv;
+        }
+        if (cg == 0) dalh[h][0][n] = das;
 #pragma unroll
         for (int q = 0; q < BDEG; ++q) {
           a[0] += al4[q] * gv[q].x; a[1] += al4[q] * gv[q].y; a[2] += al4[q] * gv[q].z;
@@ -390,13 +450,13 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          dxa[r][q] += a[q] + dal[n][0] * U[h][cg * 4 + q] + dal[n][1] * U[BH + h][cg * 4 + q];
+          dxa[r][q] += a[q] + das * U[h][cg * 4 + q] + dal[n][1] * U[BH + h][cg * 4 + q];
         if (saved) {
           // Z_h[n] = sum_i alpha_inh dout_i (the aggregation adjoint of dout): dW_h = sum_n Z_h[n] x_n^T
           float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int q = 0; q < BDEG; ++q) {
-            const float4 dv = *reinterpret_cast<const float4*>(bufB + nbl[n][q] * BZP + cg * 4);
+            const float4 dv = *reinterpret_cast<const float4*>(bufB + ids[q] * BZP + cg * 4);
             z.x += al4[q] * dv.x; z.y += al4[q] * dv.y; z.z += al4[q] * dv.z; z.w += al4[q] * dv.w;
           }
           *reinterpret_cast<float4*>(ybuf + (node0 + n) * ywidth + h * BF + cg * 4) =
@@ -418,10 +478,10 @@ __global__ __launch_bounds__(BNT) void graph_layer_bwd_kernel(
   } else {
     // dagg = do W_rel -> bufA ; dx_root = do W_root -> xs (x no longer needed)
     zero_acc(acc);
-    mfma_rows64(acc, bufB, arow, c0, lh, li, [&](int j, int c) { return w0[c * BF + j]; });
+    mfma_rows64_w(acc, bufB, arow, lh, wcur);
     acc_to_lds(acc, bufA, rblk, c0, lh, li, 1.f);
     zero_acc(acc);
-    mfma_rows64(acc, bufB, arow, c0, lh, li, [&](int j, int c) { return w1[c * BF + j]; });
+    mfma_rows64_w(acc, bufB, arow, lh, wnxt);
     __syncthreads();
     GB_STAMP(5);
     acc_to_lds(acc, xs, rblk, c0, lh, li, 1.f);
@@ -539,6 +599,8 @@ extern "C" int a2m_graph_layer_bwd_saved_f32(const float* x, const float* dy, co
   A2M_CHECK_ARG(kind == 0 ? (att_src && att_dst && datt_src && datt_dst) : (kind == 1 && w1 && dw1),
                 "graph_layer_bwd: bad kind / params");
   A2M_CHECK_ARG(!norm_res || (ln_w && ln_b && dln_w && dln_b), "graph_layer_bwd: LN params");
+  auto al16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  A2M_CHECK_ARG(al16(bias) && al16(ln_w) && al16(ln_b), "graph_layer_bwd: bias / LayerNorm vectors must be 16-byte aligned");
   const int fpb = BMAXN / J;
   const int blocks = (int)cdiv(F, fpb);
   const int64_t Nn = (int64_t)F * J;
