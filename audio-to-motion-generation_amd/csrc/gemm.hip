@@ -643,10 +643,21 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   const bool rows3 = mb == 3 && B.K1 == 1 && B.K2 == 1 && B.R1 == 1 && B.ch == 0 && B.cw == 0 &&
                      B.divh == 1 && B.divw == 1 && N % 4 == 0 &&
                      ((B.R2 == 1 && B.sr0 == 1) || (B.R2 % 4 == 0 && B.ar2 == 1 && B.sw == 1 && B.Lw >= B.R2));
-  const bool pipe_launch = pipe_on && prec == 0 && p.bm == 64 && ma == 0 &&
-                           (mb == 0 || mb == 6 || rows3 ||
-                            (mb == 5 && (a.B.halo || (B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 &&
-                                                      64 % B.R2 == 0)))) && pipe_ext;
+  // mode 4 on both sides (the 1-D conv weight gradients): one k digit (K1 = 1) in runs of a
+  // multiple of the 32-k tile, every split a whole number of tiles, offsets below 2^29
+  auto runs4 = [&](const Gather& g, int R) {
+    const int64_t rmax = (int64_t)((R - 1) / (g.R1 * g.R2)) * g.sr0 +
+                         (int64_t)std::max(0, g.Lh - 1) * std::abs(g.sh) + g.Lw + (int64_t)(K / g.K2) * g.sk0;
+    return g.K1 == 1 && g.K2 % 32 == 0 && g.bk2 == 1 && g.sw == 1 && g.divh == 1 && g.divw == 1 &&
+           g.sr0 >= 0 && g.sk0 >= 0 && below(rmax);
+  };
+  static const int pipe4_env = env_int("A2M_GEMM_PIPE4", 1);
+  const bool pipe_m4 = pipe4_env && ma == 4 && mb == 4 && p.kchunk % 32 == 0 && runs4(A, M) && runs4(B, N);
+  const bool pipe_launch = pipe_on && prec == 0 && p.bm == 64 &&
+                           ((ma == 0 && (mb == 0 || mb == 6 || rows3 ||
+                                         (mb == 5 && (a.B.halo || (B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 &&
+                                                                   64 % B.R2 == 0)))) && pipe_ext) ||
+                            pipe_m4);
   // the bf16-operand pipelined tile (gemm_pipe_bf16.h): the same operand modes, 64-channel
   // k-tiles (mode 6: Ci % 64 == 0), no halo layout (mode 5 takes the per-tap stores)
   const bool pipe_bf16 = pipe_on && prec == 1 && p.bm == 64 && ma == 0 &&

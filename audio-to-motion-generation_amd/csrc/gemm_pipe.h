@@ -18,8 +18,9 @@
 //
 // B operand modes: 0 dense k-contiguous rows, 3 row-contiguous [B][C][T] / [K][R] operands (the
 // 1x1 projections), 6 channels-last conv rows (Gather::nhwc), 5 the tap-chunked conv1d in the
-// halo layout (Gather::halo: 3 taps, pad 1, clips T >= 16 that tile the 64 rows).  A is always
-// dense rows (mode 0; the packed conv weights).
+// halo layout (Gather::halo: 3 taps, pad 1, clips T >= 16 that tile the 64 rows), 4 k-contiguous
+// runs (the 1-D conv weight gradients, with A in mode 4 too).  Otherwise A is dense rows (mode 0;
+// the packed conv weights).
 #pragma once
 #include "gemm_kernel.h"
 
@@ -82,6 +83,59 @@ struct PipeRows {
     r[p] = pipe_load(rs, knext + kq < K ? off[p] : kPipeOOB);
     off[p] += 4u * 32;
     if (p == 1) knext += 32;
+  }
+  __device__ __forceinline__ void store(float* st, const float4 (&r)[2], int p) const {
+    *reinterpret_cast<float4*>(st + (lrow + 32 * p) * kPipeLDK + kq) = r[p];
+  }
+};
+
+// k-contiguous runs (mode 4, the weight-gradient operands of the 1-D convs): element (r, k) at
+// r0 * sr0 + h * sh + w + k0 * sk0 with k = k0 * K2 + k2, w = r2 * ar2 + cw + k2 (h = r1 * ar1 + ch,
+// K1 = 1), zero where w falls outside [0, Lw) or h outside [0, Lh).  K2 % 32 == 0 (host), so a
+// k-tile is one run: k0 and the run offset are uniform, and each lane's quad is one float4 unless
+// it crosses the row's edge (the padding taps), where it loads element by element.  Thread map
+// and LDS layout of PipeRows, so the stages hold what gemm_tile's mode-4 loader stores
+struct PipeRuns {
+  __amdgpu_buffer_rsrc_t rs;
+  int rbase[2], w0[2];   // element offset of the thread's rows at (k0, k2) = (0, 0); their w origin
+  bool rv[2];
+  int kq, lrow, knext, K, k0, k2t, K2, sk0, Lw;
+  __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
+    rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
+    kq = (tid & 7) * 4;
+    lrow = tid >> 3;
+    K = KK;
+    knext = kbeg;
+    K2 = g.K2; sk0 = g.sk0; Lw = g.Lw;
+    k0 = kbeg / K2;
+    k2t = kbeg - k0 * K2;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const RowInfo ri = row_info(g, row0 + lrow + 32 * p, R);
+      rv[p] = ri.valid && ri.h >= 0 && ri.h < g.Lh;
+      rbase[p] = ri.base + ri.h * g.sh + ri.w;
+      w0[p] = ri.w;
+    }
+  }
+  __device__ __forceinline__ void load(float4 (&r)[2], int p) {
+    const int w = w0[p] + k2t + kq;                   // the quad's first element along the run
+    const int e0 = rbase[p] + k0 * sk0 + k2t + kq;    // its element offset (>= 0 where w >= 0)
+    const bool inb = rv[p] && knext < K;
+    const bool full = inb && w >= 0 && w + 3 < Lw;
+    r[p] = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
+    if (inb && !full) {   // a quad across the row's edge: the elements inside it, the rest 0
+      float e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        e[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                   rs, (unsigned)(w + j) < (unsigned)Lw ? (uint32_t)(e0 + j) * 4u : kPipeOOB, 0, 0));
+      r[p] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+    if (p == 1) {
+      knext += 32;
+      k2t += 32;
+      if (k2t == K2) { k2t = 0; ++k0; }
+    }
   }
   __device__ __forceinline__ void store(float* st, const float4 (&r)[2], int p) const {
     *reinterpret_cast<float4*>(st + (lrow + 32 * p) * kPipeLDK + kq) = r[p];
@@ -378,7 +432,7 @@ __device__ __forceinline__ void pipe_step(floatx16& acc, float (&fa0)[8], float 
   A2M_SB();
 }
 
-template <int MB, int NT = 0>   // NT > 0: mode 5 in the general (per-tap store) layout
+template <int MB, int NT = 0, int MA = 0>   // NT > 0: mode 5 in the general (per-tap store) layout
 __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   A2M_PSTAMP(4, __builtin_amdgcn_s_memrealtime());
   A2M_PSTAMP(0, __builtin_amdgcn_s_memtime());
@@ -404,11 +458,14 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   const int kend = min(args.K, kbeg + args.kchunk);
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
 
-  PipeRows la;
+  static_assert(MA == 0 || (MA == 4 && MB == 4), "A in mode 4 only with B in mode 4");
+  typename std::conditional<MA == 4, PipeRuns, PipeRows>::type la;
   la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
   using LB = typename std::conditional<
       MB == 5, typename std::conditional<TAPS, PipeTap<NT ? NT : 1>, PipeHalo>::type,
-      typename std::conditional<MB == 6, PipeNhwc, typename std::conditional<MB == 3, PipeRowsT, PipeRows>::type>::type>::type;
+      typename std::conditional<MB == 6, PipeNhwc,
+                                typename std::conditional<MB == 3, PipeRowsT,
+                                                          typename std::conditional<MB == 4, PipeRuns, PipeRows>::type>::type>::type>::type;
   LB lb;
   lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
 

@@ -1,8 +1,8 @@
 """The software-pipelined 64x64 tiles -- gemm_pipe.h (fp32) and gemm_pipe_bf16.h (bf16 operands)
 -- against gemm_tile, the engine's reference tile, on every operand mode they take: dense rows
 (mode 0), row-contiguous [K][N] operands (mode 3), the tap-chunked conv1d (mode 5, three taps)
-and ConvTranspose phases (mode 5, two taps with a shift), channels-last conv rows (mode 6); ragged
-M / N / K, one and several split-K slabs, float4 and scalar epilogues.
+and ConvTranspose phases (mode 5, two taps with a shift), channels-last conv rows (mode 6), the
+1-D conv weight gradients (mode 4 on both sides; fp32 only, bf16 takes gemm_tile); ragged M / N / K, one and several split-K slabs, float4 and scalar epilogues.
 
 Both tiles compute the same products in the same order, so the results are bitwise equal, except
 fp32 dense rows, whose gemm_tile path is the two-wave-group tile (KS = 2: the k halves summed in a
@@ -96,6 +96,18 @@ def _case_nhwc(B, Ci, Co, H, W):
     return run, ref, False
 
 
+def _case_wgrad1d(B, Ci, Co, T, k, pad):
+    Tout = T + 2 * pad - k + 1
+    x = _rand(B, Ci, T, seed=14)
+    dy = _rand(B, Co, Tout, seed=15)
+
+    def run():
+        from a2m import functional as F
+        return F.conv_wgrad(dy, x, (Co, Ci, k), 1, pad)
+    ref = torch.nn.grad.conv1d_weight(x.double(), (Co, Ci, k), dy.double(), padding=pad)
+    return run, ref, False
+
+
 CASES = {
     'gemm_200x1000x768': lambda: _case_gemm(200, 1000, 768),
     'gemm_130x998x320': lambda: _case_gemm(130, 998, 320),      # scalar epilogue (N % 4 != 0)
@@ -105,6 +117,11 @@ CASES = {
     'conv1d_b8_256to128_t16': lambda: _case_conv1d(8, 256, 128, 16),
     'convt_b8_128to64_t32': lambda: _case_convt(8, 128, 64, 32),
     'nhwc_b4_64to96_20x22': lambda: _case_nhwc(4, 64, 96, 20, 22),
+    # mode 4 on both operands (the 1-D conv weight gradients): padding taps cross the run edges
+    'wgrad_b8_48to80_t64_k3': lambda: _case_wgrad1d(8, 48, 80, 64, 3, 1),
+    'wgrad_b6_130to70_t32_k3': lambda: _case_wgrad1d(6, 130, 70, 32, 3, 1),
+    'wgrad_b4_64to64_t96_k1': lambda: _case_wgrad1d(4, 64, 64, 96, 1, 0),
+    'wgrad_b4_32to40_t64_k5': lambda: _case_wgrad1d(4, 32, 40, 64, 5, 2),
 }
 
 
