@@ -9,6 +9,7 @@
 // 1-D convs are the H = 1 case; ConvTranspose1d's dgrad / wgrad are a plain conv forward /
 // this wgrad with the operands' roles exchanged (see a2m.autograd).
 #include <algorithm>
+#include <cstdlib>
 
 #include "a2m_internal.h"
 
@@ -43,6 +44,22 @@ __global__ void dgrad_pack_kernel(const float* w, int Co, int Ci, int kh, int kw
   }
 }
 
+// The dgrad of a stride-1 "same" conv1d is that conv1d of dY with W'[ci][co][j] = W[co][ci][ks-1-j]:
+// W' packed tap-chunked ([Ci][Co/CH][ks][CH], the k order of loader mode 5) so the engine runs it
+// as the forward's tap conv (the pipelined tile's halo / per-tap layouts) instead of a mode-3
+// gather over (co, tap)
+__global__ void dgrad_tap_pack_kernel(const float* w, int Co, int Ci, int ks, int ch, float* out) {
+  const int64_t total = (int64_t)Co * Ci * ks;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int tap = (int)(i % ks);
+    const int64_t t = i / ks;
+    const int ci = (int)(t % Ci), co = (int)(t / Ci);
+    const int cc = co / ch, cl = co - cc * ch;
+    out[(((int64_t)ci * (Co / ch) + cc) * ks + (ks - 1 - tap)) * ch + cl] = w[i];
+  }
+}
+
 }  // namespace a2m
 
 using namespace a2m;
@@ -69,6 +86,32 @@ int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
   }
   hipStream_t st = as_stream(stream);
   float* packed = static_cast<float*>(ws);
+  // 1-D, stride 1, 3 taps, pad 1, clips that tile the 64-row block: the tap conv (A2M_DGRAD_TAP=0:
+  // the phase GEMM below for every conv)
+  static const int tap_on = std::getenv("A2M_DGRAD_TAP") ? std::atoi(std::getenv("A2M_DGRAD_TAP")) : 1;
+  const int chunk = gemm_k_tile();
+  if (tap_on && H == 1 && kh == 1 && pad_h == 0 && stride_h == 1 && stride_w == 1 && kw == 3 && pad_w == 1 &&
+      Wo == W && W % 4 == 0 && 64 % W == 0 && Co % chunk == 0 &&
+      (reinterpret_cast<uintptr_t>(dy) % 16) == 0 && ((int64_t)Co * W) % 4 == 0) {
+    hipLaunchKernelGGL(dgrad_tap_pack_kernel,
+                       dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Co * Ci * kw, 256), 8192)), dim3(256), 0,
+                       st, w, Co, Ci, kw, chunk, packed);
+    A2M_LAUNCH_CHECK();
+    Gather A = dense_rk(packed, Co * kw);
+    Gather Bg{};
+    Bg.base = dy; Bg.bstride = 0;
+    Bg.sr0 = Co * W; Bg.R1 = 1; Bg.R2 = W; Bg.sk0 = W;
+    Bg.K1 = Bg.K2 = 1; Bg.divh = Bg.divw = 1; Bg.Lh = Bg.Lw = 1;
+    Bg.cw = -pad_w; Bg.tapconv = kw;
+    Epilogue E = epi_dense(dx, 0);
+    E.N1 = 1; E.N2 = W; E.so0 = (int)dxs_b; E.so1 = 0; E.so2 = (int)dxs_w; E.som = (int)dxs_c;
+    E.accumulate = accumulate;
+    int rc = gemm(A, Bg, E, Ci, B * W, Co * kw, 1, static_cast<char*>(ws) + pack_bytes, ws_bytes - pack_bytes, st);
+    if (rc == A2M_EWS)
+      set_error("conv_dgrad: workspace too small (%zu < %zu bytes)", ws_bytes,
+                pack_bytes + gemm_ws_bytes(Ci, B * W, Co * kw, 1));
+    return rc;
+  }
   for (int rh = 0; rh < stride_h; ++rh) {
     const int nuh = (H - rh + stride_h - 1) / stride_h;
     if (nuh <= 0) continue;
