@@ -435,7 +435,7 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
 }
 
 static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, int kquant = 1,
-                     bool conv_rows = false) {
+                     bool conv_rows = false, bool pipe64 = false) {
   static const int env_tile = env_int("A2M_GEMM_TILE", 0);
   static const int env_split = env_int("A2M_GEMM_SPLIT", 0);
   const int force_tile = g_override_tile ? g_override_tile : env_tile;
@@ -447,6 +447,9 @@ static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, in
   double best = 1e300;
   for (int tile : {64, 128}) {
     if (force_tile && tile != force_tile) continue;
+    // operands the fp32 pipelined 64x64 tile takes: the cost table is gemm_tile's, which the
+    // pipelined tile outruns -- kept to 64 (training iteration 66.0 -> 64.5 ms, r05_n)
+    if (!force_tile && pipe64 && tile != 64) continue;
     for (int s : cand_splits) {
       if (force_split && s != force_split) continue;
       const int kchunk = (int)(cdiv(cdiv(std::max(K, 1), s), KQ) * KQ);
@@ -478,8 +481,8 @@ static size_t split_ws_bytes(const Plan& p, int M, int N, int batch) {
 // the plan gemm() launches: the planner's, unless a tuned-table entry or an A2M_GEMM_PLAN_RULES
 // rule fixes the tile / split count for the shape
 static Plan launch_plan(int M, int N, int K, int batch, bool gathered, int prec, int kquant, bool rows6,
-                        int force_split) {
-  Plan p = plan_for(M, N, K, batch, gathered, prec, kquant, rows6);
+                        int force_split, bool pipe64 = false) {
+  Plan p = plan_for(M, N, K, batch, gathered, prec, kquant, rows6, pipe64);
   if (force_split > 0) {
     p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk * kquant) * p.bk * kquant);
     p.splits = (int)cdiv(K, p.kchunk);
@@ -505,10 +508,11 @@ size_t gemm_ws_bytes(int M, int N, int K, int batch) {
   for (bool gathered : {false, true})
     for (int prec : {0, 1, 2})
       for (bool rows6 : {false, true})
-        for (int kq : {1, 2, 3}) {
-          const Plan p = launch_plan(M, N, K, batch, gathered, prec, kq, rows6, 0);
-          if (p.splits > 1) need = std::max(need, split_ws_bytes(p, M, N, batch));
-        }
+        for (int kq : {1, 2, 3})
+          for (bool p64 : {false, true}) {
+            const Plan p = launch_plan(M, N, K, batch, gathered, prec, kq, rows6, 0, p64);
+            if (p.splits > 1) need = std::max(need, split_ws_bytes(p, M, N, batch));
+          }
   return need;
 }
 
@@ -595,8 +599,47 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   const int kquant = mb == 5 ? B.tapconv : 1;
   // gathered: row-vector staging (modes 2 / 3) or gathers; k-contiguous conv rows (mode 6) load
   // like dense rows
+  static const int ks2 = env_int("A2M_GEMM_KS2", 1);
+  // software-pipelined one-wave-per-SIMD tile (gemm_pipe.h; A2M_GEMM_PIPE=0 restores gemm_tile):
+  // fp32 64x64, dense weights x dense rows / channels-last rows / halo tap conv, every element
+  // offset below 2^29 floats (raw buffer loads)
+  static const int pipe_env = env_int("A2M_GEMM_PIPE", 1);
+  const int pipe_on = g_pipe_override >= 0 ? g_pipe_override : pipe_env;
+  auto below = [](int64_t v) { return v >= 0 && v < ((int64_t)1 << 29); };
+  bool pipe_ext = below((int64_t)(M - 1) * A.sr0 + K);
+  if (mb == 0) pipe_ext = pipe_ext && below((int64_t)(N - 1) * B.sr0 + K);
+  else if (mb == 6) pipe_ext = pipe_ext && below((int64_t)((N - 1) / (B.R1 * B.R2)) * B.sr0 + (int64_t)B.Lh * B.Lw * B.nhwc);
+  else if (mb == 5) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)(K / B.tapconv) * B.sk0);
+  else if (mb == 3) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)K * B.sk0);
+  // mode 3 in its plain form only: k = channel, rows (b, t) at unit stride in groups of 4
+  const bool rows3 = mb == 3 && B.K1 == 1 && B.K2 == 1 && B.R1 == 1 && B.ch == 0 && B.cw == 0 &&
+                     B.divh == 1 && B.divw == 1 && N % 4 == 0 &&
+                     ((B.R2 == 1 && B.sr0 == 1) || (B.R2 % 4 == 0 && B.ar2 == 1 && B.sw == 1 && B.Lw >= B.R2));
+  // mode 4 on both sides (the 1-D conv weight gradients): one k digit (K1 = 1) in runs of a
+  // multiple of the 32-k tile, every split a whole number of tiles, offsets below 2^29
+  auto runs4 = [&](const Gather& g, int R) {
+    const int64_t rmax = (int64_t)((R - 1) / (g.R1 * g.R2)) * g.sr0 +
+                         (int64_t)std::max(0, g.Lh - 1) * std::abs(g.sh) + g.Lw + (int64_t)(K / g.K2) * g.sk0;
+    return g.K1 == 1 && g.K2 % 32 == 0 && g.bk2 == 1 && g.sw == 1 && g.divh == 1 && g.divw == 1 &&
+           g.sr0 >= 0 && g.sk0 >= 0 && below(rmax);
+  };
+  static const int pipe4_env = env_int("A2M_GEMM_PIPE4", 1);
+  const bool m4_ok = pipe4_env && ma == 4 && mb == 4 && runs4(A, M) && runs4(B, N);
+  // A as a plain [K][M] operand (mode 3: rows at unit stride, loaded 4 at a time) with B dense or
+  // plain mode 3 (the weight gradients of the linears / graph layers)
+  static const int pipe_a3_env = env_int("A2M_GEMM_PIPE_A3", 1);
+  const bool plainA3 = ma == 3 && A.K1 == 1 && A.K2 == 1 && A.R1 == 1 && A.R2 == 1 && A.sr0 == 1 && A.ch == 0 &&
+                       A.cw == 0 && A.divh == 1 && A.divw == 1 && M % 4 == 0 && A.sk0 >= 0 &&
+                       below((int64_t)(M - 1) + (int64_t)K * A.sk0);
+  const bool pipe_a3 = pipe_a3_env && plainA3 &&
+                       ((mb == 0 && below((int64_t)(N - 1) * B.sr0 + K)) ||
+                        (rows3 && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)K * B.sk0)));
+  // the operand modes the fp32 pipelined tile takes (at a 64-row tile)
+  const bool tap5 = mb == 5 && B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 && 64 % B.R2 == 0;
+  const bool pipe_modes = (ma == 0 && (mb == 0 || mb == 6 || rows3 || tap5) && pipe_ext) || m4_ok || pipe_a3;
+  static const int pipe64_env = env_int("A2M_GEMM_PIPE64", 1);
   const Plan p = launch_plan(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || (mb >= 3 && mb != 6), prec,
-                             kquant, mb == 6, force_split);
+                             kquant, mb == 6, force_split, pipe64_env && pipe_on && prec == 0 && pipe_modes);
   // A2M_GEMM_HALO=0: mode 5 re-stores the window shifted for every tap (the round-3 loader)
   static const int halo_on = env_int("A2M_GEMM_HALO", 1);
   a.B.halo = halo_on && mb == 5 && prec == 0 && p.bm == 64 && B.tapconv == 3 &&
@@ -627,37 +670,10 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   a.vec4 = vec4_on && !a.mcontig && N % 4 == 0 &&
            (slab_out || (in_stride == 1 && in_len % 4 == 0 && outer4 && al16(E.out) &&
                          (!E.res1 || al16(E.res1)) && (!E.res2 || al16(E.res2))));
-  static const int ks2 = env_int("A2M_GEMM_KS2", 1);
-  // software-pipelined one-wave-per-SIMD tile (gemm_pipe.h; A2M_GEMM_PIPE=0 restores gemm_tile):
-  // fp32 64x64, dense weights x dense rows / channels-last rows / halo tap conv, every element
-  // offset below 2^29 floats (raw buffer loads)
-  static const int pipe_env = env_int("A2M_GEMM_PIPE", 1);
-  const int pipe_on = g_pipe_override >= 0 ? g_pipe_override : pipe_env;
-  auto below = [](int64_t v) { return v >= 0 && v < ((int64_t)1 << 29); };
-  bool pipe_ext = below((int64_t)(M - 1) * A.sr0 + K);
-  if (mb == 0) pipe_ext = pipe_ext && below((int64_t)(N - 1) * B.sr0 + K);
-  else if (mb == 6) pipe_ext = pipe_ext && below((int64_t)((N - 1) / (B.R1 * B.R2)) * B.sr0 + (int64_t)B.Lh * B.Lw * B.nhwc);
-  else if (mb == 5) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)(K / B.tapconv) * B.sk0);
-  else if (mb == 3) pipe_ext = pipe_ext && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)K * B.sk0);
-  // mode 3 in its plain form only: k = channel, rows (b, t) at unit stride in groups of 4
-  const bool rows3 = mb == 3 && B.K1 == 1 && B.K2 == 1 && B.R1 == 1 && B.ch == 0 && B.cw == 0 &&
-                     B.divh == 1 && B.divw == 1 && N % 4 == 0 &&
-                     ((B.R2 == 1 && B.sr0 == 1) || (B.R2 % 4 == 0 && B.ar2 == 1 && B.sw == 1 && B.Lw >= B.R2));
-  // mode 4 on both sides (the 1-D conv weight gradients): one k digit (K1 = 1) in runs of a
-  // multiple of the 32-k tile, every split a whole number of tiles, offsets below 2^29
-  auto runs4 = [&](const Gather& g, int R) {
-    const int64_t rmax = (int64_t)((R - 1) / (g.R1 * g.R2)) * g.sr0 +
-                         (int64_t)std::max(0, g.Lh - 1) * std::abs(g.sh) + g.Lw + (int64_t)(K / g.K2) * g.sk0;
-    return g.K1 == 1 && g.K2 % 32 == 0 && g.bk2 == 1 && g.sw == 1 && g.divh == 1 && g.divw == 1 &&
-           g.sr0 >= 0 && g.sk0 >= 0 && below(rmax);
-  };
-  static const int pipe4_env = env_int("A2M_GEMM_PIPE4", 1);
-  const bool pipe_m4 = pipe4_env && ma == 4 && mb == 4 && p.kchunk % 32 == 0 && runs4(A, M) && runs4(B, N);
+  const bool pipe_m4 = m4_ok && p.kchunk % 32 == 0;
   const bool pipe_launch = pipe_on && prec == 0 && p.bm == 64 &&
-                           ((ma == 0 && (mb == 0 || mb == 6 || rows3 ||
-                                         (mb == 5 && (a.B.halo || (B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 &&
-                                                                   64 % B.R2 == 0)))) && pipe_ext) ||
-                            pipe_m4);
+                           ((ma == 0 && (mb == 0 || mb == 6 || rows3 || (mb == 5 && (a.B.halo || tap5))) && pipe_ext) ||
+                            pipe_m4 || pipe_a3);
   // the bf16-operand pipelined tile (gemm_pipe_bf16.h): the same operand modes, 64-channel
   // k-tiles (mode 6: Ci % 64 == 0), no halo layout (mode 5 takes the per-tap stores)
   const bool pipe_bf16 = pipe_on && prec == 1 && p.bm == 64 && ma == 0 &&
@@ -703,7 +719,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     if (p.bm == 128) launch_tile<128, 128, 32, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
   } else {
-    if (pipe_launch) launch_pipe(a, mb, batch, stream);
+    if (pipe_launch) launch_pipe(a, ma, mb, batch, stream);
     else if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
     // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end

@@ -19,8 +19,9 @@
 // B operand modes: 0 dense k-contiguous rows, 3 row-contiguous [B][C][T] / [K][R] operands (the
 // 1x1 projections), 6 channels-last conv rows (Gather::nhwc), 5 the tap-chunked conv1d in the
 // halo layout (Gather::halo: 3 taps, pad 1, clips T >= 16 that tile the 64 rows), 4 k-contiguous
-// runs (the 1-D conv weight gradients, with A in mode 4 too).  Otherwise A is dense rows (mode 0;
-// the packed conv weights).
+// runs (the 1-D conv weight gradients, with A in mode 4 too).  A is dense rows (mode 0; the packed
+// conv weights), a plain [K][M] operand (mode 3, with B in mode 0 / 3: the weight gradients of the
+// linears and graph layers) or mode 4.
 #pragma once
 #include "gemm_kernel.h"
 
@@ -458,8 +459,9 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   const int kend = min(args.K, kbeg + args.kchunk);
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
 
-  static_assert(MA == 0 || (MA == 4 && MB == 4), "A in mode 4 only with B in mode 4");
-  typename std::conditional<MA == 4, PipeRuns, PipeRows>::type la;
+  static_assert(MA == 0 || (MA == 3 && (MB == 0 || MB == 3)) || (MA == 4 && MB == 4),
+                "A in mode 3 with B in mode 0 / 3, in mode 4 with B in mode 4");
+  typename std::conditional<MA == 4, PipeRuns, typename std::conditional<MA == 3, PipeRowsT, PipeRows>::type>::type la;
   la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
   using LB = typename std::conditional<
       MB == 5, typename std::conditional<TAPS, PipeTap<NT ? NT : 1>, PipeHalo>::type,
@@ -686,6 +688,6 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
 #endif
 }
 
-void launch_pipe(const GemmArgs& a, int mb, int batch, hipStream_t st);
+void launch_pipe(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st);
 
 }  // namespace a2m

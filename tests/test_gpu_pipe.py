@@ -54,6 +54,20 @@ def _case_gemm_kr(M, N, K):
     return run, A.double() @ Bt.double(), False
 
 
+def _case_gemm_at(M, N, K, b_rows):
+    """A as a plain [K][M] operand (mode 3), B dense [N][K] rows or [K][N] (mode 3): the weight
+    gradients of the linears and graph layers."""
+    At = _rand(K, M, seed=16)
+    B = _rand(N, K, seed=17) if b_rows else _rand(K, N, seed=18)
+    C = torch.empty(M, N, device=DEV)
+
+    def run():
+        from a2m import functional as F
+        return F.gemm(M, N, K, At, 1, M, B, K if b_rows else 1, 1 if b_rows else N, C, N, 1)
+    ref = At.double().t() @ (B.double().t() if b_rows else B.double())
+    return run, ref, False
+
+
 def _case_conv1d(B, Ci, Co, T):
     x = _rand(B, Ci, T, seed=5)
     w = _rand(Co, Ci, 3, seed=6, scale=(3 * Ci) ** -0.5)
@@ -117,6 +131,10 @@ CASES = {
     'conv1d_b8_256to128_t16': lambda: _case_conv1d(8, 256, 128, 16),
     'convt_b8_128to64_t32': lambda: _case_convt(8, 128, 64, 32),
     'nhwc_b4_64to96_20x22': lambda: _case_nhwc(4, 64, 96, 20, 22),
+    # A in mode 3 (plain [K][M]) with dense or mode-3 B
+    'gemm_at_128x1000x700_rows': lambda: _case_gemm_at(128, 1000, 700, True),
+    'gemm_at_64x64x20000_kr': lambda: _case_gemm_at(64, 64, 20000, False),
+    'gemm_at_256x2688x512_kr': lambda: _case_gemm_at(256, 2688, 512, False),
     # mode 4 on both operands (the 1-D conv weight gradients): padding taps cross the run edges
     'wgrad_b8_48to80_t64_k3': lambda: _case_wgrad1d(8, 48, 80, 64, 3, 1),
     'wgrad_b6_130to70_t32_k3': lambda: _case_wgrad1d(6, 130, 70, 32, 3, 1),
