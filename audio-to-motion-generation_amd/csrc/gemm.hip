@@ -676,10 +676,13 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                             pipe_m4 || pipe_a3);
   // the bf16-operand pipelined tile (gemm_pipe_bf16.h): the same operand modes, 64-channel
   // k-tiles (mode 6: Ci % 64 == 0), no halo layout (mode 5 takes the per-tap stores)
-  const bool pipe_bf16 = pipe_on && prec == 1 && p.bm == 64 && ma == 0 &&
-                         (mb == 0 || (mb == 6 && B.nhwc % 64 == 0) || rows3 ||
-                          (mb == 5 && B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 && 64 % B.R2 == 0)) &&
-                         pipe_ext;
+  // (and, as the fp32 tile, mode-4 runs on both sides -- runs of a multiple of its 64-k tile --
+  // and plain [K][M] A operands)
+  const bool pipe_bf16 = pipe_on && prec == 1 && p.bm == 64 &&
+                         ((ma == 0 && (mb == 0 || (mb == 6 && B.nhwc % 64 == 0) || rows3 ||
+                                       (mb == 5 && B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 && 64 % B.R2 == 0)) &&
+                           pipe_ext) ||
+                          (m4_ok && A.K2 % 64 == 0 && B.K2 % 64 == 0 && p.kchunk % 64 == 0) || pipe_a3);
   // ... and its halo layout for the 3-tap pad-1 convs over clips of T >= 16 (the window stored
   // once per chunk instead of once per tap); gemm_tile's bf16 tile takes the per-tap stores
   if (pipe_bf16 && halo_on && mb == 5 && B.tapconv == 3 && B.cw == -1 && B.R2 >= 16 && 64 % B.R2 == 0)
@@ -712,7 +715,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     }
   }
   if (prec == 1) {
-    if (pipe_bf16) launch_pipe_bf16(a, mb, batch, stream);
+    if (pipe_bf16) launch_pipe_bf16(a, ma, mb, batch, stream);
     else if (p.bm == 128) launch_tile<128, 128, 64, 1>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 64, 1>(a, ma, mb, batch, stream);
   } else if (prec == 2) {

@@ -87,6 +87,57 @@ struct PipeRowsH {
   }
 };
 
+// k-contiguous runs (mode 4, the 1-D conv weight gradients; PipeRuns' addressing with 64-k tiles,
+// K2 % 64 == 0): PipeRowsH's map, a quad across a run's edge loaded element by element
+struct PipeRunsH {
+  static constexpr int NST = 4;
+  __amdgpu_buffer_rsrc_t rs;
+  int rbase[4], w0[4];
+  bool rv[4];
+  int kq, lrow, knext, K, k0, k2t, K2, sk0, Lw;
+  __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
+    rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
+    kq = (tid & 15) * 4;
+    lrow = tid >> 4;
+    K = KK;
+    knext = kbeg;
+    K2 = g.K2; sk0 = g.sk0; Lw = g.Lw;
+    k0 = kbeg / K2;
+    k2t = kbeg - k0 * K2;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const RowInfo ri = row_info(g, row0 + lrow + 16 * p, R);
+      rv[p] = ri.valid && ri.h >= 0 && ri.h < g.Lh;
+      rbase[p] = ri.base + ri.h * g.sh + ri.w;
+      w0[p] = ri.w;
+    }
+  }
+  __device__ __forceinline__ void load(float4 (&r)[4], int p) {
+    const int w = w0[p] + k2t + kq;
+    const int e0 = rbase[p] + k0 * sk0 + k2t + kq;
+    const bool inb = rv[p] && knext < K;
+    const bool full = inb && w >= 0 && w + 3 < Lw;
+    r[p] = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
+    if (inb && !full) {
+      float e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        e[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                   rs, (unsigned)(w + j) < (unsigned)Lw ? (uint32_t)(e0 + j) * 4u : kPipeOOB, 0, 0));
+      r[p] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+    if (p == 3) {
+      knext += 64;
+      k2t += 64;
+      if (k2t == K2) { k2t = 0; ++k0; }
+    }
+  }
+  __device__ __forceinline__ void store(float* st, const float4 (&r)[4], int s) const {
+    *reinterpret_cast<uint2*>(reinterpret_cast<__bf16*>(st) + (lrow + 16 * s) * kHK + kq) =
+        make_uint2(hpack2(r[s].x, r[s].y), hpack2(r[s].z, r[s].w));
+  }
+};
+
 // channels-last conv rows (mode 6): a k-tile is 64 channels of one tap (i, j); each row reads its
 // pixel (h + i, w + j) if it lies in the image
 struct PipeNhwcH {
@@ -309,7 +360,7 @@ __device__ __forceinline__ void pipe_step_h(floatx16& acc, bf16x8 (&fa0)[2], bf1
   A2M_SB();
 }
 
-template <int MB, int NT = 0>   // MB 5: NT = taps (1-3)
+template <int MB, int NT = 0, int MA = 0>   // MB 5: NT = taps (1-3); MA: A's mode (0, 3 or 4)
 __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
   span_begin(args.ts);
   constexpr int BM = 64;
@@ -332,12 +383,16 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
   const int kend = min(args.K, kbeg + args.kchunk);
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + 63) / 64 : 0);
 
-  PipeRowsH la;
+  static_assert(MA == 0 || (MA == 3 && (MB == 0 || MB == 3)) || (MA == 4 && MB == 4),
+                "A in mode 3 with B in mode 0 / 3, in mode 4 with B in mode 4");
+  using LA = typename std::conditional<MA == 4, PipeRunsH, typename std::conditional<MA == 3, PipeRowsTH, PipeRowsH>::type>::type;
+  LA la;
   la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
   using LB = typename std::conditional<
       MB == 5, typename std::conditional<TAPS, PipeTapH<NT ? NT : 1>, PipeHaloH>::type,
       typename std::conditional<MB == 6, PipeNhwcH,
-                                typename std::conditional<MB == 3, PipeRowsTH, PipeRowsH>::type>::type>::type;
+                                typename std::conditional<MB == 3, PipeRowsTH,
+                                                          typename std::conditional<MB == 4, PipeRunsH, PipeRowsH>::type>::type>::type>::type;
   LB lb;
   lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
 
@@ -490,7 +545,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
 #pragma unroll
     for (int d = 1; d < D; ++d) { load4(la, xa[d]); load4(lb, xb[d]); }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) la.store(As, xa[0], s);
+    for (int s = 0; s < LA::NST; ++s) la.store(As, xa[0], s);
 #pragma unroll
     for (int s = 0; s < LB::NST; ++s) lb.store(Bs, xb[0], s);
     load4(la, xa[0]);
@@ -504,7 +559,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
       float* const nB = Bs + n;
       pipe_step_h(acc, fa0, fb0, H(As + c) + arow, H(Bs + c) + brow, H(nA) + arow, H(nB) + brow, [&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        if constexpr (s < 4) la.store(nA, xa[Q], s);
+        if constexpr (s < 4) { if constexpr (s < LA::NST) la.store(nA, xa[Q], s); }
         else if constexpr (s < 4 + LB::NST) lb.store(nB, xb[Q], s - 4);
         else if constexpr (s >= 8 && s < 12) { if (!(A2M_PIPE_HALF_A && (s & 1))) la.load(xa[Q], s - 8); }
         else if constexpr (s >= 12) lb.load(xb[Q], s - 12);
@@ -529,6 +584,6 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
   span_end(args.ts);
 }
 
-void launch_pipe_bf16(const GemmArgs& a, int mb, int batch, hipStream_t st);
+void launch_pipe_bf16(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st);
 
 }  // namespace a2m
