@@ -49,14 +49,16 @@ __global__ void dgrad_pack_kernel(const float* w, int Co, int Ci, int kh, int kw
 // as the forward's tap conv (the pipelined tile's halo / per-tap layouts) instead of a mode-3
 // gather over (co, tap)
 __global__ void dgrad_tap_pack_kernel(const float* w, int Co, int Ci, int ks, int ch, float* out) {
-  const int64_t total = (int64_t)Co * Ci * ks;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int tap = (int)(i % ks);
-    const int64_t t = i / ks;
-    const int ci = (int)(t % Ci), co = (int)(t / Ci);
-    const int cc = co / ch, cl = co - cc * ch;
-    out[(((int64_t)ci * (Co / ch) + cc) * ks + (ks - 1 - tap)) * ch + cl] = w[i];
+  // one block row per ci (blockIdx.y), 32-bit index math, the packed row written contiguously
+  // (dgrad_pack_kernel's layout of the work)
+  const int ci = blockIdx.y;
+  const int per = Co * ks;   // packed row length (< 2^31: host)
+  const int cch = ks * ch;
+  float* orow = out + (int64_t)ci * per;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < per; o += gridDim.x * blockDim.x) {
+    const int cc = o / cch, rem = o - cc * cch;
+    const int j = rem / ch, cl = rem - j * ch;
+    orow[o] = w[((int64_t)(cc * ch + cl) * Ci + ci) * ks + (ks - 1 - j)];
   }
 }
 
@@ -93,9 +95,8 @@ int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
   if (tap_on && H == 1 && kh == 1 && pad_h == 0 && stride_h == 1 && stride_w == 1 && kw == 3 && pad_w == 1 &&
       Wo == W && W % 4 == 0 && 64 % W == 0 && Co % chunk == 0 &&
       (reinterpret_cast<uintptr_t>(dy) % 16) == 0 && ((int64_t)Co * W) % 4 == 0) {
-    hipLaunchKernelGGL(dgrad_tap_pack_kernel,
-                       dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Co * Ci * kw, 256), 8192)), dim3(256), 0,
-                       st, w, Co, Ci, kw, chunk, packed);
+    hipLaunchKernelGGL(dgrad_tap_pack_kernel, dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Co * kw, 256), 64), (unsigned)Ci),
+                       dim3(256), 0, st, w, Co, Ci, kw, chunk, packed);
     A2M_LAUNCH_CHECK();
     Gather A = dense_rk(packed, Co * kw);
     Gather Bg{};
