@@ -616,11 +616,11 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                      B.divh == 1 && B.divw == 1 && N % 4 == 0 &&
                      ((B.R2 == 1 && B.sr0 == 1) || (B.R2 % 4 == 0 && B.ar2 == 1 && B.sw == 1 && B.Lw >= B.R2));
   // mode 4 on both sides (the 1-D conv weight gradients): one k digit (K1 = 1) in runs of a
-  // multiple of the 32-k tile, every split a whole number of tiles, offsets below 2^29
+  // multiple of 4, every split a whole number of k-tiles, offsets below 2^29
   auto runs4 = [&](const Gather& g, int R) {
     const int64_t rmax = (int64_t)((R - 1) / (g.R1 * g.R2)) * g.sr0 +
                          (int64_t)std::max(0, g.Lh - 1) * std::abs(g.sh) + g.Lw + (int64_t)(K / g.K2) * g.sk0;
-    return g.K1 == 1 && g.K2 % 32 == 0 && g.bk2 == 1 && g.sw == 1 && g.divh == 1 && g.divw == 1 &&
+    return g.K1 == 1 && g.K2 % 4 == 0 && g.bk2 == 1 && g.sw == 1 && g.divh == 1 && g.divw == 1 &&
            g.sr0 >= 0 && g.sk0 >= 0 && below(rmax);
   };
   static const int pipe4_env = env_int("A2M_GEMM_PIPE4", 1);
@@ -682,7 +682,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
                          ((ma == 0 && (mb == 0 || (mb == 6 && B.nhwc % 64 == 0) || rows3 ||
                                        (mb == 5 && B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 && 64 % B.R2 == 0)) &&
                            pipe_ext) ||
-                          (m4_ok && A.K2 % 64 == 0 && B.K2 % 64 == 0 && p.kchunk % 64 == 0) || pipe_a3);
+                          (m4_ok && p.kchunk % 64 == 0) || pipe_a3);
   // ... and its halo layout for the 3-tap pad-1 convs over clips of T >= 16 (the window stored
   // once per chunk instead of once per tap); gemm_tile's bf16 tile takes the per-tap stores
   if (pipe_bf16 && halo_on && mb == 5 && B.tapconv == 3 && B.cw == -1 && B.R2 >= 16 && 64 % B.R2 == 0)

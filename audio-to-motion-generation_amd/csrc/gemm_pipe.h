@@ -92,15 +92,16 @@ struct PipeRows {
 
 // k-contiguous runs (mode 4, the weight-gradient operands of the 1-D convs): element (r, k) at
 // r0 * sr0 + h * sh + w + k0 * sk0 with k = k0 * K2 + k2, w = r2 * ar2 + cw + k2 (h = r1 * ar1 + ch,
-// K1 = 1), zero where w falls outside [0, Lw) or h outside [0, Lh).  K2 % 32 == 0 (host), so a
-// k-tile is one run: k0 and the run offset are uniform, and each lane's quad is one float4 unless
-// it crosses the row's edge (the padding taps), where it loads element by element.  Thread map
-// and LDS layout of PipeRows, so the stages hold what gemm_tile's mode-4 loader stores
+// K1 = 1), zero where w falls outside [0, Lw) or h outside [0, Lh).  K2 % 4 == 0 (host), so a
+// lane's quad of k lies in one run (each lane tracks its own run k0 and offset k2, the tile's 32 k
+// may span several short runs); the quad is one float4 unless it crosses the row's edge (the
+// padding taps), where it loads element by element.  Thread map and LDS layout of PipeRows, so
+// the stages hold what gemm_tile's mode-4 loader stores
 struct PipeRuns {
   __amdgpu_buffer_rsrc_t rs;
   int rbase[2], w0[2];   // element offset of the thread's rows at (k0, k2) = (0, 0); their w origin
   bool rv[2];
-  int kq, lrow, knext, K, k0, k2t, K2, sk0, Lw;
+  int kq, lrow, knext, K, k0, k2, K2, sk0, Lw;   // k0 / k2: this lane's quad at the next load
   __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
     rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
     kq = (tid & 7) * 4;
@@ -108,8 +109,8 @@ struct PipeRuns {
     K = KK;
     knext = kbeg;
     K2 = g.K2; sk0 = g.sk0; Lw = g.Lw;
-    k0 = kbeg / K2;
-    k2t = kbeg - k0 * K2;
+    k0 = (kbeg + kq) / K2;
+    k2 = kbeg + kq - k0 * K2;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const RowInfo ri = row_info(g, row0 + lrow + 32 * p, R);
@@ -119,9 +120,9 @@ struct PipeRuns {
     }
   }
   __device__ __forceinline__ void load(float4 (&r)[2], int p) {
-    const int w = w0[p] + k2t + kq;                   // the quad's first element along the run
-    const int e0 = rbase[p] + k0 * sk0 + k2t + kq;    // its element offset (>= 0 where w >= 0)
-    const bool inb = rv[p] && knext < K;
+    const int w = w0[p] + k2;                   // the quad's first element along the run
+    const int e0 = rbase[p] + k0 * sk0 + k2;    // its element offset (>= 0 where w >= 0)
+    const bool inb = rv[p] && knext + kq < K;
     const bool full = inb && w >= 0 && w + 3 < Lw;
     r[p] = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
     if (inb && !full) {   // a quad across the row's edge: the elements inside it, the rest 0
@@ -134,8 +135,8 @@ struct PipeRuns {
     }
     if (p == 1) {
       knext += 32;
-      k2t += 32;
-      if (k2t == K2) { k2t = 0; ++k0; }
+      k2 += 32;
+      while (k2 >= K2) { k2 -= K2; ++k0; }
     }
   }
   __device__ __forceinline__ void store(float* st, const float4 (&r)[2], int p) const {

@@ -87,14 +87,15 @@ struct PipeRowsH {
   }
 };
 
-// k-contiguous runs (mode 4, the 1-D conv weight gradients; PipeRuns' addressing with 64-k tiles,
-// K2 % 64 == 0): PipeRowsH's map, a quad across a run's edge loaded element by element
+// k-contiguous runs (mode 4, the 1-D conv weight gradients; PipeRuns' addressing and per-lane run
+// position with 64-k tiles, K2 % 4 == 0): PipeRowsH's map, a quad across a run's edge loaded
+// element by element
 struct PipeRunsH {
   static constexpr int NST = 4;
   __amdgpu_buffer_rsrc_t rs;
   int rbase[4], w0[4];
   bool rv[4];
-  int kq, lrow, knext, K, k0, k2t, K2, sk0, Lw;
+  int kq, lrow, knext, K, k0, k2, K2, sk0, Lw;
   __device__ __forceinline__ void init(const Gather& g, int z, int row0, int R, int KK, int tid, int kbeg) {
     rs = pipe_rsrc(g.base + (int64_t)z * g.bstride);
     kq = (tid & 15) * 4;
@@ -102,8 +103,8 @@ struct PipeRunsH {
     K = KK;
     knext = kbeg;
     K2 = g.K2; sk0 = g.sk0; Lw = g.Lw;
-    k0 = kbeg / K2;
-    k2t = kbeg - k0 * K2;
+    k0 = (kbeg + kq) / K2;
+    k2 = kbeg + kq - k0 * K2;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const RowInfo ri = row_info(g, row0 + lrow + 16 * p, R);
@@ -113,9 +114,9 @@ struct PipeRunsH {
     }
   }
   __device__ __forceinline__ void load(float4 (&r)[4], int p) {
-    const int w = w0[p] + k2t + kq;
-    const int e0 = rbase[p] + k0 * sk0 + k2t + kq;
-    const bool inb = rv[p] && knext < K;
+    const int w = w0[p] + k2;
+    const int e0 = rbase[p] + k0 * sk0 + k2;
+    const bool inb = rv[p] && knext + kq < K;
     const bool full = inb && w >= 0 && w + 3 < Lw;
     r[p] = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
     if (inb && !full) {
@@ -128,8 +129,8 @@ struct PipeRunsH {
     }
     if (p == 3) {
       knext += 64;
-      k2t += 64;
-      if (k2t == K2) { k2t = 0; ++k0; }
+      k2 += 64;
+      while (k2 >= K2) { k2 -= K2; ++k0; }
     }
   }
   __device__ __forceinline__ void store(float* st, const float4 (&r)[4], int s) const {

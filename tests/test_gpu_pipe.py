@@ -140,6 +140,10 @@ CASES = {
     'wgrad_b6_130to70_t32_k3': lambda: _case_wgrad1d(6, 130, 70, 32, 3, 1),
     'wgrad_b4_64to64_t96_k1': lambda: _case_wgrad1d(4, 64, 64, 96, 1, 0),
     'wgrad_b4_32to40_t64_k5': lambda: _case_wgrad1d(4, 32, 40, 64, 5, 2),
+    # runs shorter than the k-tile (a tile spans several clips' runs)
+    'wgrad_b16_64to48_t16_k3': lambda: _case_wgrad1d(16, 64, 48, 16, 3, 1),
+    'wgrad_b24_32to36_t4_k3': lambda: _case_wgrad1d(24, 32, 36, 4, 3, 1),
+    'wgrad_b10_40to40_t20_k3': lambda: _case_wgrad1d(10, 40, 40, 20, 3, 1),
 }
 
 
