@@ -624,7 +624,12 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
            g.sr0 >= 0 && g.sk0 >= 0 && below(rmax);
   };
   static const int pipe4_env = env_int("A2M_GEMM_PIPE4", 1);
-  const bool m4_ok = pipe4_env && ma == 4 && mb == 4 && runs4(A, M) && runs4(B, N);
+  // ... and B as stride-2 runs (a stride-2 conv's input: gemm_tile gathers it, mode 1)
+  const bool runs_s2 = mb == 1 && B.K1 == 1 && B.K2 % 4 == 0 && B.bk2 == 2 && B.sw == 1 && B.divh == 1 &&
+                       B.divw == 1 && B.sr0 >= 0 && B.sk0 >= 0 &&
+                       below((int64_t)((N - 1) / (B.R1 * B.R2)) * B.sr0 + (int64_t)std::max(0, B.Lh - 1) * std::abs(B.sh) +
+                             B.Lw + (int64_t)(K / B.K2) * B.sk0);
+  const bool m4_ok = pipe4_env && ma == 4 && runs4(A, M) && ((mb == 4 && runs4(B, N)) || runs_s2);
   // A as a plain [K][M] operand (mode 3: rows at unit stride, loaded 4 at a time) with B dense or
   // plain mode 3 (the weight gradients of the linears / graph layers)
   static const int pipe_a3_env = env_int("A2M_GEMM_PIPE_A3", 1);

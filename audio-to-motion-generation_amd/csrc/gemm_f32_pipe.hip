@@ -8,6 +8,7 @@ namespace a2m {
 void launch_pipe(const GemmArgs& a, int ma, int mb, int batch, hipStream_t st) {
   const dim3 grid((unsigned)cdiv(a.N, 64), (unsigned)cdiv(a.M, 64), (unsigned)(batch * a.splits));
   if (mb == 4) { hipLaunchKernelGGL((gemm_pipe_kernel<4, 0, 4>), grid, dim3(256), 0, st, a); return; }
+  if (mb == 1) { hipLaunchKernelGGL((gemm_pipe_kernel<7, 0, 4>), grid, dim3(256), 0, st, a); return; }   // stride-2 runs
   if (ma == 3) {
     if (mb == 3) hipLaunchKernelGGL((gemm_pipe_kernel<3, 0, 3>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((gemm_pipe_kernel<0, 0, 3>), grid, dim3(256), 0, st, a);

@@ -96,7 +96,10 @@ struct PipeRows {
 // lane's quad of k lies in one run (each lane tracks its own run k0 and offset k2, the tile's 32 k
 // may span several short runs); the quad is one float4 unless it crosses the row's edge (the
 // padding taps), where it loads element by element.  Thread map and LDS layout of PipeRows, so
-// the stages hold what gemm_tile's mode-4 loader stores
+// the stages hold what gemm_tile's mode-4 loader stores.  S = 2: the runs of a stride-2 conv's input
+// (w = r2 * ar2 + cw + 2 k2, gemm_tile's mode 1 for it): a quad's 4 elements from two float4 (their
+// even elements) unless it reaches past the row, element by element there
+template <int S = 1>
 struct PipeRuns {
   __amdgpu_buffer_rsrc_t rs;
   int rbase[2], w0[2];   // element offset of the thread's rows at (k0, k2) = (0, 0); their w origin
@@ -120,17 +123,23 @@ struct PipeRuns {
     }
   }
   __device__ __forceinline__ void load(float4 (&r)[2], int p) {
-    const int w = w0[p] + k2;                   // the quad's first element along the run
-    const int e0 = rbase[p] + k0 * sk0 + k2;    // its element offset (>= 0 where w >= 0)
+    const int w = w0[p] + S * k2;                   // the quad's first element along the run
+    const int e0 = rbase[p] + k0 * sk0 + S * k2;    // its element offset (>= 0 where w >= 0)
     const bool inb = rv[p] && knext + kq < K;
-    const bool full = inb && w >= 0 && w + 3 < Lw;
-    r[p] = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
+    const bool full = inb && w >= 0 && w + 4 * S - 1 < Lw;
+    if constexpr (S == 1) {
+      r[p] = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
+    } else {
+      const float4 lo = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
+      const float4 hi = pipe_load(rs, full ? (uint32_t)(e0 + 4) * 4u : kPipeOOB);
+      r[p] = make_float4(lo.x, lo.z, hi.x, hi.z);
+    }
     if (inb && !full) {   // a quad across the row's edge: the elements inside it, the rest 0
       float e[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         e[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                   rs, (unsigned)(w + j) < (unsigned)Lw ? (uint32_t)(e0 + j) * 4u : kPipeOOB, 0, 0));
+                   rs, (unsigned)(w + S * j) < (unsigned)Lw ? (uint32_t)(e0 + S * j) * 4u : kPipeOOB, 0, 0));
       r[p] = make_float4(e[0], e[1], e[2], e[3]);
     }
     if (p == 1) {
@@ -460,15 +469,17 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemmArgs args) {
   const int kend = min(args.K, kbeg + args.kchunk);
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0);
 
-  static_assert(MA == 0 || (MA == 3 && (MB == 0 || MB == 3)) || (MA == 4 && MB == 4),
-                "A in mode 3 with B in mode 0 / 3, in mode 4 with B in mode 4");
-  typename std::conditional<MA == 4, PipeRuns, typename std::conditional<MA == 3, PipeRowsT, PipeRows>::type>::type la;
+  // MB 7: stride-2 runs (PipeRuns<2>; gemm_tile's mode 1 for them)
+  static_assert(MA == 0 || (MA == 3 && (MB == 0 || MB == 3)) || (MA == 4 && (MB == 4 || MB == 7)),
+                "A in mode 3 with B in mode 0 / 3, in mode 4 with B in runs");
+  typename std::conditional<MA == 4, PipeRuns<1>, typename std::conditional<MA == 3, PipeRowsT, PipeRows>::type>::type la;
   la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
   using LB = typename std::conditional<
       MB == 5, typename std::conditional<TAPS, PipeTap<NT ? NT : 1>, PipeHalo>::type,
       typename std::conditional<MB == 6, PipeNhwc,
                                 typename std::conditional<MB == 3, PipeRowsT,
-                                                          typename std::conditional<MB == 4, PipeRuns, PipeRows>::type>::type>::type>::type;
+                                                          typename std::conditional<MB == 4, PipeRuns<1>,
+                                                                                    typename std::conditional<MB == 7, PipeRuns<2>, PipeRows>::type>::type>::type>::type>::type;
   LB lb;
   lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
 

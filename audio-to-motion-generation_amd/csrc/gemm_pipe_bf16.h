@@ -89,7 +89,8 @@ struct PipeRowsH {
 
 // k-contiguous runs (mode 4, the 1-D conv weight gradients; PipeRuns' addressing and per-lane run
 // position with 64-k tiles, K2 % 4 == 0): PipeRowsH's map, a quad across a run's edge loaded
-// element by element
+// element by element (S = 2: stride-2 runs, as PipeRuns<2>)
+template <int S = 1>
 struct PipeRunsH {
   static constexpr int NST = 4;
   __amdgpu_buffer_rsrc_t rs;
@@ -114,17 +115,23 @@ struct PipeRunsH {
     }
   }
   __device__ __forceinline__ void load(float4 (&r)[4], int p) {
-    const int w = w0[p] + k2;
-    const int e0 = rbase[p] + k0 * sk0 + k2;
+    const int w = w0[p] + S * k2;
+    const int e0 = rbase[p] + k0 * sk0 + S * k2;
     const bool inb = rv[p] && knext + kq < K;
-    const bool full = inb && w >= 0 && w + 3 < Lw;
-    r[p] = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
+    const bool full = inb && w >= 0 && w + 4 * S - 1 < Lw;
+    if constexpr (S == 1) {
+      r[p] = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
+    } else {
+      const float4 lo = pipe_load(rs, full ? (uint32_t)e0 * 4u : kPipeOOB);
+      const float4 hi = pipe_load(rs, full ? (uint32_t)(e0 + 4) * 4u : kPipeOOB);
+      r[p] = make_float4(lo.x, lo.z, hi.x, hi.z);
+    }
     if (inb && !full) {
       float e[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         e[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                   rs, (unsigned)(w + j) < (unsigned)Lw ? (uint32_t)(e0 + j) * 4u : kPipeOOB, 0, 0));
+                   rs, (unsigned)(w + S * j) < (unsigned)Lw ? (uint32_t)(e0 + S * j) * 4u : kPipeOOB, 0, 0));
       r[p] = make_float4(e[0], e[1], e[2], e[3]);
     }
     if (p == 3) {
@@ -384,16 +391,18 @@ __global__ __launch_bounds__(256) void gemm_pipe_bf16_kernel(GemmArgs args) {
   const int kend = min(args.K, kbeg + args.kchunk);
   const int nk = __builtin_amdgcn_readfirstlane(kbeg < kend ? (kend - kbeg + 63) / 64 : 0);
 
-  static_assert(MA == 0 || (MA == 3 && (MB == 0 || MB == 3)) || (MA == 4 && MB == 4),
-                "A in mode 3 with B in mode 0 / 3, in mode 4 with B in mode 4");
-  using LA = typename std::conditional<MA == 4, PipeRunsH, typename std::conditional<MA == 3, PipeRowsTH, PipeRowsH>::type>::type;
+  // MB 7: stride-2 runs (PipeRunsH<2>; gemm_tile's mode 1 for them)
+  static_assert(MA == 0 || (MA == 3 && (MB == 0 || MB == 3)) || (MA == 4 && (MB == 4 || MB == 7)),
+                "A in mode 3 with B in mode 0 / 3, in mode 4 with B in runs");
+  using LA = typename std::conditional<MA == 4, PipeRunsH<1>, typename std::conditional<MA == 3, PipeRowsTH, PipeRowsH>::type>::type;
   LA la;
   la.init(args.A, batch, m0, args.M, args.K, tid, kbeg);
   using LB = typename std::conditional<
       MB == 5, typename std::conditional<TAPS, PipeTapH<NT ? NT : 1>, PipeHaloH>::type,
       typename std::conditional<MB == 6, PipeNhwcH,
                                 typename std::conditional<MB == 3, PipeRowsTH,
-                                                          typename std::conditional<MB == 4, PipeRunsH, PipeRowsH>::type>::type>::type>::type;
+                                                          typename std::conditional<MB == 4, PipeRunsH<1>,
+                                                                                    typename std::conditional<MB == 7, PipeRunsH<2>, PipeRowsH>::type>::type>::type>::type>::type;
   LB lb;
   lb.init(args.B, batch, n0, args.N, args.K, tid, kbeg);
 

@@ -2,7 +2,8 @@
 -- against gemm_tile, the engine's reference tile, on every operand mode they take: dense rows
 (mode 0), row-contiguous [K][N] operands (mode 3), the tap-chunked conv1d (mode 5, three taps)
 and ConvTranspose phases (mode 5, two taps with a shift), channels-last conv rows (mode 6), the
-1-D conv weight gradients (mode 4 on both sides; fp32 only, bf16 takes gemm_tile); ragged M / N / K, one and several split-K slabs, float4 and scalar epilogues.
+1-D conv weight gradients (mode-4 runs on both sides, x as stride-2 runs for stride-2 convs), plain
+[K][M] A operands; ragged M / N / K, one and several split-K slabs, float4 and scalar epilogues.
 
 Both tiles compute the same products in the same order, so the results are bitwise equal, except
 fp32 dense rows, whose gemm_tile path is the two-wave-group tile (KS = 2: the k halves summed in a
@@ -110,15 +111,15 @@ def _case_nhwc(B, Ci, Co, H, W):
     return run, ref, False
 
 
-def _case_wgrad1d(B, Ci, Co, T, k, pad):
-    Tout = T + 2 * pad - k + 1
+def _case_wgrad1d(B, Ci, Co, T, k, pad, stride=1):
+    Tout = (T + 2 * pad - k) // stride + 1
     x = _rand(B, Ci, T, seed=14)
     dy = _rand(B, Co, Tout, seed=15)
 
     def run():
         from a2m import functional as F
-        return F.conv_wgrad(dy, x, (Co, Ci, k), 1, pad)
-    ref = torch.nn.grad.conv1d_weight(x.double(), (Co, Ci, k), dy.double(), padding=pad)
+        return F.conv_wgrad(dy, x, (Co, Ci, k), stride, pad)
+    ref = torch.nn.grad.conv1d_weight(x.double(), (Co, Ci, k), dy.double(), stride=stride, padding=pad)
     return run, ref, False
 
 
@@ -144,6 +145,10 @@ CASES = {
     'wgrad_b16_64to48_t16_k3': lambda: _case_wgrad1d(16, 64, 48, 16, 3, 1),
     'wgrad_b24_32to36_t4_k3': lambda: _case_wgrad1d(24, 32, 36, 4, 3, 1),
     'wgrad_b10_40to40_t20_k3': lambda: _case_wgrad1d(10, 40, 40, 20, 3, 1),
+    # stride-2 convs: x read as stride-2 runs (gemm_tile gathers them, mode 1)
+    'wgrad_s2_b8_48to64_t64_k4': lambda: _case_wgrad1d(8, 48, 64, 64, 4, 1, 2),
+    'wgrad_s2_b12_40to36_t32_k3': lambda: _case_wgrad1d(12, 40, 36, 32, 3, 1, 2),
+    'wgrad_s2_b16_64to64_t16_k4': lambda: _case_wgrad1d(16, 64, 64, 16, 4, 1, 2),
 }
 
 
