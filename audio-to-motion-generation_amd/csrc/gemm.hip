@@ -642,9 +642,16 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   // the operand modes the fp32 pipelined tile takes (at a 64-row tile)
   const bool tap5 = mb == 5 && B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 && 64 % B.R2 == 0;
   const bool pipe_modes = (ma == 0 && (mb == 0 || mb == 6 || rows3 || tap5) && pipe_ext) || m4_ok || pipe_a3;
-  static const int pipe64_env = env_int("A2M_GEMM_PIPE64", 1);
+  // A2M_GEMM_PIPE64: 0 off, 1 fp32 launches only, 2 (default) also bf16's training modes (mode-4 /
+  // plain mode-3 A: bf16 B=32 training kernel time 43.0 -> 41.7 ms a step, r05_p)
+  static const int pipe64_env = env_int("A2M_GEMM_PIPE64", 2);
   const Plan p = launch_plan(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || (mb >= 3 && mb != 6), prec,
-                             kquant, mb == 6, force_split, pipe64_env && pipe_on && prec == 0 && pipe_modes);
+                             kquant, mb == 6, force_split,
+                             pipe64_env && pipe_on &&
+                                 ((prec == 0 && pipe_modes) ||
+                                  // bf16: the training modes only (its planner table was refitted on the
+                                  // inference launches with the bf16 pipelined tile in place)
+                                  (prec == 1 && pipe64_env >= 2 && (m4_ok || pipe_a3))));
   // A2M_GEMM_HALO=0: mode 5 re-stores the window shifted for every tap (the round-3 loader)
   static const int halo_on = env_int("A2M_GEMM_HALO", 1);
   a.B.halo = halo_on && mb == 5 && prec == 0 && p.bm == 64 && B.tapconv == 3 &&
