@@ -113,6 +113,48 @@ int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
                 pack_bytes + gemm_ws_bytes(Ci, B * W, Co * kw, 1));
     return rc;
   }
+  // 1-D, stride s > 1 with s * Wo == W: dX is the ConvTranspose1d of dY with W read as its
+  // [in = Co][out = Ci][k] weight -- per output phase a tap conv of dY (the eval ConvTranspose's
+  // tap-chunked pack and phases), clips of Wo rows that tile the 64-row block
+  if (tap_on && H == 1 && kh == 1 && pad_h == 0 && stride_h == 1 && stride_w > 1 && stride_w * Wo == W &&
+      Wo % 4 == 0 && 64 % Wo == 0 && Co % chunk == 0 && (reinterpret_cast<uintptr_t>(dy) % 16) == 0) {
+    bool shifts_ok = true;
+    for (int r = 0; r < stride_w; ++r) {
+      const PhaseTaps tw = phase_taps_h(r, kw, stride_w, pad_w);
+      if (tw.n == 0) continue;
+      const int cw = (r + pad_w - tw.k0) / stride_w - tw.n + 1;
+      shifts_ok = shifts_ok && tw.n <= 3 && cw > -Wo && cw + tw.n - 1 < Wo;
+    }
+    if (shifts_ok) {
+      int rc = a2m_convt1d_tap_pack_f32(w, Co, Ci, kw, stride_w, pad_w, chunk, packed, stream);
+      if (rc) return rc;
+      size_t off = 0;
+      for (int r = 0; r < stride_w; ++r) {
+        const PhaseTaps tw = phase_taps_h(r, kw, stride_w, pad_w);
+        Epilogue E = epi_dense(dx + r * dxs_w, 0);
+        E.N1 = 1; E.N2 = Wo; E.so0 = (int)dxs_b; E.so1 = 0; E.so2 = (int)(stride_w * dxs_w); E.som = (int)dxs_c;
+        E.accumulate = accumulate;
+        if (tw.n == 0) {   // no tap reaches this phase: zeros (or nothing added)
+          rc = gemm(dense_rk(packed, 1), dense_rk(dy, 1), E, Ci, B * Wo, 0, 1, nullptr, 0, st);
+          if (rc) return rc;
+          continue;
+        }
+        Gather Bg{};
+        Bg.base = dy; Bg.bstride = 0;
+        Bg.sr0 = Co * Wo; Bg.R1 = 1; Bg.R2 = Wo; Bg.sk0 = Wo;
+        Bg.K1 = Bg.K2 = 1; Bg.divh = Bg.divw = 1; Bg.Lh = Bg.Lw = 1;
+        Bg.cw = (r + pad_w - tw.k0) / stride_w - tw.n + 1; Bg.tapconv = tw.n;
+        rc = gemm(dense_rk(packed + off, tw.n * Co), Bg, E, Ci, B * Wo, tw.n * Co, 1,
+                  static_cast<char*>(ws) + pack_bytes, ws_bytes - pack_bytes, st);
+        if (rc == A2M_EWS)
+          set_error("conv_dgrad: workspace too small (%zu < %zu bytes)", ws_bytes,
+                    pack_bytes + gemm_ws_bytes(Ci, B * Wo, tw.n * Co, 1));
+        if (rc) return rc;
+        off += (size_t)Ci * tw.n * Co;
+      }
+      return A2M_OK;
+    }
+  }
   for (int rh = 0; rh < stride_h; ++rh) {
     const int nuh = (H - rh + stride_h - 1) / stride_h;
     if (nuh <= 0) continue;

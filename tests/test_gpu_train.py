@@ -644,3 +644,28 @@ def test_reference_loop_body_with_torch_adam(g_state, d_state):
     assert np.all(rg[1:] < 5e-2) and rd < 5e-2
     a, b = np.abs(fp_after.cpu().numpy()).max(), np.abs(ref['fake_pose_after']).max()
     assert np.isfinite(fp_after.cpu().numpy()).all() and 0.5 < a / b < 2.0
+
+
+@pytest.mark.parametrize('B,Ci,Co,T,k,s,p', [
+    (8, 48, 64, 64, 3, 1, 1),     # stride 1, 3 taps: the tap conv of dY (halo layout)
+    (6, 40, 96, 16, 3, 1, 1),
+    (8, 48, 64, 64, 4, 2, 1),     # stride 2: the ConvTranspose phases (2 + 2 taps)
+    (12, 40, 32, 32, 3, 2, 1),    # stride 2, k 3: phases of 1 and 2 taps
+    (4, 64, 64, 128, 4, 2, 1),
+    (5, 24, 40, 60, 3, 1, 1),     # clips that do not tile 64 rows: the phase GEMM
+])
+@pytest.mark.parametrize('accumulate', [False, True])
+def test_conv1d_dgrad_paths(B, Ci, Co, T, k, s, p, accumulate):
+    """conv1d data gradient on each path a2m_conv2d_dgrad_f32 takes, against the fp64 gradient
+    (and accumulating into an existing dx)."""
+    from a2m import functional as F
+    Tout = (T + 2 * p - k) // s + 1
+    dy = _r(B, Co, Tout, seed=31).to(DEV)
+    w = _r(Co, Ci, k, seed=32, scale=(k * Co) ** -0.5).to(DEV)
+    base = _r(B, Ci, T, seed=33).to(DEV)
+    dx = base.clone() if accumulate else None
+    out = F.conv_dgrad(dy, w, (B, Ci, T), s, p, dx=dx, accumulate=accumulate)
+    ref = torch.nn.grad.conv1d_input((B, Ci, T), w.double(), dy.double(), stride=s, padding=p)
+    if accumulate:
+        ref = ref + base.double()
+    assert rel_err(out.double().cpu(), ref.cpu()) < TOL
