@@ -1,5 +1,5 @@
 # bf16 training with the training-mode launches kept on the 64x64 pipelined tile (A2M_GEMM_PIPE64=2)
-# against the default: kernel time per step from traces (the wall time follows the dynamic schedule)
+# against the default: kernel time per step from traces (the wall time varies run to run with fixed work)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 # bf16 B=32 training kernel traces with the training-mode pipelined tiles off / on: per-family
-# kernel time per step and launch counts (the iteration's wall time varies with the dynamic GAN
-# schedule's branch decisions, the kernel sums per launch do not)
+# kernel time per step and launch counts (the iteration's wall time varies run to run with fixed
+# work -- the gaps between its short kernels -- the kernel sums do not)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

@@ -1,4 +1,4 @@
-# repeated training-iteration lines on one box (the bf16 B=32 wall time follows the dynamic schedule)
+# repeated training-iteration lines on one box (the bf16 B=32 wall time varies run to run with fixed work)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 for i in 1 2 3; do
