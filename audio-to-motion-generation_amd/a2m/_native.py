@@ -74,10 +74,11 @@ SIGNATURES = {
                                             U64, I32, F32, P, I64, I64, P, P, P, SZ, P]),
     'a2m_bn_train_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, I32, P, P, P, P, F32, I32,
                                             U64, I32, F32, P, P, P, P, P, SZ, P]),
-    'a2m_bn_eval_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, P, P, F32, I32, F32, P, I64, I64,
-                                           P, P, P]),
-    'a2m_bn_eval_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, I32, P, P, P, P, I32, F32,
-                                           P, P, P, P, P, SZ, P]),
+    'a2m_bn_eval_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, P, P, P, F32, F32, I32, U64, I32, F32,
+                                           P, I64, I64, P, P, P]),
+    'a2m_bn_eval_bwd_f32': (ctypes.c_int, [P, I64, I64, P, I64, I64, I32, I32, I32, P, P, P, P, F32, I32, U64,
+                                           I32, F32, P, P, P, P, P, SZ, P]),
+    'a2m_set_dropout_seed_offset': (ctypes.c_int, [P]),
     'a2m_bn_sync_stats_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, F32, I32, U64, P, P, SZ, P]),
     'a2m_bn_sync_apply_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, I64, P, P, P, P, F32, F32, F32,
                                              I32, U64, I32, F32, P, I64, I64, P, P, P]),
@@ -116,6 +117,7 @@ SIGNATURES = {
     'a2m_diff_time_f32': (ctypes.c_int, [P, I32, I32, I32, P, P]),
     'a2m_diff_time_bwd_f32': (ctypes.c_int, [P, I32, I32, I32, P, I32, P]),
     'a2m_adam_f32': (ctypes.c_int, [P, P, P, P, I64, F32, F32, F32, F32, F32, I32, P]),
+    'a2m_adam_dev_f32': (ctypes.c_int, [P, P, P, P, I64, P, F32, F32, F32, F32, P, P]),
     'a2m_gather_segments_f32': (ctypes.c_int, [P, P, P, I32, P, P]),
     'a2m_gemm_f32': (ctypes.c_int, [I32, I32, I32, I32, I32, I32, P, I64, I64, I64, I64, P, I64, I64, I64,
                                     I64, I64, P, I64, I64, I64, I64, P, F32, I32, P, SZ, P]),

@@ -96,37 +96,42 @@ class _deferred_batch_counters:
 
 def _bn_fwd(raw, gamma, beta, cfg, p, mode, seed, act, slope):
     """BatchNorm (+ dropout) + activation of a conv output: batch statistics in training mode,
-    the running statistics (fixed, not updated; no dropout) in eval mode."""
+    the running statistics (fixed, not updated) in eval mode; dropout follows its own module."""
     if cfg['eval']:
-        return F.bn_eval(raw, gamma, beta, cfg['rm'], cfg['rv'], cfg['eps'], act, slope)
+        return F.bn_eval(raw, gamma, beta, cfg['rm'], cfg['rv'], cfg['eps'], act, slope, p=p, mode=mode,
+                         seed=seed)
     return F.bn_train(raw, gamma, beta, cfg['rm'], cfg['rv'], cfg['momentum'], cfg['eps'], p, mode, seed, act,
                       slope)
 
 
 def _bn_bwd(dout, raw, gamma, beta, mean, rstd, cfg, p, mode, seed, act, slope, want_bias):
     if cfg['eval']:
-        return F.bn_eval_bwd(dout, raw, gamma, beta, mean, rstd, act, slope, want_bias=want_bias)
+        return F.bn_eval_bwd(dout, raw, gamma, beta, mean, rstd, act, slope, want_bias=want_bias, p=p, mode=mode,
+                             seed=seed)
     return F.bn_train_bwd(dout, raw, gamma, beta, mean, rstd, p, mode, seed, act, slope, want_bias=want_bias)
 
 
 def _bn_cfg(norm, two_d, stride, pad, p, mode, act):
-    """Per-call BatchNorm settings.  A module in eval mode with gradients (e.g. attribution or
+    """Per-call BatchNorm settings.  A norm in eval mode with gradients (e.g. attribution or
     fine-tuning through a frozen G) normalises with its running statistics, as nn.BatchNorm*d
-    does in eval mode: no statistics update, no batch counter, and dropout is off (p = 0)."""
+    does in eval mode: no statistics update, no batch counter.  Dropout (p, mode) is the
+    caller's, chosen from the Dropout module's own training flag, so freezing only the norms
+    (bn.eval(), dropout left in training mode) still drops, as in the reference."""
+    seed = next_seed() if p > 0 else 0
     if not norm.training:
         return dict(two_d=two_d, stride=stride, pad=pad, rm=norm.running_mean, rv=norm.running_var,
-                    momentum=0.0, eps=norm.eps, p=0.0, mode=F.DROP_NONE, seed=0, act=act, slope=0.2,
-                    eval=True)
+                    momentum=0.0, eps=norm.eps, p=p, mode=mode if p > 0 else F.DROP_NONE, seed=seed,
+                    act=act, slope=0.2, eval=True)
     _count_batch(norm)
     return dict(two_d=two_d, stride=stride, pad=pad, rm=norm.running_mean, rv=norm.running_var,
                 momentum=norm.momentum if norm.momentum is not None else 0.1, eps=norm.eps, p=p,
-                mode=mode, seed=next_seed() if p > 0 else 0, act=act, slope=0.2, eval=False)
+                mode=mode, seed=seed, act=act, slope=0.2, eval=False)
 
 
 def conv_norm_act(m, x, out=None):
     k, s, p = m.geometry()
     two_d = m.type == '2d'
-    drop = m.dropout.p if m.training else 0.0
+    drop = m.dropout.p if m.dropout.training else 0.0
     mode = (F.DROP_BEFORE_CH if two_d else F.DROP_BEFORE) if drop > 0 else F.DROP_NONE
     cfg = _bn_cfg(m.norm, two_d, s, tuple(p) if two_d else p, drop, mode, m.act)
     y = _ConvBNAct.apply(x, m.conv.weight, m.conv.bias, m.norm.weight, m.norm.bias, cfg)

@@ -652,9 +652,10 @@ def bn_train(x, gamma, beta, rmean, rvar, momentum, eps, p, mode, seed, act, slo
     return out, mean, rstd
 
 
-def bn_eval(x, gamma, beta, rmean, rvar, eps, act, slope=0.2, out=None):
-    """Eval-mode BatchNorm (running statistics, not updated) fused with the activation, for a
-    forward with gradients; returns (out, mean, rstd) for bn_eval_bwd."""
+def bn_eval(x, gamma, beta, rmean, rvar, eps, act, slope=0.2, out=None, p=0.0, mode=0, seed=0):
+    """Eval-mode BatchNorm (running statistics, not updated) fused with the activation (and the
+    caller's dropout, DROP_* mode), for a forward with gradients; returns (out, mean, rstd) for
+    bn_eval_bwd."""
     _check_dev(x, gamma, beta, rmean, rvar, out)
     B, C, L, xsb, xsc = _bcl(x)
     if out is None:
@@ -663,11 +664,12 @@ def bn_eval(x, gamma, beta, rmean, rvar, eps, act, slope=0.2, out=None):
     mean = torch.empty(C, device=x.device)
     rstd = torch.empty(C, device=x.device)
     N.check(N.lib.a2m_bn_eval_fwd_f32(_p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(rmean), _p(rvar),
-                                      eps, act, slope, _p(out), ysb, ysc, _p(mean), _p(rstd), _stream()))
+                                      eps, p, mode, seed, act, slope, _p(out), ysb, ysc, _p(mean), _p(rstd),
+                                      _stream()))
     return out, mean, rstd
 
 
-def bn_eval_bwd(dy, x, gamma, beta, mean, rstd, act, slope=0.2, want_bias=True):
+def bn_eval_bwd(dy, x, gamma, beta, mean, rstd, act, slope=0.2, want_bias=True, p=0.0, mode=0, seed=0):
     """Backward of bn_eval: (dx, dgamma, dbeta, dbias) with the statistics held fixed."""
     _check_dev(dy, x)
     B, C, L, xsb, xsc = _bcl(x)
@@ -677,8 +679,8 @@ def bn_eval_bwd(dy, x, gamma, beta, mean, rstd, act, slope=0.2, want_bias=True):
     db = torch.empty(C, device=x.device) if beta is not None else None
     dbias = torch.empty(C, device=x.device) if want_bias else None
     _with_ws(x.device, lambda wp, wn: N.lib.a2m_bn_eval_bwd_f32(
-        _p(dy), dsb, dsc, _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(mean), _p(rstd), act, slope,
-        _p(dx), _p(dg), _p(db), _p(dbias), wp, wn, _stream()))
+        _p(dy), dsb, dsc, _p(x), xsb, xsc, B, C, L, _p(gamma), _p(beta), _p(mean), _p(rstd), p, mode, seed,
+        act, slope, _p(dx), _p(dg), _p(db), _p(dbias), wp, wn, _stream()))
     return dx, dg, db, dbias
 
 
@@ -945,6 +947,32 @@ def gather_segments_(dst, segments):
     n = (ctypes.c_int64 * k)(*[t.numel() for _, t in segments])
     N.check(N.lib.a2m_gather_segments_f32(src, off, n, k, _p(dst), _stream()))
     return dst
+
+
+def set_dropout_seed_offset(counter):
+    """Register a device uint64 counter (int64 tensor of one element) whose value offsets every
+    dropout seed of the launches issued while it is registered (a2m_set_dropout_seed_offset: a
+    graph-replayed training step draws fresh masks); None restores the plain seeds."""
+    if counter is not None:
+        _check_dev_any(counter)
+        assert counter.dtype == torch.int64 and counter.numel() == 1
+    N.check(N.lib.a2m_set_dropout_seed_offset(_p(counter)))
+
+
+def _check_dev_any(*ts):
+    for t in ts:
+        if not t.is_cuda:
+            raise RuntimeError('a2m ops need device tensors (no CPU fallback); got a CPU tensor')
+
+
+def adam_dev_(param, grad, exp_avg, exp_avg_sq, lr_dev, beta1, beta2, eps, weight_decay, step_dev):
+    """Adam with the learning rate (device float32[1]) and step (device int32[1], advanced by one
+    here) in device memory: the launch of a graph-captured step (a2m_adam_dev_f32)."""
+    _check_dev(param, grad, exp_avg, exp_avg_sq, lr_dev)
+    _check_dev_any(step_dev)
+    assert step_dev.dtype == torch.int32
+    N.check(N.lib.a2m_adam_dev_f32(_p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), _p(lr_dev),
+                                   beta1, beta2, eps, weight_decay, _p(step_dev), _stream()))
 
 
 def adam_(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):

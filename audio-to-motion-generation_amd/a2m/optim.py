@@ -35,6 +35,8 @@ class FlatAdam:
             p.grad = self.flat_grad[off:off + k].view_as(p)
         self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)]
         self.step_count = 0
+        self._dev_hyper = None     # (lr float32[1], step int32[1]) once use_device_hyper() is called
+        self._dev_lr = None
 
     def zero_grad(self, set_to_none=False):
         """Zero the flat gradient and detach .grad from it: autograd then hands each parameter
@@ -67,13 +69,39 @@ class FlatAdam:
             yield off, p.numel()
             off += -(-p.numel() // ALIGN) * ALIGN
 
+    def use_device_hyper(self):
+        """Keep the learning rate and the step count in device memory (a2m_adam_dev_f32), so a
+        step captured in a HIP graph reads the current values when replayed: the launch advances
+        the device step itself, and sync_hyper() rewrites the device lr when param_groups' lr
+        changed (DynamicGANTraining).  Bitwise the same update as the host-argument launch."""
+        if self._dev_hyper is None:
+            dev = self.flat.device
+            self._dev_hyper = (torch.zeros(1, device=dev), torch.zeros(1, dtype=torch.int32, device=dev))
+            self._dev_lr = None
+        self._dev_hyper[1].fill_(self.step_count)
+        self.sync_hyper()
+
+    def sync_hyper(self):
+        """Write param_groups' lr to the device copy if it changed (stream-ordered, outside any
+        captured region)."""
+        lr = float(self.param_groups[0]['lr'])
+        if self._dev_hyper is not None and lr != self._dev_lr:
+            self._dev_hyper[0].fill_(lr)
+            self._dev_lr = lr
+
     @torch.no_grad()
     def step(self):
         self.collect_grads()
         self.step_count += 1
         g = self.param_groups[0]
-        F.adam_(self.flat, self.flat_grad, self.exp_avg, self.exp_avg_sq, g['lr'], g['betas'][0],
-                g['betas'][1], g['eps'], g['weight_decay'], self.step_count)
+        if self._dev_hyper is not None:
+            if not torch.cuda.is_current_stream_capturing():
+                self.sync_hyper()
+            F.adam_dev_(self.flat, self.flat_grad, self.exp_avg, self.exp_avg_sq, self._dev_hyper[0],
+                        g['betas'][0], g['betas'][1], g['eps'], g['weight_decay'], self._dev_hyper[1])
+        else:
+            F.adam_(self.flat, self.flat_grad, self.exp_avg, self.exp_avg_sq, g['lr'], g['betas'][0],
+                    g['betas'][1], g['eps'], g['weight_decay'], self.step_count)
         F.bump_weights_epoch()   # the HIP update is invisible to torch's version counters
 
     def state_dict(self):
@@ -82,6 +110,10 @@ class FlatAdam:
 
     def load_state_dict(self, sd):
         self.step_count = sd['step']
+        if self._dev_hyper is not None:
+            self._dev_hyper[1].fill_(self.step_count)
+            self._dev_lr = None
         self.exp_avg.copy_(sd['exp_avg'])
         self.exp_avg_sq.copy_(sd['exp_avg_sq'])
         self.param_groups = [dict(g) for g in sd['param_groups']]
+        self.sync_hyper()

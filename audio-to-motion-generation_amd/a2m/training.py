@@ -250,10 +250,15 @@ class GradReducer:
 
     @torch.no_grad()
     def finish(self):
-        """Reduce the buckets not yet launched, wait for all, average.  Returns flat_grad."""
+        """Reduce the buckets not yet launched, wait for all, average.  Returns flat_grad.
+        Inside a HIP-graph capture (GANTrainer(graphs=True)) the plan is frozen: every replay
+        issues exactly the captured bucket all-reduces in the captured order on every rank, so
+        the host-side plan checks (which read a flag back) are skipped there; a capture with a
+        plan violation raises here at once."""
         if not self.active:
             self.opt.collect_grads()
             return self.opt.flat_grad
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         while self.next < len(self.buckets):
             self._launch(self.next)
             self.next += 1
@@ -265,6 +270,13 @@ class GradReducer:
             work.wait()
             if buf is not sl:
                 sl.copy_(buf)
+        if capturing:
+            self.active = False
+            if self.error:
+                raise RuntimeError(self.error)
+            if self.world > 1:
+                self.opt.flat_grad.div_(self.world)
+            return self.opt.flat_grad
         if self.error and self._sticky_error is None:
             self._sticky_error = self.error
         self.steps += 1
@@ -310,19 +322,45 @@ class GradReducer:
                                       'learnt parameter set')
 
 
+class _CapturedStep:
+    """One G-step or D-step body captured as a HIP graph: private static copies of its inputs
+    (each call copies the caller's tensors in), the graph, and its loss output."""
+
+    def __init__(self, key, inputs):
+        self.key, self.inputs = key, inputs
+        self.graph = torch.cuda.CUDAGraph()
+        self.loss = None
+
+
 class GANTrainer:
     """One version5_model_train.py iteration per call, optionally data-parallel."""
 
+    # eager steps of each kind before its body is captured (the first ones learn the bucket plan,
+    # fill the host-side caches and grow the workspaces)
+    GRAPH_WARMUP = 2
+
     def __init__(self, generator, discriminator, lr=10e-4, lambda_gan=1.0, lambda_d=1.0,
                  dynamic=None, fixed_labels=None, process_group=None, sync_bn=False,
-                 bucket_mb=25.0, grad_reduce_dtype=None, label_seed=None, force_collectives=False):
+                 bucket_mb=25.0, grad_reduce_dtype=None, label_seed=None, force_collectives=False,
+                 graphs=False):
         """label_seed: seed of the generator the noisy GAN labels are drawn from; None (the
         default) derives it from torch.initial_seed() of rank 0, so the labels follow the
         caller's torch.manual_seed like the reference's global-RNG draw (an unseeded process
         draws different labels each run, as the reference does).  With several ranks the seed
         is broadcast here, at construction, not inside a step.  force_collectives: run the
         data-parallel machinery (bucketed gradient all-reduce, SyncBN) also when the process
-        group has one rank -- the RCCL path on one GPU (tests/test_gpu_rccl.py)."""
+        group has one rank -- the RCCL path on one GPU (tests/test_gpu_rccl.py).
+
+        graphs: capture the G-step body (forward, losses, backward, gradient gather, bucket
+        all-reduces when data-parallel over RCCL, Adam) and the D-step body as HIP graphs after
+        GRAPH_WARMUP eager steps of each, and replay them: one graph launch per step instead of
+        ~500-1,000 dependent kernel launches.  The reference's host decisions stay on the host,
+        between replays (G/D frequencies, should_train_discriminator, the learning rates, which
+        reach the device through FlatAdam.use_device_hyper); the labels are drawn eagerly per
+        iteration and copied into the graph's inputs; dropout masks stay fresh per step through a
+        device seed counter (a2m_set_dropout_seed_offset).  Needs one rank, or a process group on
+        the nccl (RCCL) backend, whose collectives the capture records.  A new input shape or
+        GEMM precision recaptures."""
         self.G, self.D = generator, discriminator
         self.opt_G = FlatAdam(generator.parameters(), lr=lr)
         self.opt_D = FlatAdam(discriminator.parameters(), lr=lr)
@@ -342,6 +380,22 @@ class GANTrainer:
         self.label_seed = label_seed
         self._label_gen = None
         self.last_d_loss = None
+        self.graphs = bool(graphs)
+        self._collectives = self.world > 1 or force
+        self._captured = {'g': None, 'd': None}
+        self._warm = {'g': 0, 'd': 0}
+        self._seed_ctr = None
+        if self.graphs:
+            dev = next(generator.parameters()).device
+            if dev.type != 'cuda':
+                raise RuntimeError('GANTrainer(graphs=True) needs the models on a ROCm device')
+            if self._collectives and dist.get_backend(process_group) != 'nccl':
+                raise RuntimeError('GANTrainer(graphs=True) with data parallelism needs the nccl '
+                                   '(RCCL) backend: gloo collectives cannot be captured')
+            self._seed_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._cap_stream = torch.cuda.Stream(device=dev)
+            self.opt_G.use_device_hyper()
+            self.opt_D.use_device_hyper()
         if fixed_labels is None and label_seed is None and self.world > 1:
             # agree on the label seed now (a collective), not lazily inside the first step
             dev = next(generator.parameters()).device
@@ -380,7 +434,65 @@ class GANTrainer:
         fake = self.dyn.get_smooth_labels(epoch, Bg, dev, False, generator=self._label_gen)
         return real[lo:lo + B], fake[lo:lo + B]
 
+    # ---------------------------------------------------------------- HIP-graph replay
+    def _body(self, fn, args):
+        """Run one step body with the dropout seed counter registered and advanced (graph mode:
+        eager warm-up steps, the capture, and hence every replay)."""
+        if self._seed_ctr is None:
+            return fn(*args)
+        F.set_dropout_seed_offset(self._seed_ctr)
+        try:
+            self._seed_ctr.add_(1)
+            return fn(*args)
+        finally:
+            F.set_dropout_seed_offset(None)
+
+    def _graphed(self, kind, fn, opt, args):
+        """One step of `kind` ('g' / 'd'): eager for the first GRAPH_WARMUP calls, then captured
+        once (the capture records, it does not run: its call replays right after) and replayed."""
+        key = tuple((tuple(a.shape), a.dtype) for a in args) + (F.N.lib.a2m_get_gemm_precision(),)
+        st = self._captured[kind]
+        if st is not None and st.key != key:
+            st = self._captured[kind] = None
+        if st is None:
+            if self._warm[kind] < self.GRAPH_WARMUP:
+                self._warm[kind] += 1
+                return self._body(fn, args)
+            st = _CapturedStep(key, [a.detach().clone() for a in args])
+            torch.cuda.synchronize()
+            steps = opt.step_count
+            # each graph keeps its own memory pool: a host cache can drop a buffer that one graph
+            # still writes on replay, and only that graph's own recapture may reuse it
+            # with collectives, thread-local capture: RCCL's watchdog thread keeps querying the
+            # events of earlier (eager) collectives while this thread captures
+            mode = 'thread_local' if self._collectives else 'global'
+            with torch.cuda.graph(st.graph, stream=self._cap_stream, capture_error_mode=mode):
+                st.loss = self._body(fn, st.inputs)
+            opt.step_count = steps          # the capture recorded the step; the replay below runs it
+            self._captured[kind] = st
+        for dst, a in zip(st.inputs, args):
+            if dst.data_ptr() != a.data_ptr():
+                dst.copy_(a)
+        opt.sync_hyper()
+        st.graph.replay()
+        opt.step_count += 1
+        F.bump_weights_epoch()
+        return st.loss.clone()
+
+    def _graphs_on(self):
+        return self.graphs and torch.cuda.is_available()
+
     def g_step(self, audio, real_pose, valid):
+        if self._graphs_on():
+            return self._graphed('g', self._g_step, self.opt_G, (audio, real_pose, valid))
+        return self._body(self._g_step, (audio, real_pose, valid))
+
+    def d_step(self, audio, real_motion, valid, fake):
+        if self._graphs_on():
+            return self._graphed('d', self._d_step, self.opt_D, (audio, real_motion, valid, fake))
+        return self._body(self._d_step, (audio, real_motion, valid, fake))
+
+    def _g_step(self, audio, real_pose, valid):
         self.opt_G.zero_grad()
         self.red_G.begin()
         fake_pose, internal = self.G(audio, real_pose=real_pose)
@@ -394,7 +506,7 @@ class GANTrainer:
         self.opt_G.step()
         return g_loss.detach()
 
-    def d_step(self, audio, real_motion, valid, fake):
+    def _d_step(self, audio, real_motion, valid, fake):
         self.opt_D.zero_grad()
         with torch.no_grad():
             fp, _ = self.G(audio)

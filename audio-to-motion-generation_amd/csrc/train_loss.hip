@@ -328,6 +328,34 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, int64_
   }
 }
 
+// The same update with its step-dependent hyperparameters in device memory, for a step captured
+// in a HIP graph (a replay re-runs the launch with its baked arguments): adam_tick_kernel advances
+// the step counter, then every thread derives the bias corrections from it exactly as the host
+// entry point does (double pow / sqrt, rounded to float) and reads the learning rate, which the
+// host rewrites only when it changes (DynamicGANTraining.adjust_learning_rates).
+__global__ void adam_tick_kernel(int32_t* step) {
+  if (threadIdx.x == 0) step[0] += 1;
+}
+
+__global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, int64_t n, const float* lr_p,
+                                float b1, float b2, float eps, float wd, const int32_t* step_p) {
+  const int32_t step = step_p[0];
+  const float lr = lr_p[0];
+  const float bc1 = (float)(1.0 - pow((double)b1, (double)step));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, (double)step));
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    if (wd != 0.f) gi += wd * p[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] -= (lr / bc1) * (mi / denom);
+  }
+}
+
 // Segment gather: dst[off_i .. off_i + n_i) = src_i[0 .. n_i) for up to GS_MAX segments per
 // launch (FlatAdam: the step's per-parameter gradients, which autograd hands over as fresh
 // tensors, land in the flat gradient buffer in one launch instead of one add or copy per
@@ -450,6 +478,20 @@ int a2m_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 8192)), dim3(256), 0,
                      as_stream(stream), param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps,
                      weight_decay, (float)bc1, (float)std::sqrt(bc2));
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+int a2m_adam_dev_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                     const float* lr, float beta1, float beta2, float eps, float weight_decay,
+                     int32_t* step, void* stream) {
+  A2M_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && lr && step && n >= 0, "adam_dev: bad args");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, st, step);
+  A2M_LAUNCH_CHECK();
+  if (n == 0) return A2M_OK;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3((unsigned)std::min<int64_t>(cdiv(n, 256), 8192)), dim3(256), 0,
+                     st, param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

@@ -37,7 +37,21 @@ struct BNArgs {
   const float* x; int64_t xs_b, xs_c;
   int B, C, L, slices;
   float p; int mode; uint64_t seed;
+  const uint64_t* seed_off;  // device step counter (a2m_set_dropout_seed_offset) or null
 };
+
+// Dropout seed offset for captured training steps: a HIP graph bakes every launch's seed, so a
+// replayed step would redraw the same masks.  With a device counter registered (the trainer
+// bumps it once per replayed step, inside the graph) each launch hashes seed + counter * K,
+// read when the kernel runs.  Null: the seed as passed (eager steps, unchanged bits).
+static const uint64_t* g_seed_off = nullptr;
+
+__device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* off, float p) {
+  return (off && p > 0.f) ? seed + off[0] * 0xA0761D6478BD642Full : seed;
+}
+// kernels take their arguments as `a_in` and work on a copy whose seed has the offset applied
+#define A2M_BN_RESOLVE(T, a_in) T a = a_in; a.seed = eff_seed(a_in.seed, a_in.seed_off, a_in.p)
+#define A2M_BNB_RESOLVE(a_in) BNBwdArgs a = a_in; a.f.seed = eff_seed(a_in.f.seed, a_in.f.seed_off, a_in.f.p)
 
 __device__ __forceinline__ float pre_drop(const BNArgs& a, int b, int c, int l) {
   if (a.mode == DROP_BEFORE) return drop_scale(a.seed, ((uint64_t)b * a.C + c) * a.L + l, a.p);
@@ -57,7 +71,8 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 }
 
 // partial (sum z, sum z^2) per (channel, slice)
-__global__ __launch_bounds__(256) void bn_stats_kernel(BNArgs a, double* part) {
+__global__ __launch_bounds__(256) void bn_stats_kernel(BNArgs a_in, double* part) {
+  A2M_BN_RESOLVE(BNArgs, a_in);
   __shared__ double red[4];
   const int c = blockIdx.x / a.slices, s = blockIdx.x % a.slices;
   const int64_t N = (int64_t)a.B * a.L;
@@ -94,12 +109,13 @@ __device__ __forceinline__ float act_grad(float pre, int act, float slope) {
 // launch fewer per BatchNorm layer): every workgroup of channel c reduces the channel's slice
 // partials in the same fixed order (so every workgroup gets the same mean / rstd bits), and the
 // slice-0 workgroup publishes them and updates the running statistics.
-__global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNArgs a, const double* part, float eps,
+__global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNArgs a_in, const double* part, float eps,
                                                              float momentum, float* rmean,
                                                              float* rvar, float* mean_out,
                                                              float* rstd_out, const float* gamma,
                                                              const float* beta, int act, float slope,
                                                              float* y, int64_t ys_b, int64_t ys_c) {
+  A2M_BN_RESOLVE(BNArgs, a_in);
   __shared__ float stat[2];
   const int c = blockIdx.x / a.slices, s = blockIdx.x % a.slices;
   const int64_t N = (int64_t)a.B * a.L;
@@ -137,10 +153,11 @@ __global__ __launch_bounds__(256) void bn_apply_fused_kernel(BNArgs a, const dou
   }
 }
 
-__global__ __launch_bounds__(256) void bn_apply_kernel(BNArgs a, const float* mean, const float* rstd,
+__global__ __launch_bounds__(256) void bn_apply_kernel(BNArgs a_in, const float* mean, const float* rstd,
                                                        const float* gamma, const float* beta,
                                                        int act, float slope, float* y,
                                                        int64_t ys_b, int64_t ys_c) {
+  A2M_BN_RESOLVE(BNArgs, a_in);
   const int c = blockIdx.x / a.slices, s = blockIdx.x % a.slices;
   const int64_t N = (int64_t)a.B * a.L;
   const int64_t i0 = (int64_t)s * kSlice, i1 = min<int64_t>(N, i0 + kSlice);
@@ -171,7 +188,8 @@ __device__ __forceinline__ float bn_g(const BNBwdArgs& a, int b, int c, int l, f
   return g;
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_stats_kernel(BNBwdArgs a, double* part) {
+__global__ __launch_bounds__(256) void bn_bwd_stats_kernel(BNBwdArgs a_in, double* part) {
+  A2M_BNB_RESOLVE(a_in);
   __shared__ double red[4];
   const BNArgs& f = a.f;
   const int c = blockIdx.x / f.slices, s = blockIdx.x % f.slices;
@@ -197,8 +215,9 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(BNBwdArgs a, double* 
 
 // dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)); dx_raw = dz * drop-before scale;
 // partial sums of dx_raw (the conv bias gradient) per (channel, slice)
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a, const float* sums, float* dx,
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a_in, const float* sums, float* dx,
                                                            double* part) {
+  A2M_BNB_RESOLVE(a_in);
   __shared__ double red[4];
   const BNArgs& f = a.f;
   const int c = blockIdx.x / f.slices, s = blockIdx.x % f.slices;
@@ -225,9 +244,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BNBwdArgs a, const fl
 // its channel's (sum g, sum g xhat) partials in the fixed slice order, the slice-0 workgroup
 // writes dgamma / dbeta; the dbias partials go to their own region (dpart) because other
 // workgroups may still be reading `part`.
-__global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(BNBwdArgs a, const double* part,
+__global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(BNBwdArgs a_in, const double* part,
                                                                  float* dgamma, float* dbeta,
                                                                  float* dx, double* dpart) {
+  A2M_BNB_RESOLVE(a_in);
   __shared__ double red[4];
   __shared__ float sums[2];
   const BNArgs& f = a.f;
@@ -268,7 +288,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(BNBwdArgs a, co
 // Eval-mode BatchNorm with gradients (nn.BatchNorm*d in .eval(), model_layers.py:51-118): the
 // running statistics normalise and are not updated; the kernels above run with mean = running
 // mean and rstd = 1 / sqrt(running var + eps), and the backward drops the batch-statistics terms
-// (the apply divides the (sum g, sum g xhat) pair by n_div = +inf: exactly 0, so dz = gamma rstd g)
+// (the apply divides the (sum g, sum g xhat) pair by n_div = +inf: exactly 0, so dz = gamma rstd g).
+// Dropout follows the caller's Dropout module, which may still be in training mode when only the
+// norms are frozen (bn.eval()): the masks are applied exactly as in the training kernels.
 __global__ void bn_eval_consts_kernel(const float* rmean, const float* rvar, int C, float eps,
                                       float* mean, float* rstd) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -325,7 +347,9 @@ __global__ void reduce_slices_kernel(const double* part, int C, int slices, floa
   out[c] = (float)s;
 }
 
-__global__ void dropout_kernel(const float* x, int64_t n, float p, uint64_t seed, float* y) {
+__global__ void dropout_kernel(const float* x, int64_t n, float p, uint64_t seed_in,
+                               const uint64_t* seed_off, float* y) {
+  const uint64_t seed = eff_seed(seed_in, seed_off, p);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     y[i] = x[i] * drop_scale(seed, (uint64_t)i, p);
@@ -460,7 +484,7 @@ int a2m_bn_train_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, 
   A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
   const size_t need = sizeof(double) * 2 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_train_fwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
-  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   hipStream_t st = as_stream(stream);
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL(bn_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
@@ -485,7 +509,7 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
   const size_t need = sizeof(double) * 3 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_train_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNBwdArgs a;
-  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
   a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
   a.n_div = (float)N;
@@ -507,13 +531,16 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
 
 int a2m_bn_eval_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
                         const float* gamma, const float* beta, const float* running_mean,
-                        const float* running_var, float eps, int32_t act, float slope, float* y,
-                        int64_t ys_b, int64_t ys_c, float* save_mean, float* save_rstd, void* stream) {
+                        const float* running_var, float eps, float drop_p, int32_t drop_mode,
+                        uint64_t seed, int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
+                        float* save_mean, float* save_rstd, void* stream) {
   A2M_CHECK_ARG(x && y && running_mean && running_var && save_mean && save_rstd && B > 0 && C > 0 && L > 0,
                 "bn_eval_fwd: bad args");
+  A2M_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f && drop_mode >= DROP_NONE && drop_mode <= DROP_AFTER,
+                "bn_eval_fwd: bad dropout (p %g, mode %d)", (double)drop_p, drop_mode);
   const int S = bn_slices((int64_t)B * L);
   A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)B * L);
-  BNArgs a{x, xs_b, xs_c, B, C, L, S, 0.f, DROP_NONE, 0};
+  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(bn_eval_consts_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, running_mean,
                      running_var, C, eps, save_mean, save_rstd);
@@ -526,17 +553,20 @@ int a2m_bn_eval_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, i
 
 int a2m_bn_eval_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x, int64_t xs_b,
                         int64_t xs_c, int32_t B, int32_t C, int32_t L, const float* gamma,
-                        const float* beta, const float* save_mean, const float* save_rstd, int32_t act,
-                        float slope, float* dx, float* dgamma, float* dbeta, float* dbias, void* ws,
-                        size_t ws_bytes, void* stream) {
+                        const float* beta, const float* save_mean, const float* save_rstd, float drop_p,
+                        int32_t drop_mode, uint64_t seed, int32_t act, float slope, float* dx,
+                        float* dgamma, float* dbeta, float* dbias, void* ws, size_t ws_bytes,
+                        void* stream) {
   A2M_CHECK_ARG(dy && x && dx && save_mean && save_rstd && B > 0 && C > 0 && L > 0, "bn_eval_bwd: bad args");
+  A2M_CHECK_ARG(drop_p >= 0.f && drop_p < 1.f && drop_mode >= DROP_NONE && drop_mode <= DROP_AFTER,
+                "bn_eval_bwd: bad dropout (p %g, mode %d)", (double)drop_p, drop_mode);
   const int64_t N = (int64_t)B * L;
   const int S = bn_slices(N);
   A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
   const size_t need = sizeof(double) * 3 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_eval_bwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNBwdArgs a;
-  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, 0.f, DROP_NONE, 0};
+  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
   a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
   a.n_div = __builtin_inff();   // fixed statistics: no mean(g) / mean(g xhat) terms
@@ -566,7 +596,7 @@ int a2m_bn_sync_stats_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B,
   A2M_CHECK_ARG(S > 0, "batchnorm: %lld elements per channel (at most 2^31 - 1)", (long long)N);
   const size_t need = sizeof(double) * 2 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_sync_stats: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
-  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   hipStream_t st = as_stream(stream);
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL(bn_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
@@ -586,7 +616,7 @@ int a2m_bn_sync_apply_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B,
   A2M_CHECK_ARG(x && y && sums && save_mean && save_rstd && B > 0 && C > 0 && L > 0 && n_total > 0,
                 "bn_sync_apply: bad args");
   const int S = bn_slices((int64_t)B * L);
-  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, st, sums, C,
                      n_total, eps, momentum, running_mean, running_var, save_mean, save_rstd);
@@ -611,7 +641,7 @@ int a2m_bn_sync_bwd_stats_f32(const float* dy, int64_t dys_b, int64_t dys_c, con
   const size_t need = sizeof(double) * 2 * (size_t)C * S;
   if (!ws || ws_bytes < need) { set_error("bn_sync_bwd_stats: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNBwdArgs a;
-  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
   a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
   a.n_div = (float)N;
@@ -640,7 +670,7 @@ int a2m_bn_sync_bwd_apply_f32(const float* dy, int64_t dys_b, int64_t dys_c, con
   const size_t need = sizeof(double) * (size_t)C * S + sizeof(float) * 2 * (size_t)C + 16;
   if (!ws || ws_bytes < need) { set_error("bn_sync_bwd_apply: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNBwdArgs a;
-  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed};
+  a.f = BNArgs{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   a.dy = dy; a.dys_b = dys_b; a.dys_c = dys_c;
   a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
   a.n_div = (float)n_total;
@@ -660,11 +690,17 @@ int a2m_bn_sync_bwd_apply_f32(const float* dy, int64_t dys_b, int64_t dys_c, con
   return A2M_OK;
 }
 
+int a2m_set_dropout_seed_offset(const uint64_t* counter) {
+  g_seed_off = counter;
+  return A2M_OK;
+}
+
 int a2m_dropout_f32(const float* x, int64_t n, float p, uint64_t seed, float* y, void* stream) {
   A2M_CHECK_ARG(x && y && n >= 0 && p >= 0.f && p < 1.f, "dropout: bad args");
   if (n == 0) return A2M_OK;
   const int blocks = (int)std::min<int64_t>(cdiv(n, 256), 8192);
-  hipLaunchKernelGGL(dropout_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, n, p, seed, y);
+  hipLaunchKernelGGL(dropout_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, n, p, seed,
+                     g_seed_off, y);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

@@ -426,8 +426,9 @@ def run_train(args, world, rank, dev):
     torch.manual_seed(1234)                           # identical initial weights on every rank
     g = SelfAttention_G(time_steps=T, p=0.2).to(dev).train()
     d = SelfAttention_D(out_channels=64).to(dev).train()
+    graphs = not args.no_graph and (world == 1 or dist.get_backend() == 'nccl')
     tr = GANTrainer(g, d, lr=10e-4, sync_bn=args.sync_bn, bucket_mb=args.bucket_mb, label_seed=7,
-                    grad_reduce_dtype=torch.bfloat16 if args.dtype == 'bf16' else None)
+                    grad_reduce_dtype=torch.bfloat16 if args.dtype == 'bf16' else None, graphs=graphs)
     gen = torch.Generator(device='cpu').manual_seed(100 + rank)
     audio = torch.randn(B, T, 128, generator=gen).to(dev)
     pose = torch.randn(B, T, 104, generator=gen).to(dev)
@@ -452,6 +453,7 @@ def run_train(args, world, rank, dev):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    tr.flush()   # the ranks agree that every step's gradients followed the bucket plan
     ms = elapsed / args.steps * 1e3
     flops = TRAIN_GFLOP_PER_CLIP_T64 * 1e9 * B * T / 64           # per rank
     tf = flops * world / (ms * 1e-3) / 1e12
@@ -467,6 +469,7 @@ def run_train(args, world, rank, dev):
         'config': {'workload': cfg + ': version5_model_train.py iteration (G x3 + D x1, Adam, '
                                'smoothed noisy labels), DP over ranks',
                    'batchnorm': 'sync' if tr.sync_bn else 'per-rank statistics',
+                   'hip_graph': ('G-step and D-step bodies captured, replayed per step' if graphs else 'none'),
                    'grad_allreduce': (f'{len(tr.red_G.buckets)} G / {len(tr.red_D.buckets)} D buckets '
                                       f'(each closed once >= {args.bucket_mb:g} MB), overlapped with backward, '
                                       f'{"bf16" if args.dtype == "bf16" else "fp32"} on the wire'),
@@ -551,6 +554,14 @@ def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
 
 
 GEMM_FAMILY = ('gemm_kernel', 'gemm_pipe_kernel', 'gemm_pipe_bf16_kernel', 'splitk_reduce')   # the engine's kernels
+
+
+def under_profiler():
+    """True when this process already runs under rocprofv3 (its preload library and ROCPROF_*
+    settings are inherited): a nested traced child would stack a second profiler, so the line
+    then keeps the span-stamp basis (roofline.basis says which)."""
+    pre = os.environ.get('LD_PRELOAD', '')
+    return 'librocprofiler-sdk-tool' in pre or 'ROCPROF_OUTPUT_PATH' in os.environ
 
 
 def trace_child(args):
@@ -798,7 +809,8 @@ def main():
         mel_enc['instep_mel_encoder_ms'] = round(it['mel_enc_ms'], 4)
         mel_enc['path_frac_instep'] = round(mel_enc['path_roofline_ms'] / it['mel_enc_ms'], 4)
         tr = None
-        if world == 1 and not args.no_trace and graph is not None and not args.branch_graphs:
+        if world == 1 and not args.no_trace and graph is not None and not args.branch_graphs and \
+                not under_profiler():
             tr = traced_family(args, it['flops'], keep_dir=os.environ.get('A2M_BENCH_TRACE_DIR'))
         if tr and tr['mel_enc_us']:
             mel_enc['instep_mel_encoder_ms_trace'] = round(tr['mel_enc_us'] / 1e3, 4)

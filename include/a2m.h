@@ -339,18 +339,28 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
 /* Eval-mode BatchNorm with gradients (nn.BatchNorm*d after .eval(), model_layers.py:51-118, e.g.
  * fine-tuning or input attribution through a frozen G): normalises with the running statistics,
  * which it does not update, fused with the activation; save_mean / save_rstd receive the running
- * mean and 1 / sqrt(running_var + eps) for the backward.  No dropout (eval). */
+ * mean and 1 / sqrt(running_var + eps) for the backward.  drop_p / drop_mode / seed as in
+ * a2m_bn_train_fwd_f32: the surrounding Dropout module may still be in training mode when only the
+ * norm is frozen (bn.eval(), dropout left on); pass drop_p = 0 for a whole module in eval. */
 int a2m_bn_eval_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, int32_t C, int32_t L,
                         const float* gamma, const float* beta, const float* running_mean,
-                        const float* running_var, float eps, int32_t act, float slope, float* y,
-                        int64_t ys_b, int64_t ys_c, float* save_mean, float* save_rstd, void* stream);
-/* Its backward: dx = gamma * rstd * act'(.) * dy (fixed statistics: no batch-mean terms),
- * dgamma = sum g * xhat, dbeta = sum g, dbias = sum dx, g = act'(.) * dy. */
+                        const float* running_var, float eps, float drop_p, int32_t drop_mode,
+                        uint64_t seed, int32_t act, float slope, float* y, int64_t ys_b, int64_t ys_c,
+                        float* save_mean, float* save_rstd, void* stream);
+/* Its backward: dx = gamma * rstd * act'(.) * dy (* the dropout scale; fixed statistics: no
+ * batch-mean terms), dgamma = sum g * xhat, dbeta = sum g, dbias = sum dx, g = act'(.) * dy. */
 int a2m_bn_eval_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const float* x, int64_t xs_b,
                         int64_t xs_c, int32_t B, int32_t C, int32_t L, const float* gamma,
-                        const float* beta, const float* save_mean, const float* save_rstd, int32_t act,
-                        float slope, float* dx, float* dgamma, float* dbeta, float* dbias, void* ws,
-                        size_t ws_bytes, void* stream);
+                        const float* beta, const float* save_mean, const float* save_rstd, float drop_p,
+                        int32_t drop_mode, uint64_t seed, int32_t act, float slope, float* dx,
+                        float* dgamma, float* dbeta, float* dbias, void* ws, size_t ws_bytes,
+                        void* stream);
+/* Dropout seed offset for training steps captured in a HIP graph (version5_model_train.py:
+ * 342-405 replayed per G / D step): every dropout launch issued while `counter` (a device
+ * uint64) is registered hashes with seed + counter[0] * K, read when the kernel runs, so a
+ * replayed step that advances the counter draws fresh masks although its seeds are baked.
+ * NULL (the default) restores the plain seeds.  Library-global; set it around the launches. */
+int a2m_set_dropout_seed_offset(const uint64_t* counter);
 /* SyncBatchNorm phases for data-parallel training (per-layer all-reduce of the
  * BatchNorm statistics so DP over ranks normalises like the single-device batch,
  * version5_model_train.py:342-414 at B = 64).  The fused bn_train_fwd/bwd above split at their
@@ -482,6 +492,14 @@ int a2m_gemm_f32(int32_t M, int32_t N, int32_t N1, int32_t K, int32_t K1, int32_
 int a2m_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                  float lr, float beta1, float beta2, float eps, float weight_decay, int32_t step,
                  void* stream);
+
+/* The same update for a step captured in a HIP graph: step (device int32) is advanced by one in
+ * the launch and the bias corrections derived from it on the device; lr is a device float the
+ * host rewrites when DynamicGANTraining changes it (version5_model_train.py:80-107).  Bitwise
+ * the update of a2m_adam_f32 at the same step and lr. */
+int a2m_adam_dev_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                     const float* lr, float beta1, float beta2, float eps, float weight_decay,
+                     int32_t* step, void* stream);
 
 /* dst[dst_off[i] .. dst_off[i] + n[i]) = src[i][0 .. n[i]) for i < count (host arrays of device
  * pointers / element counts; segments must not overlap).  The optimiser's gradient collection:

@@ -124,8 +124,72 @@ def test_rccl_dp_step_one_rank(tmp_path):
     assert s['g_rel'] < 1e-3 and s['d_rel'] < 1e-3, s
 
 
+def _child_graph(out):
+    """GANTrainer(graphs=True) over the one-rank RCCL group: the G-step and D-step bodies are
+    captured with their bucket all-reduces (launched from the gradient hooks during the captured
+    backward) and replayed; the replayed gradients equal the local eager step's bit for bit."""
+    import torch
+    import torch.distributed as dist
+    sys.path[:0] = [REPO, os.path.join(REPO, 'audio-to-motion-generation_amd'), os.path.join(REPO, 'tests')]
+    dev = torch.device('cuda', 0)
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
+    torch.cuda.set_device(dev)
+    from a2m import autograd as AG
+    from a2m.training import GANTrainer
+    from oracle import synth
+    from test_gpu_configs import _models
+    gen = torch.Generator().manual_seed(31)
+    B = 8
+    audio = (torch.randn(B, 64, 128, generator=gen) * 2.0 - 3.0).to(dev)
+    pose = torch.from_numpy(synth.pose_targets(B, 64, seed=32)).to(dev)
+    res = {}
+    for mode in ('local', 'dp_graph'):
+        g, d = _models(dev)
+        tr = GANTrainer(g, d, lr=0.0, fixed_labels=(0.93, 0.07), bucket_mb=8.0,
+                        force_collectives=mode != 'local', graphs=mode == 'dp_graph')
+        valid, fake = tr._labels(0, B, dev)
+        for p_ in d.parameters():
+            p_.requires_grad_(False)
+        gls = [tr.g_step(audio, pose, valid).item() for _ in range(4)]
+        for p_ in d.parameters():
+            p_.requires_grad_(True)
+        gg = tr.opt_G.flat_grad.detach().clone()
+        dls = [tr.d_step(audio, AG.pos_to_motion(pose), valid, fake).item() for _ in range(4)]
+        dg = tr.opt_D.flat_grad.detach().clone()
+        torch.cuda.synchronize()
+        res[mode] = dict(gls=gls, dls=dls, gg=gg, dg=dg, buckets=(len(tr.red_G.buckets), len(tr.red_D.buckets)),
+                         captured=(tr._captured['g'] is not None, tr._captured['d'] is not None))
+    loc, r = res['local'], res['dp_graph']
+    rep = {'backend': dist.get_backend(), 'world': dist.get_world_size(),
+           'g_equal': bool(torch.equal(r['gg'], loc['gg'])), 'd_equal': bool(torch.equal(r['dg'], loc['dg'])),
+           'losses_equal': r['gls'] == loc['gls'] and r['dls'] == loc['dls'],
+           'gls': r['gls'], 'gls_local': loc['gls'], 'buckets': r['buckets'], 'captured': r['captured']}
+    dist.destroy_process_group()
+    with open(out, 'w') as f:
+        json.dump(rep, f)
+
+
+def test_rccl_dp_graph_one_rank(tmp_path):
+    out = str(tmp_path / 'rccl_graph.json')
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1',
+               LOCAL_RANK='0')
+    p = subprocess.run([sys.executable, os.path.abspath(__file__), '--child-graph', out], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-4000:]
+    rep = json.load(open(out))
+    print(json.dumps(rep))
+    assert rep['backend'] == 'nccl' and rep['captured'] == [True, True], rep
+    assert rep['buckets'][0] > 1, rep
+    assert rep['g_equal'] and rep['d_equal'] and rep['losses_equal'], rep
+
+
 if __name__ == '__main__':
     if len(sys.argv) == 3 and sys.argv[1] == '--child':
         _child(sys.argv[2])
+    elif len(sys.argv) == 3 and sys.argv[1] == '--child-graph':
+        _child_graph(sys.argv[2])
     else:
         sys.exit('usage: test_gpu_rccl.py --child OUT.json (run by pytest)')

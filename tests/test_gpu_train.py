@@ -103,6 +103,64 @@ def test_conv_norm_act_eval_mode_gradients(two_d):
                   'beta': (m.norm.bias.grad, ref.norm.bias.grad)})
 
 
+@pytest.mark.parametrize('two_d', [False, True])
+def test_frozen_norm_with_dropout_in_training(two_d):
+    """Only the norm frozen (m.norm.eval(), the Dropout module left in training mode, a common
+    fine-tuning pattern): the reference still drops (model_layers.py:118 runs self.dropout before
+    the eval-mode norm).  The hash mask cannot be torch's, so it is read back from the HIP output
+    (each element is either the kept raw / (1 - p) or the dropped 0 through the fixed norm) and the
+    layer is checked against torch-CPU autograd of conv -> mask -> eval BN -> LeakyReLU with that
+    mask; the dropped fraction must be ~p and the mask must differ from none."""
+    from a2m.model_layers import ConvNormRelu
+    torch.manual_seed(0)
+    args = (3, 16) if two_d else (6, 16)
+    kind = '2d' if two_d else '1d'
+    p = 0.4
+    m = ConvNormRelu(*args, type=kind, leaky=True, downsample=True, p=p)
+    ref = ConvNormRelu(*args, type=kind, leaky=True, downsample=True, p=p)
+    ref.load_state_dict(m.state_dict())
+    with torch.no_grad():
+        for mod in (m, ref):
+            mod.norm.running_mean.copy_(_r(args[1], seed=5, scale=0.3))
+            mod.norm.running_var.copy_(_r(args[1], seed=6).abs() + 0.5)
+            mod.norm.weight.copy_(_r(args[1], seed=7).abs() + 0.5)
+            mod.norm.bias.copy_(_r(args[1], seed=8, scale=0.2))
+    m.to(DEV).train()
+    m.norm.eval()
+    assert m.dropout.training
+    rm0 = m.norm.running_mean.clone()
+    x = _r(8, 3, 12, 20, seed=1) if two_d else _r(8, 6, 40, seed=1)
+    xd, xc = _leaf(x)
+    yd = m(xd)
+    assert torch.equal(m.norm.running_mean, rm0)
+    conv = TF.conv2d if two_d else TF.conv1d
+    n = ref.norm
+
+    def head(z):
+        return TF.leaky_relu(TF.batch_norm(z, n.running_mean, n.running_var, n.weight, n.bias, False, 0.1,
+                                           1e-5), 0.2)
+    with torch.no_grad():
+        raw = conv(xc, ref.conv.weight, ref.conv.bias, stride=2, padding=1)
+        y_keep, y_drop = head(raw / (1 - p)), head(raw * 0)
+        y = yd.detach().cpu()
+        keep = ((y - y_keep).abs() <= (y - y_drop).abs()).float()
+        if two_d:   # Dropout2d: one decision per (clip, channel)
+            frac = keep.mean(dim=(2, 3), keepdim=True)
+            assert torch.all((frac == 0) | (frac == 1)), 'channel mask not uniform over the map'
+            keep = frac.expand_as(keep).contiguous()
+    dropped = 1 - keep.mean().item()
+    assert 0.2 < dropped < 0.6, dropped
+    yc = head(conv(xc, ref.conv.weight, ref.conv.bias, stride=2, padding=1) * keep / (1 - p))
+    assert rel_err(y, yc.detach()) < TOL
+    gy = _r(*yc.shape, seed=2)
+    yd.backward(gy.to(DEV))
+    yc.backward(gy)
+    _check_grads({'x': (xd.grad, xc.grad), 'w': (m.conv.weight.grad, ref.conv.weight.grad),
+                  'bias': (m.conv.bias.grad, ref.conv.bias.grad),
+                  'gamma': (m.norm.weight.grad, ref.norm.weight.grad),
+                  'beta': (m.norm.bias.grad, ref.norm.bias.grad)})
+
+
 def test_generator_eval_mode_input_gradient():
     """SelfAttention_G in eval mode with gradients enabled (every BatchNorm on its running
     statistics): the forward equals the no-grad eval forward, and d(pose)/d(mel) matches the
