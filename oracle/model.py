@@ -147,7 +147,7 @@ def _gat_fn(x, edges, lw, a_s, a_d, bias, heads):
     e = F.leaky_relu(asrc[ei[0]] + adst[ei[1]], 0.2)
     alpha = pyg._segment_softmax(e, ei[1], N)
     msg = xp[ei[0]] * alpha.unsqueeze(-1)   # (under autocast: bf16 rows x fp32 weights -> fp32)
-    out = torch.zeros(xp.shape, dtype=msg.dtype).index_add(0, ei[1], msg)
+    out = torch.zeros(xp.shape, dtype=msg.dtype, device=xp.device).index_add(0, ei[1], msg)
     return out.mean(1) + bias
 
 

@@ -75,7 +75,8 @@ class GATConv(nn.Module):
         e = F.leaky_relu(a_src[src] + a_dst[dst], self.negative_slope)
         alpha = _segment_softmax(e, dst, N)
         msg = xp[src] * alpha.unsqueeze(-1)
-        out = torch.zeros((N, H, C), dtype=x.dtype, device=x.device).index_add_(0, dst, msg)
+        # PyG scatters into an output of the message dtype (fp32 under autocast: bf16 x * fp32 alpha)
+        out = torch.zeros((N, H, C), dtype=msg.dtype, device=x.device).index_add_(0, dst, msg)
         out = out.reshape(N, H * C) if self.concat else out.mean(dim=1)
         if self.bias is not None:
             out = out + self.bias

@@ -275,9 +275,12 @@ def test_bf16_train_step_b32():
     assert abs(res['bf16'][2] - res['fp32'][2]) < 1e-2 * abs(res['fp32'][2])
     assert abs(res['bf16'][3] - res['fp32'][3]) < 2e-2 * abs(res['fp32'][3])
     assert cb[0] >= 0.999 and cb[1] >= 0.999, cb
-    ref = json.load(open(os.path.join(GOLDEN_DIR, 'bf16_autocast.json')))
-    assert cg[0] >= ref['g_cos_global'] - 0.03 and cg[1] >= ref['g_cos_weight_median'] - 0.03, (cg, ref)
-    assert cd[0] >= ref['d_cos_global'] - 0.01, (cd, ref)
+    # pinned to both: the oracle under autocast and the reference's own modules under autocast
+    # (tests/golden/bf16_autocast_ref.json; the two agree within 0.011, test_oracle_golden.py)
+    for name in ('bf16_autocast.json', 'bf16_autocast_ref.json'):
+        ref = json.load(open(os.path.join(GOLDEN_DIR, name)))
+        assert cg[0] >= ref['g_cos_global'] - 0.03 and cg[1] >= ref['g_cos_weight_median'] - 0.03, (name, cg, ref)
+        assert cd[0] >= ref['d_cos_global'] - 0.01, (name, cd, ref)
     assert cd[0] > 0.99
     torch.manual_seed(0)
     from a2m.real_motion_model import SelfAttention_D, SelfAttention_G

@@ -454,13 +454,19 @@ def _grad_errors(module, t, f64, prefix):
 
 def _check_grad_errors(errs, prefix, med_ratio, max_floor, max_ratio):
     """Median GPU error <= med_ratio x the reference's median error; every parameter within
-    max(max_floor, max_ratio x the reference's own error on that parameter)."""
+    max_ratio x max(the reference's own error on that parameter, max_floor).  max_floor is an
+    fp32-noise scale (relative to the gradient's scale): it only binds where the reference's own
+    error is itself below it, so a parameter the reference gets to 4e-5 cannot pass at 5e-2
+    (the old absolute 5 % floor could hide a >1,000x regression)."""
     e = np.array([x[1] for x in errs])
     r = np.array([x[2] for x in errs])
-    bad = [x for x in errs if x[1] > max(max_floor, max_ratio * x[2])]
+    bound = [max_ratio * max(x[2], max_floor) for x in errs]
+    bad = [(x, b) for x, b in zip(errs, bound) if x[1] > b]
+    ratios = sorted(((x[1] / max(x[2], max_floor), x[0]) for x in errs), reverse=True)
     print(f'{prefix}: median err vs exact {np.median(e):.2e} (reference fp32 {np.median(r):.2e}, '
           f'ratio {np.median(e) / max(np.median(r), 1e-30):.2f}), max {e.max():.2e} '
-          f'(reference {r.max():.2e}); worst {sorted(errs, key=lambda x: -x[1])[:3]}')
+          f'(reference {r.max():.2e}); worst {sorted(errs, key=lambda x: -x[1])[:3]}; '
+          f'largest err / max(ref, floor): {[(n, round(float(q), 2)) for q, n in ratios[:5]]}')
     assert not bad, bad[:10]
     assert np.median(e) <= med_ratio * np.median(r), (np.median(e), np.median(r))
 
@@ -471,10 +477,11 @@ def _check_grad_errors(errs, prefix, med_ratio, max_floor, max_ratio):
 # test_train_step_vs_reference.
 STEP_CASES = {
     # B=16: the gradient bounds DESIGN.md 2.3 states
-    'b16': dict(fixture='train_step_b16t64', tol_out=1e-4, med=2.0, floor=0.05, ratio=8.0),
-    # B=2: batch-statistics BN over 8-16 values in D; outputs at 4e-4 and the loose gradient
-    # bounds of the round-1 test (kept as a second, smaller case)
-    'b2': dict(fixture='train_step_b2t64', tol_out=4e-4, med=8.0, floor=0.6, ratio=10.0),
+    # (every parameter within 8x max(reference error, 1e-4); the round-5 bound was max(5 %, 8x))
+    'b16': dict(fixture='train_step_b16t64', tol_out=1e-4, med=2.0, floor=1e-4, ratio=8.0),
+    # B=2: batch-statistics BN over 8-16 values in D; outputs at 4e-4 and looser gradient
+    # bounds (kept as a second, smaller case; the round-1 bound was max(60 %, 10x))
+    'b2': dict(fixture='train_step_b2t64', tol_out=4e-4, med=8.0, floor=1e-3, ratio=10.0),
 }
 
 
