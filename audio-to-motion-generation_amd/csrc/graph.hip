@@ -28,6 +28,14 @@ constexpr int GF = 64;          // joint feature dim
 #ifndef STACK_WG_PER_CU
 #define STACK_WG_PER_CU 3
 #endif
+// 1: the stack's layer products computed transposed (MFMA rows = output features, columns = the
+// wave's 32 nodes), so each lane ends a layer holding 32 of its node's 64 features and the
+// partner lane (l ^ 32) the other 32: the LayerNorm statistics are register sums plus one
+// v_permlane32_swap, with no per-wave LDS scratch and no wave barriers (0: the round-2 epilogue
+// through an 8-row LDS scratch)
+#ifndef STACK_TEPI
+#define STACK_TEPI 1
+#endif
 constexpr int GHEADS = 4;
 constexpr int GMAXN = 128;      // node rows per workgroup (4 waves x 32 MFMA rows)
 constexpr int ZP = GF + 4;      // LDS row pitch (floats): 16-B aligned, conflict-free b128 reads
@@ -328,6 +336,7 @@ __device__ __forceinline__ void stack_mfma4(const float (&af)[4], const float4 (
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       if (STACK_ABL == 1) acc[t][s] += af[s] * bf[s];
+      else if (STACK_TEPI) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(bf[s], af[s], acc[t], 0, 0, 0);
       else acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc[t], 0, 0, 0);
     }
   }
@@ -500,7 +509,8 @@ __device__ __forceinline__ void stack_layer_kh(const float* xs, const float (*al
         const float4 b0 = *reinterpret_cast<const float4*>(wr);
         const float4 b1 = *reinterpret_cast<const float4*>(wr + 4);
         const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, stack_pack8(bv), acc[t], 0, 0, 0);
+        if (STACK_TEPI) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(stack_pack8(bv), af, acc[t], 0, 0, 0);
+        else acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, stack_pack8(bv), acc[t], 0, 0, 0);
       }
     }
   }
@@ -552,8 +562,10 @@ __global__ __launch_bounds__(256, BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU)
   __shared__ unsigned char ndeg[GMAXN];
   __shared__ unsigned char rown[GMAXN];                                // MFMA row -> node (0xff: none)
   __shared__ int csr[2 * GMAXN];
+#if !STACK_TEPI
   __shared__ __attribute__((aligned(16))) float osc[4][8 * ZP];         // per-wave epilogue scratch (8 rows)
-  __shared__ __attribute__((aligned(16))) float lnp[2 * GF];            // this layer's LN weight | bias
+#endif
+  __shared__ __attribute__((aligned(16))) float lnp[3 * GF];            // this layer's LN weight | bias | layer bias
 
   const int fpb = GMAXN / J;
   const int NBmax = fpb * J;
@@ -677,8 +689,69 @@ __global__ __launch_bounds__(256, BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU)
     // contiguous features of a row: the LayerNorm sums are 8-element register sums plus two
     // DPP adds over the row's 8 lanes, instead of cross-lane reductions in the MFMA layout.
     const float scale = gat ? 1.f / GHEADS : 1.f;
-    if (tid < 2 * GF) lnp[tid] = tid < GF ? S.ln_w[L][tid] : S.ln_b[L][tid - GF];
+    if (tid < 3 * GF) lnp[tid] = tid < GF ? S.ln_w[L][tid] : tid < 2 * GF ? S.ln_b[L][tid - GF] : S.bias[L][tid - 2 * GF];
     __syncthreads();   // every gather of this layer has read the tile; LN params visible
+#if STACK_TEPI
+    {
+      // lane (li, lh) holds features 32 t + 8 g + 4 lh + j (j < 4) of node `node` (MFMA column li)
+      // in acc[t][4 g + j]; lane li ^ 32 holds the others
+      const bool last_l = L + 1 == S.nlayers;
+      float v[2][16];
+      float sm = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bb = *reinterpret_cast<const float4*>(lnp + 2 * GF + 32 * t + 8 * g + 4 * lh);
+          const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[t][4 * g + j] = acc[t][4 * g + j] * scale + bv[j];
+            sm += v[t][4 * g + j];
+          }
+        }
+      {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(sm), __float_as_uint(sm), false, false);
+        sm = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      }
+      const float mean = sm * (1.f / GF);
+      float sq = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sq += (v[t][e] - mean) * (v[t][e] - mean);
+      {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(sq), __float_as_uint(sq), false, false);
+        sq = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      }
+      const float rstd = 1.f / sqrtf(sq * (1.f / GF) + 1e-5f);
+      if (live) {
+        float* xr = xs + node * ZP;
+        float* yr = y + (node0 + node) * GF;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int f = 32 * t + 8 * g + 4 * lh;
+            const float4 xv = *reinterpret_cast<const float4*>(xr + f);
+            const float4 w = *reinterpret_cast<const float4*>(lnp + f);
+            const float4 bb = *reinterpret_cast<const float4*>(lnp + GF + f);
+            const float* q = &v[t][4 * g];
+            float4 u;
+            u.x = (q[0] - mean) * rstd * w.x + bb.x;
+            u.y = (q[1] - mean) * rstd * w.y + bb.y;
+            u.z = (q[2] - mean) * rstd * w.z + bb.z;
+            u.w = (q[3] - mean) * rstd * w.w + bb.w;
+            u.x = (u.x > 0.f ? u.x : u.x * S.slope) + xv.x;
+            u.y = (u.y > 0.f ? u.y : u.y * S.slope) + xv.y;
+            u.z = (u.z > 0.f ? u.z : u.z * S.slope) + xv.z;
+            u.w = (u.w > 0.f ? u.w : u.w * S.slope) + xv.w;
+            if (last_l) *reinterpret_cast<float4*>(yr + f) = u;
+            else *reinterpret_cast<float4*>(xr + f) = u;
+          }
+      }
+    }
+#else
     {
       const float* bias = S.bias[L];
       const float b0 = bias[li], b1 = bias[32 + li];
@@ -735,6 +808,7 @@ __global__ __launch_bounds__(256, BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU)
         }
       }
     }
+#endif
     const bool last = L + 1 == S.nlayers;
     if (!last) __syncthreads();   // the layer's output is the next layer's tile
   }
