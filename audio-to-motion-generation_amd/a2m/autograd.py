@@ -298,9 +298,11 @@ _GRAPH_SAVE_PRE = os.environ.get('A2M_GRAPH_SAVE_PRE', '1') != '0'
 class _GraphLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w0, w1, att_src, att_dst, bias, ln_w, ln_b, topo):
-        J, kind, ptr, idx, norm_res = topo
+        J, kind, ptr, idx, norm_res, grads = topo
         x = x.contiguous()
-        pre = torch.empty_like(x) if norm_res and _GRAPH_SAVE_PRE else None
+        # the pre-LayerNorm copy only when a backward will read it (not under no_grad, nor when no
+        # input needs a gradient: e.g. a validation forward in train mode)
+        pre = torch.empty_like(x) if norm_res and _GRAPH_SAVE_PRE and grads else None
         y = F.graph_layer(x, J, kind, ptr, idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
                           norm_res=norm_res, pre_ln=pre)
         ctx.save_for_backward(x, w0, w1, att_src, att_dst, bias, ln_w, ln_b, pre)
@@ -310,22 +312,29 @@ class _GraphLayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w0, w1, att_src, att_dst, bias, ln_w, ln_b, pre = ctx.saved_tensors
-        J, kind, ptr, idx, norm_res = ctx.topo
+        J, kind, ptr, idx, norm_res, _ = ctx.topo
         dx, dw0, dw1, das, dad, dbias, dlw, dlb = F.graph_layer_bwd(
             x, dy, J, kind, ptr, idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
             norm_res=norm_res, pre_ln=pre)
         return dx, dw0, dw1, das, dad, dbias, dlw, dlb, None
 
 
+def _grads_wanted(*ts):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
 def gat(g, x, J, ptr, idx, ln=None):
-    return _GraphLayer.apply(x, g.lin.weight, None, g.att_src, g.att_dst, g.bias,
-                             ln.weight if ln is not None else None, ln.bias if ln is not None else None,
-                             (J, 0, ptr, idx, ln is not None))
+    lw, lb = (ln.weight, ln.bias) if ln is not None else (None, None)
+    return _GraphLayer.apply(x, g.lin.weight, None, g.att_src, g.att_dst, g.bias, lw, lb,
+                             (J, 0, ptr, idx, ln is not None,
+                              _grads_wanted(x, g.lin.weight, g.att_src, g.att_dst, g.bias, lw, lb)))
 
 
 def graph_conv(g, x, J, ptr, idx, ln):
     return _GraphLayer.apply(x, g.lin_rel.weight, g.lin_root.weight, None, None, g.lin_rel.bias,
-                             ln.weight, ln.bias, (J, 1, ptr, idx, True))
+                             ln.weight, ln.bias,
+                             (J, 1, ptr, idx, True, _grads_wanted(x, g.lin_rel.weight, g.lin_root.weight,
+                                                                  g.lin_rel.bias, ln.weight, ln.bias)))
 
 
 class _Dropout(torch.autograd.Function):

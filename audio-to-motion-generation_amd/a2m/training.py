@@ -21,6 +21,7 @@ are frozen during the G steps: the reference computes their gradients there and 
 away (optimizer_D.zero_grad() at :388).
 """
 import contextlib
+import time
 
 import numpy as np
 import torch
@@ -460,6 +461,11 @@ class GANTrainer:
                 return self._body(fn, args)
             st = _CapturedStep(key, [a.detach().clone() for a in args])
             torch.cuda.synchronize()
+            if self._collectives:
+                # RCCL's watchdog thread polls the events of finished eager collectives (every
+                # ~100 ms); HIP refuses a query on an event whose stream has since joined a capture
+                # (hipErrorCapturedEvent), so let it retire them before the NCCL stream is captured
+                time.sleep(0.5)
             steps = opt.step_count
             # each graph keeps its own memory pool: a host cache can drop a buffer that one graph
             # still writes on replay, and only that graph's own recapture may reuse it

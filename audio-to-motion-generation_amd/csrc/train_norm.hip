@@ -16,6 +16,12 @@ namespace a2m {
 // activation is 1,024 workgroups instead of 256 at one latency-bound round trip per element)
 constexpr int kSlice = 1024;
 
+// A2M_BN_CHAN=0: every BatchNorm on the sliced kernels (the round-5 path; A/B and tests)
+static bool chan_path_off() {
+  static const bool off = std::getenv("A2M_BN_CHAN") && std::atoi(std::getenv("A2M_BN_CHAN")) == 0;
+  return off;
+}
+
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
   uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -300,6 +306,156 @@ __global__ void bn_eval_consts_kernel(const float* rmean, const float* rvar, int
   }
 }
 
+// Whole-channel BatchNorm (round 6): one workgroup per channel when a channel's B * L elements fit
+// the workgroup's registers (kChanMax): the forward reads x once, reduces (sum z, sum z^2) in the
+// workgroup (float64, fixed order), finalises mean / rstd / the running statistics and applies, in
+// ONE launch (the sliced path: stats + apply, x read twice); the backward reads dy and x once and
+// writes dgamma / dbeta, dx and the conv-bias gradient in ONE launch (the sliced path: three).  At
+// the training step's sizes most BatchNorms are latency- and launch-bound (decoder 256 x 4096,
+// UNet 512..2048 x 1024..4096, D), so the launch count and the second read are the cost.
+constexpr int kChanMax = 16384;
+
+template <int NT, int EPT>
+__global__ __launch_bounds__(NT) void bn_train_chan_kernel(BNArgs a_in, float eps, float momentum,
+                                                                      float* rmean, float* rvar, float* mean_out,
+                                                                      float* rstd_out, const float* gamma,
+                                                                      const float* beta, int act, float slope,
+                                                                      float* y, int64_t ys_b, int64_t ys_c) {
+  A2M_BN_RESOLVE(BNArgs, a_in);
+  __shared__ double red[NT / 64];
+  const int c = blockIdx.x;
+  const int N = a.B * a.L;
+  float z[EPT];
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int i = threadIdx.x + NT * j;
+    z[j] = 0.f;
+    if (i < N) {
+      const int b = i / a.L, l = i - b * a.L;
+      z[j] = a.x[b * a.xs_b + c * a.xs_c + l] * pre_drop(a, b, c, l);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    s1 += z[j];
+    s2 += (double)z[j] * z[j];
+  }
+  s1 = block_sum_d(s1, red);
+  s2 = block_sum_d(s2, red);
+  const double mean = s1 / (double)N;
+  double var = s2 / (double)N - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  const float mu = (float)mean, rs = (float)(1.0 / sqrt(var + (double)eps));
+  if (threadIdx.x == 0) {
+    mean_out[c] = mu;
+    rstd_out[c] = rs;
+    if (rmean) {
+      const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
+      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+  }
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int i = threadIdx.x + NT * j;
+    if (i < N) {
+      const int b = i / a.L, l = i - b * a.L;
+      float v = act_fwd((z[j] - mu) * rs * g + bt, act, slope);
+      if (a.mode == DROP_AFTER) v *= drop_scale(a.seed, ((uint64_t)b * a.C + c) * a.L + l, a.p);
+      y[b * ys_b + c * ys_c + l] = v;
+    }
+  }
+}
+
+template <int NT, int EPT>
+__global__ __launch_bounds__(NT) void bn_bwd_chan_kernel(BNBwdArgs a_in, float* dgamma, float* dbeta,
+                                                                    float* dx, float* dbias) {
+  A2M_BNB_RESOLVE(a_in);
+  __shared__ double red[NT / 64];
+  const BNArgs& f = a.f;
+  const int c = blockIdx.x;
+  const int N = f.B * f.L;
+  const float mu = a.mean[c], rs = a.rstd[c], gm = a.gamma ? a.gamma[c] : 1.f;
+  float xh[EPT], gg[EPT], ds[EPT];
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int i = threadIdx.x + NT * j;
+    xh[j] = gg[j] = ds[j] = 0.f;
+    if (i < N) {
+      const int b = i / f.L, l = i - b * f.L;
+      ds[j] = pre_drop(f, b, c, l);
+      xh[j] = (f.x[b * f.xs_b + c * f.xs_c + l] * ds[j] - mu) * rs;
+      gg[j] = bn_g(a, b, c, l, xh[j]);
+    }
+  }
+  double sg = 0.0, sgx = 0.0;
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    sg += gg[j];
+    sgx += (double)gg[j] * xh[j];
+  }
+  const float fsg = (float)block_sum_d(sg, red), fsgx = (float)block_sum_d(sgx, red);
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = fsgx;
+    if (dbeta) dbeta[c] = fsg;
+  }
+  const float mg = fsg / a.n_div, mgx = fsgx / a.n_div;
+  double sd = 0.0;
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int i = threadIdx.x + NT * j;
+    if (i < N) {
+      const int b = i / f.L, l = i - b * f.L;
+      const float v = gm * rs * (gg[j] - mg - xh[j] * mgx) * ds[j];
+      dx[((int64_t)b * f.C + c) * f.L + l] = v;
+      sd += v;
+    }
+  }
+  sd = block_sum_d(sd, red);
+  if (threadIdx.x == 0 && dbias) dbias[c] = (float)sd;
+}
+
+// the whole-channel launches, EPT = elements per thread (a power of two >= N / 256); false when the
+// channel does not fit (the sliced kernels run instead)
+static bool bn_chan_fwd(const BNArgs& a, float eps, float momentum, float* rmean, float* rvar, float* mean_out,
+                        float* rstd_out, const float* gamma, const float* beta, int act, float slope, float* y,
+                        int64_t ys_b, int64_t ys_c, hipStream_t st) {
+  const int64_t N = (int64_t)a.B * a.L;
+  if (N > kChanMax || chan_path_off()) return false;
+#define A2M_CHAN_FWD(T, E) hipLaunchKernelGGL((bn_train_chan_kernel<T, E>), dim3(a.C), dim3(T), 0, st, a, eps, \
+                                              momentum, rmean, rvar, mean_out, rstd_out, gamma, beta, act, slope, y, \
+                                              ys_b, ys_c)
+  // 1,024 threads (16 waves) for channels of >= 4,096 elements: every load of the channel in flight
+  // at once (256 threads took 14.6 us a call at 4,096 elements, latency-bound)
+  if (N <= 256) A2M_CHAN_FWD(256, 1);
+  else if (N <= 512) A2M_CHAN_FWD(256, 2);
+  else if (N <= 1024) A2M_CHAN_FWD(256, 4);
+  else if (N <= 2048) A2M_CHAN_FWD(512, 4);
+  else if (N <= 4096) A2M_CHAN_FWD(1024, 4);
+  else if (N <= 8192) A2M_CHAN_FWD(1024, 8);
+  else A2M_CHAN_FWD(1024, 16);
+#undef A2M_CHAN_FWD
+  return true;
+}
+
+static bool bn_chan_bwd(const BNBwdArgs& a, float* dgamma, float* dbeta, float* dx, float* dbias, hipStream_t st) {
+  const int64_t N = (int64_t)a.f.B * a.f.L;
+  if (N > kChanMax || chan_path_off()) return false;
+#define A2M_CHAN_BWD(T, E) hipLaunchKernelGGL((bn_bwd_chan_kernel<T, E>), dim3(a.f.C), dim3(T), 0, st, a, dgamma, \
+                                              dbeta, dx, dbias)
+  if (N <= 256) A2M_CHAN_BWD(256, 1);
+  else if (N <= 512) A2M_CHAN_BWD(256, 2);
+  else if (N <= 1024) A2M_CHAN_BWD(256, 4);
+  else if (N <= 2048) A2M_CHAN_BWD(512, 4);
+  else if (N <= 4096) A2M_CHAN_BWD(1024, 4);
+  else if (N <= 8192) A2M_CHAN_BWD(1024, 8);
+  else A2M_CHAN_BWD(1024, 16);
+#undef A2M_CHAN_BWD
+  return true;
+}
+
 // SyncBN helpers: per-channel float64 (sum, sum2) pairs over the slices (all-reduced by the
 // host between the stats and apply phases), and the finalize / conversion steps on them.
 __global__ void reduce_pairs_kernel(const double* part, int C, int slices, double* sums,
@@ -486,6 +642,11 @@ int a2m_bn_train_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int32_t B, 
   if (!ws || ws_bytes < need) { set_error("bn_train_fwd: workspace too small (%zu < %zu bytes)", ws_bytes, need); return A2M_EWS; }
   BNArgs a{x, xs_b, xs_c, B, C, L, S, drop_p, drop_mode, seed, g_seed_off};
   hipStream_t st = as_stream(stream);
+  if (bn_chan_fwd(a, eps, momentum, running_mean, running_var, save_mean, save_rstd, gamma, beta, act, slope, y,
+                  ys_b, ys_c, st)) {
+    A2M_LAUNCH_CHECK();
+    return A2M_OK;
+  }
   double* part = static_cast<double*>(ws);
   hipLaunchKernelGGL(bn_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
   A2M_LAUNCH_CHECK();
@@ -514,6 +675,10 @@ int a2m_bn_train_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const fl
   a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
   a.n_div = (float)N;
   hipStream_t st = as_stream(stream);
+  if (bn_chan_bwd(a, dgamma, dbeta, dx, dbias, st)) {
+    A2M_LAUNCH_CHECK();
+    return A2M_OK;
+  }
   double* part = static_cast<double*>(ws);
   double* dpart = part + 2 * (size_t)C * S;
   hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);
@@ -571,6 +736,10 @@ int a2m_bn_eval_bwd_f32(const float* dy, int64_t dys_b, int64_t dys_c, const flo
   a.mean = save_mean; a.rstd = save_rstd; a.gamma = gamma; a.beta = beta; a.act = act; a.slope = slope;
   a.n_div = __builtin_inff();   // fixed statistics: no mean(g) / mean(g xhat) terms
   hipStream_t st = as_stream(stream);
+  if (bn_chan_bwd(a, dgamma, dbeta, dx, dbias, st)) {
+    A2M_LAUNCH_CHECK();
+    return A2M_OK;
+  }
   double* part = static_cast<double*>(ws);
   double* dpart = part + 2 * (size_t)C * S;
   hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(C * S), dim3(256), 0, st, a, part);

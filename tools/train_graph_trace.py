@@ -30,5 +30,11 @@ print(f'{n_it} iterations: kernel time {sum(busy) / n_it:.3f} ms, span {sum(span
 print('per iteration kernel ms:', ' '.join(f'{b:.2f}' for b in busy))
 print('per iteration span ms:  ', ' '.join(f'{s:.2f}' for s in span))
 tot = sum(v[1] for v in agg.values())
-for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:30]:
+fam = {'batchnorm (bn_*, reduce_slices)': ('bn_', 'reduce_slices'), 'split-K reduce': ('splitk_reduce',),
+       'engine tiles (gemm_kernel, gemm_pipe*)': ('gemm_kernel', 'gemm_pipe')}
+for name, keys in fam.items():
+    us = sum(v[1] for k, v in agg.items() if any(q in k for q in keys))
+    n = sum(v[0] for k, v in agg.items() if any(q in k for q in keys))
+    print(f'family {name}: {us / n_it / 1e3:.3f} ms / iter, {n / n_it:.0f} launches / iter')
+for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
     print(f'{us / n_it:10.1f} us/iter {n / n_it:7.1f} calls/iter {100 * us / tot:5.1f}%  {k}')
