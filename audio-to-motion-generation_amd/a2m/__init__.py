@@ -14,11 +14,10 @@ __version__ = '0.1.0'
 def set_gemm_precision(dtype):
     """Operand precision of every GEMM-engine launch issued afterwards: 'fp32' (default, the
     parity configuration: v_mfma_f32_32x32x2_f32), 'bf16' (bf16 operands, fp32 accumulation,
-    fp32 storage -- the torch.autocast(dtype=torch.bfloat16)-equivalent of BASELINE configs[4])
-    or 'bf16x6' (fp32 operands split exactly into three bf16 pieces on their way into LDS, the
-    six products of order >= 2^-16 accumulated in fp32 on the bf16 MFMA: fp32-class results at
-    16/6 of the f32 MFMA rate).  Returns the previous setting.  HIP graphs keep the precision
-    they were captured with."""
+    fp32 storage -- the torch.autocast(dtype=torch.bfloat16)-equivalent of BASELINE configs[4]).
+    ('bf16x6', three-way bf16 operand splits, exists only in a library built with
+    -DA2M_WITH_X6: it measured slower than fp32)  Returns the previous setting.
+    HIP graphs keep the precision they were captured with."""
     prev = _PREC_NAMES[_native.lib.a2m_get_gemm_precision()]
     if dtype in ('bf16', torch.bfloat16):
         flag = 1
@@ -27,7 +26,7 @@ def set_gemm_precision(dtype):
     elif dtype == 'bf16x6':
         flag = 2
     else:
-        raise ValueError(f'unsupported GEMM precision {dtype!r} (fp32, bf16 or bf16x6)')
+        raise ValueError(f'unsupported GEMM precision {dtype!r} (fp32 or bf16)')
     _native.check(_native.lib.a2m_set_gemm_precision(flag))
     return prev
 

@@ -730,9 +730,11 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     if (pipe_bf16) launch_pipe_bf16(a, ma, mb, batch, stream);
     else if (p.bm == 128) launch_tile<128, 128, 64, 1>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 64, 1>(a, ma, mb, batch, stream);
+#ifdef A2M_WITH_X6
   } else if (prec == 2) {
     if (p.bm == 128) launch_tile<128, 128, 32, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, 2>(a, ma, mb, batch, stream);
+#endif
   } else {
     if (pipe_launch) launch_pipe(a, ma, mb, batch, stream);
     else if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
@@ -788,7 +790,13 @@ int a2m_gemm_pipe_override(int32_t mode) {
 }
 
 int a2m_set_gemm_precision(int32_t prec) {
+#ifdef A2M_WITH_X6
   A2M_CHECK_ARG(prec >= 0 && prec <= 2, "set_gemm_precision: %d (0 = fp32, 1 = bf16, 2 = bf16x6)", prec);
+#else
+  // bf16x6 (2) is a build-time option (make EXTRA=-DA2M_WITH_X6): an experiment that measured
+  // slower than fp32 end to end, so the shipped library carries fp32 and bf16 only
+  A2M_CHECK_ARG(prec >= 0 && prec <= 1, "set_gemm_precision: %d (0 = fp32, 1 = bf16)", prec);
+#endif
   a2m::g_gemm_prec = prec;
   return A2M_OK;
 }

@@ -488,15 +488,12 @@ def run_train(args, world, rank, dev):
 
 
 def dtype_label(dtype):
-    """Arithmetic type of the GEMMs: f32; bf16 (bf16 operands, f32 accumulation); bf16x6 (f32
-    operands split exactly into three bf16 planes, six bf16 products: f32-class results)."""
-    return {'fp32': 'f32', 'bf16': 'bf16', 'bf16x6': 'bf16x6'}[dtype]
+    """Arithmetic type of the GEMMs: f32; bf16 (bf16 operands, f32 accumulation)."""
+    return {'fp32': 'f32', 'bf16': 'bf16'}[dtype]
 
 
 def mfma_peak(dtype):
-    # bf16x6: six bf16 MFMAs per fp32-class product -> the fp32-equivalent ceiling is bf16 / 6
-    return {'fp32': FP32_MFMA_PEAK_TFLOPS, 'bf16': BF16_MFMA_PEAK_TFLOPS,
-            'bf16x6': BF16_MFMA_PEAK_TFLOPS / 6}[dtype]
+    return {'fp32': FP32_MFMA_PEAK_TFLOPS, 'bf16': BF16_MFMA_PEAK_TFLOPS}[dtype]
 
 
 def roofline_entry(it, gt, peak=None, dispatch_ms=0.0, tr=None):
@@ -715,7 +712,7 @@ def main():
                     help='train mode: SyncBN over the DP ranks (SURVEY 8(e)); default per-rank statistics')
     ap.add_argument('--bucket-mb', type=float, default=25.0,
                     help='train mode: gradient all-reduce bucket size (MB)')
-    ap.add_argument('--dtype', choices=('fp32', 'bf16', 'bf16x6'), default='fp32',
+    ap.add_argument('--dtype', choices=('fp32', 'bf16'), default='fp32',
                     help='GEMM operand precision (bf16: configs[4], fp32 accumulation/storage)')
     ap.add_argument('--trace-child', type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument('--no-trace', action='store_true',

@@ -555,9 +555,8 @@ int a2m_gemm_pipe_override(int32_t mode);
  * backward) issued after the call: 0 = fp32 (default; the parity configuration), 1 = bf16
  * operands with fp32 accumulation (BASELINE configs[4], torch.autocast(bfloat16)-equivalent:
  * weights and activations stay fp32 in HBM, rounded to bf16 where they enter the MFMA),
- * 2 = bf16x6 (fp32 operands split exactly into hi + mid + lo bf16 pieces where they enter LDS;
- * the six products a_i b_j with i + j <= 2 accumulate in fp32 on the bf16 MFMA: fp32-class
- * results, each dropped term below 2^-24 |a b|).
+ * (2 = bf16x6, fp32 operands split into three bf16 pieces, six products: only in a library built
+ * with -DA2M_WITH_X6, an experiment measured slower than fp32; A2M_EINVAL otherwise).
  * Process-wide; not thread-safe against concurrent launches. */
 int a2m_set_gemm_precision(int32_t prec);
 int32_t a2m_get_gemm_precision(void);

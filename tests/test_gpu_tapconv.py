@@ -1,11 +1,10 @@
-"""Tap-chunked conv1d (a2m_conv1d_tap_fwd_f32, GEMM loader mode 5) and the bf16x6 engine precision.
+"""Tap-chunked conv1d (a2m_conv1d_tap_fwd_f32, GEMM loader mode 5) at fp32 and bf16 operand precision.
 
 The tap path is the forward of nn.Conv1d(k, stride=1, padding=(k-1)/2) (model_layers.py:75-120,
 the ConvNormRelu / ResBlock convs of the UNet and both decoders) without an im2col matrix: the
 B loader stages each channel chunk's x window once and re-stores it shifted per tap.  It must
 agree with an fp64 convolution at fp32 accuracy, wrap nothing across clip boundaries, and
-match the im2col path it replaces.  bf16x6 (three-way bf16 operand split, six products) must
-be fp32-class against fp64.
+match the im2col path it replaces.
 """
 import os
 
@@ -27,7 +26,7 @@ def _conv_ref(x, w, b, pad):
                                       padding=pad)
 
 
-@pytest.mark.parametrize('prec', ['fp32', 'bf16x6', 'bf16'])
+@pytest.mark.parametrize('prec', ['fp32', 'bf16'])
 @pytest.mark.parametrize('B,Ci,Co,T,k', [(64, 256, 256, 64, 3), (8, 512, 1024, 32, 3),
                                          (5, 1024, 2048, 16, 3), (1, 256, 512, 16, 3),
                                          (3, 64, 96, 8, 5), (2, 32, 20, 4, 3)])
@@ -146,35 +145,6 @@ def test_tap_conv1d_rejects_ineligible():
                                           chunk, None, 64, 3, 1, None, None, None, None, 1e-5, 0,
                                           0.2, y.data_ptr(), 64 * 64, 64, 1, None, 0, None)
     assert rc == N.A2M_EINVAL and 'chunk' in N.last_error()
-
-
-@pytest.mark.parametrize('M,N,K', [(256, 4096, 768), (300, 1000, 500), (1024, 2048, 6144)])
-def test_bf16x6_gemm_fp32_class(M, N, K):
-    """bf16x6 against fp64 on unrounded fp32 operands: within fp32 accumulation error."""
-    import a2m
-    from a2m import functional as F
-    g = torch.Generator().manual_seed(M * 3 + K)
-    A = torch.randn(M, K, generator=g)
-    B = torch.randn(N, K, generator=g)
-    ref = A.double() @ B.double().t()
-    C = torch.empty(M, N, device=DEV)
-    with a2m.gemm_precision('bf16x6'):
-        F.gemm(M, N, K, A.to(DEV), K, 1, B.to(DEV), K, 1, C, N, 1)
-    assert rel_err(C.cpu().double(), ref) < TOL32
-
-
-def test_bf16x6_generator_eval_golden(g_state):
-    """G eval (B=2, T=64 reference fixture) with every GEMM in bf16x6: north_star's 1e-4."""
-    import a2m
-    from a2m.real_motion_model import SelfAttention_G
-    z = golden('g_eval_b2t64.npz')
-    g = SelfAttention_G(p=0.0)
-    g.load_state_dict(g_state, strict=False)
-    g = g.to(DEV).eval()
-    with torch.no_grad(), a2m.gemm_precision('bf16x6'):
-        pose, _ = g(torch.from_numpy(z['audio']).to(DEV))
-    e = rel_err(pose.cpu(), z["pose"])
-    assert e < 1e-4, e
 
 
 @pytest.mark.parametrize('B,Ci,Co,H,W,k,s,p,cols', [
