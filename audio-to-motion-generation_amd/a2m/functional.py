@@ -370,12 +370,35 @@ def _wkey(ts):
     return (WEIGHTS_EPOCH[0],) + tuple(None if t is None else (t.data_ptr(), t._version) for t in ts)
 
 
+def _adjacent_view(ts, shape):
+    """A view of shape `shape` over the tensors `ts` when they lie back to back in one storage
+    (each contiguous, in order), else None."""
+    t0 = ts[0]
+    off = t0.storage_offset()
+    for t in ts:
+        if not t.is_contiguous() or t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr() or \
+                t.storage_offset() != off:
+            return None
+        off += t.numel()
+    stride = [1] * len(shape)
+    for i in range(len(shape) - 2, -1, -1):
+        stride[i] = stride[i + 1] * shape[i + 1]
+    return torch.as_strided(t0.detach(), shape, stride, t0.storage_offset())
+
+
 def stacked_qkv(wq, bq, wk, bk, wv, bv, cache=None):
-    """[C/4 + C][C] stacked q/k/v weights and [C/4 + C] biases (cached in `cache` if given)."""
+    """[C/4 + C][C] stacked q/k/v weights and [C/4 + C] biases (cached in `cache` if given).
+    When the weights (and the biases) already lie back to back in memory -- FlatAdam places a
+    SelfAttention's parameters that way (optim.flat_order) -- the stack is a view: no copy launch
+    each training step, and a captured graph reads the live weights."""
+    C = wq.shape[1]
+    w = _adjacent_view((wq, wk, wv), (C // 4 + C, C))
+    b = _adjacent_view((bq, bk, bv), (C // 4 + C,)) if w is not None else None
+    if w is not None and b is not None:
+        return w, b
     key = _wkey((wq, bq, wk, bk, wv, bv))
     if cache is not None and cache.get('key') == key:
         return cache['w'], cache['b']
-    C = wq.shape[1]
     w = torch.empty(C // 4 + C, C, device=wq.device)
     b = torch.empty(C // 4 + C, device=wq.device)
     N.check(N.lib.a2m_stack_qkv_f32(_p(wq), _p(bq), _p(wk), _p(bk), _p(wv), _p(bv), C, _p(w), _p(b),

@@ -20,6 +20,33 @@ import torch
 from . import functional as F
 
 
+def flat_order(module):
+    """module.parameters() in FlatAdam placement order: each SelfAttention's query / key / value
+    weights back to back, then their biases (then gamma), so its stacked QKV operand is a view of
+    the flat buffer (functional.stacked_qkv) instead of a copy per weight version -- 80 launches
+    an iteration of the training step.  Every other parameter keeps module order."""
+    from .model_layers import SelfAttention
+    order, seen = [], set()
+
+    def add(p):
+        if id(p) not in seen:
+            seen.add(id(p))
+            order.append(p)
+    grouped = {}
+    for m in module.modules():
+        if isinstance(m, SelfAttention):
+            wq, bq, wk, bk, wv, bv, g = m.weights()
+            grouped[id(wq)] = (wq, wk, wv, bq, bk, bv, g)
+    members = {id(p) for ps in grouped.values() for p in ps}
+    for p in module.parameters():
+        if id(p) in grouped:
+            for q in grouped[id(p)]:
+                add(q)
+        elif id(p) not in members:
+            add(p)
+    return order
+
+
 class FlatAdam:
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         self.params = [p for p in params if p.requires_grad]

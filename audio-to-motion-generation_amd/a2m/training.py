@@ -29,7 +29,7 @@ import torch.distributed as dist
 
 from . import autograd as AG
 from . import functional as F
-from .optim import FlatAdam
+from .optim import FlatAdam, flat_order
 
 
 class DynamicGANTraining:
@@ -363,8 +363,8 @@ class GANTrainer:
         the nccl (RCCL) backend, whose collectives the capture records.  A new input shape or
         GEMM precision recaptures."""
         self.G, self.D = generator, discriminator
-        self.opt_G = FlatAdam(generator.parameters(), lr=lr)
-        self.opt_D = FlatAdam(discriminator.parameters(), lr=lr)
+        self.opt_G = FlatAdam(flat_order(generator), lr=lr)
+        self.opt_D = FlatAdam(flat_order(discriminator), lr=lr)
         self.dyn = dynamic if dynamic is not None else DynamicGANTraining(g_lr=lr / 2, d_lr=lr)
         self.lambda_gan, self.lambda_d = lambda_gan, lambda_d
         self.fixed_labels = fixed_labels          # (valid, fake) values for deterministic runs

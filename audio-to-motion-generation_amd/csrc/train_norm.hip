@@ -315,18 +315,71 @@ __global__ void bn_eval_consts_kernel(const float* rmean, const float* rvar, int
 // UNet 512..2048 x 1024..4096, D), so the launch count and the second read are the cost.
 constexpr int kChanMax = 16384;
 
+// Workgroup sums in fp64 for the whole-channel kernels, as the sliced kernels accumulate (the
+// B = 2 train step is chaotic enough to amplify fp32 statistics into its gradients): wave sums
+// with the DPP / permlane exchanges on the two 32-bit halves of each double (no LDS round trip
+// per step, unlike __shfl_xor), one LDS slot per wave, every thread adding the slots in the same
+// fixed order.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int64_t u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffff), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double wave64_sum_d(double v) {
+  v += dpp_d<DPP_XOR1>(v);
+  v += dpp_d<DPP_XOR2>(v);
+  v += dpp_d<DPP_HALF_MIRROR>(v);
+  v += dpp_d<DPP_MIRROR>(v);
+  {
+    const int64_t u = __double_as_longlong(v);
+    const auto rl = __builtin_amdgcn_permlane16_swap((uint32_t)(u & 0xffffffff), (uint32_t)(u & 0xffffffff), false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+    v = __longlong_as_double(((int64_t)rh[0] << 32) | rl[0]) + __longlong_as_double(((int64_t)rh[1] << 32) | rl[1]);
+  }
+  {
+    const int64_t u = __double_as_longlong(v);
+    const auto rl = __builtin_amdgcn_permlane32_swap((uint32_t)(u & 0xffffffff), (uint32_t)(u & 0xffffffff), false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+    v = __longlong_as_double(((int64_t)rh[0] << 32) | rl[0]) + __longlong_as_double(((int64_t)rh[1] << 32) | rl[1]);
+  }
+  return v;
+}
+template <int NT, int NV>
+__device__ __forceinline__ void chan_sum(double (&v)[NV], double* red) {
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = wave64_sum_d(v[q]);
+  __syncthreads();   // the slots' previous values have been read
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[q * (NT / 64) + (threadIdx.x >> 6)] = v[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) s += red[q * (NT / 64) + w];
+    v[q] = s;
+  }
+}
+
 template <int NT, int EPT>
 __global__ __launch_bounds__(NT) void bn_train_chan_kernel(BNArgs a_in, float eps, float momentum,
-                                                                      float* rmean, float* rvar, float* mean_out,
-                                                                      float* rstd_out, const float* gamma,
-                                                                      const float* beta, int act, float slope,
-                                                                      float* y, int64_t ys_b, int64_t ys_c) {
+                                                            float* rmean, float* rvar, float* mean_out,
+                                                            float* rstd_out, const float* gamma,
+                                                            const float* beta, int act, float slope,
+                                                            float* y, int64_t ys_b, int64_t ys_c) {
   A2M_BN_RESOLVE(BNArgs, a_in);
-  __shared__ double red[NT / 64];
+  __shared__ double red[2 * (NT / 64)];
   const int c = blockIdx.x;
   const int N = a.B * a.L;
+  // the per-channel operands first: their round trips overlap the channel's loads instead of
+  // following the reductions (the running-statistics update ends the kernel)
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  const float rm0 = rmean ? rmean[c] : 0.f, rv0 = rmean ? rvar[c] : 0.f;
   float z[EPT];
-  double s1 = 0.0, s2 = 0.0;
+  double sums[2] = {0.0, 0.0};
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int i = threadIdx.x + NT * j;
@@ -338,13 +391,12 @@ __global__ __launch_bounds__(NT) void bn_train_chan_kernel(BNArgs a_in, float ep
   }
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    s1 += z[j];
-    s2 += (double)z[j] * z[j];
+    sums[0] += z[j];
+    sums[1] += (double)z[j] * z[j];
   }
-  s1 = block_sum_d(s1, red);
-  s2 = block_sum_d(s2, red);
-  const double mean = s1 / (double)N;
-  double var = s2 / (double)N - mean * mean;
+  chan_sum<NT, 2>(sums, red);
+  const double mean = sums[0] / (double)N;
+  double var = sums[1] / (double)N - mean * mean;
   var = var > 0.0 ? var : 0.0;
   const float mu = (float)mean, rs = (float)(1.0 / sqrt(var + (double)eps));
   if (threadIdx.x == 0) {
@@ -352,11 +404,10 @@ __global__ __launch_bounds__(NT) void bn_train_chan_kernel(BNArgs a_in, float ep
     rstd_out[c] = rs;
     if (rmean) {
       const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
-      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+      rmean[c] = (float)((1.0 - momentum) * rm0 + momentum * mean);
+      rvar[c] = (float)((1.0 - momentum) * rv0 + momentum * unb);
     }
   }
-  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int i = threadIdx.x + NT * j;
@@ -371,9 +422,9 @@ __global__ __launch_bounds__(NT) void bn_train_chan_kernel(BNArgs a_in, float ep
 
 template <int NT, int EPT>
 __global__ __launch_bounds__(NT) void bn_bwd_chan_kernel(BNBwdArgs a_in, float* dgamma, float* dbeta,
-                                                                    float* dx, float* dbias) {
+                                                          float* dx, float* dbias) {
   A2M_BNB_RESOLVE(a_in);
-  __shared__ double red[NT / 64];
+  __shared__ double red[2 * (NT / 64)];
   const BNArgs& f = a.f;
   const int c = blockIdx.x;
   const int N = f.B * f.L;
@@ -390,19 +441,20 @@ __global__ __launch_bounds__(NT) void bn_bwd_chan_kernel(BNBwdArgs a_in, float* 
       gg[j] = bn_g(a, b, c, l, xh[j]);
     }
   }
-  double sg = 0.0, sgx = 0.0;
+  double sums[2] = {0.0, 0.0};
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
-    sg += gg[j];
-    sgx += (double)gg[j] * xh[j];
+    sums[0] += gg[j];
+    sums[1] += (double)gg[j] * xh[j];
   }
-  const float fsg = (float)block_sum_d(sg, red), fsgx = (float)block_sum_d(sgx, red);
+  chan_sum<NT, 2>(sums, red);
+  const float fsg = (float)sums[0], fsgx = (float)sums[1];
   if (threadIdx.x == 0) {
     if (dgamma) dgamma[c] = fsgx;
     if (dbeta) dbeta[c] = fsg;
   }
   const float mg = fsg / a.n_div, mgx = fsgx / a.n_div;
-  double sd = 0.0;
+  double sd[1] = {0.0};
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int i = threadIdx.x + NT * j;
@@ -410,11 +462,11 @@ __global__ __launch_bounds__(NT) void bn_bwd_chan_kernel(BNBwdArgs a_in, float* 
       const int b = i / f.L, l = i - b * f.L;
       const float v = gm * rs * (gg[j] - mg - xh[j] * mgx) * ds[j];
       dx[((int64_t)b * f.C + c) * f.L + l] = v;
-      sd += v;
+      sd[0] += v;
     }
   }
-  sd = block_sum_d(sd, red);
-  if (threadIdx.x == 0 && dbias) dbias[c] = (float)sd;
+  chan_sum<NT, 1>(sd, red);
+  if (threadIdx.x == 0 && dbias) dbias[c] = (float)sd[0];
 }
 
 // the whole-channel launches, EPT = elements per thread (a power of two >= N / 256); false when the

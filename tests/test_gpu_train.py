@@ -287,7 +287,7 @@ def test_graph_layer_train(kind, J, lo, norm_res, Fr, save_pre, monkeypatch):
     dev_p = [p.clone().to(DEV).requires_grad_(True) if p is not None else None for p in allp]
     cpu_p = [p.clone().requires_grad_(True) if p is not None else None for p in allp]
     xd, xc = _leaf(x)
-    yd = AG._GraphLayer.apply(xd, *dev_p, (J, kind, ptr, idx, norm_res))
+    yd = AG._GraphLayer.apply(xd, *dev_p, (J, kind, ptr, idx, norm_res, True))
     w0, w1, a_s, a_d, b, lw, lb = cpu_p
     if kind == 0:
         g = OM._gat_fn(xc, edges, w0, a_s, a_d, b, 4)
