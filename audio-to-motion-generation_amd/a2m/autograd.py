@@ -11,7 +11,6 @@ from a2m.autograd.next_seed() (seeded from torch.initial_seed(), or manual_seed(
 BatchNorm in eval mode with gradients enabled normalises with the running statistics (fixed in
 the backward), as nn.BatchNorm*d.eval() does.
 """
-import os
 
 import torch
 
@@ -290,9 +289,6 @@ class _LayerNormBCT(torch.autograd.Function):
         return dx, dw, db, None
 
 
-# A2M_GRAPH_SAVE_PRE=0: the graph-layer backward recomputes the pre-LayerNorm output instead of
-# reading the forward's copy (one [nodes][64] tensor per layer kept for the backward)
-_GRAPH_SAVE_PRE = os.environ.get('A2M_GRAPH_SAVE_PRE', '1') != '0'
 
 
 class _GraphLayer(torch.autograd.Function):
@@ -302,7 +298,7 @@ class _GraphLayer(torch.autograd.Function):
         x = x.contiguous()
         # the pre-LayerNorm copy only when a backward will read it (not under no_grad, nor when no
         # input needs a gradient: e.g. a validation forward in train mode)
-        pre = torch.empty_like(x) if norm_res and _GRAPH_SAVE_PRE and grads else None
+        pre = torch.empty_like(x) if norm_res and grads else None
         y = F.graph_layer(x, J, kind, ptr, idx, w0, w1, att_src, att_dst, bias, ln_w, ln_b,
                           norm_res=norm_res, pre_ln=pre)
         ctx.save_for_backward(x, w0, w1, att_src, att_dst, bias, ln_w, ln_b, pre)

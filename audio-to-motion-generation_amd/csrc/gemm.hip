@@ -273,17 +273,15 @@ static int operand_mode(const Gather& g, int K) {
                          g.divw == 1;
     const bool along_h = g.R2 == 1 && g.R1 > 1 && g.R1 % 4 == 0 && (g.ar1 == 1 || g.ar1 == 2) &&
                          g.sh == 1 && g.divh == 1;
-    static const int allow = env_int("A2M_GEMM_MODE3", 1);
-    return allow && (plain || along_w || along_h) ? 3 : 2;
+    return plain || along_w || along_h ? 3 : 2;
   }
   const bool dense = g.K1 == 1 && g.K2 == 1 && g.sk0 == 1 && g.Lh == 1 && g.Lw == 1 &&
                      g.sh == 0 && g.sw == 0 && g.ch == 0 && g.cw == 0 && g.divh == 1 && g.divw == 1;
   const bool aligned = (reinterpret_cast<uintptr_t>(g.base) % 16 == 0) && (g.sr0 % 4 == 0) &&
                        (g.bstride % 4 == 0) && (K % 4 == 0);
   if (dense && aligned) return 0;
-  static const int allow4 = env_int("A2M_GEMM_MODE4", 1);
   const bool runs = g.K2 % 4 == 0 && g.bk2 == 1 && g.sw == 1 && g.divw == 1;
-  return allow4 && runs ? 4 : 1;
+  return runs ? 4 : 1;
 }
 
 struct Plan {
@@ -315,13 +313,12 @@ static int g_gemm_prec = 0;
 static int gemm_bk(int prec) { return prec == 1 ? 64 : 32; }
 int gemm_k_tile() { return gemm_bk(g_gemm_prec); }
 
-static int gemm_xcd_group() {
-  static const int g = env_int("A2M_GEMM_XCD", 8);
-  return g < 0 ? 0 : g;
-}
+// XCD-aware block order: groups of 8 M-tiles share an XCD's L2 (40 MB a launch instead of ~64 MB
+// at a 0.5 % step cost; identity order and groups of 2 / 4 measured within noise)
+static int gemm_xcd_group() { return 8; }
 
 static int g_override_tile = 0, g_override_split = 0;   // a2m_gemm_plan_override (tuning)
-static int g_pipe_override = -1;   // a2m_gemm_pipe_override: -1 A2M_GEMM_PIPE, 0 gemm_tile, 1 pipelined
+static int g_pipe_override = -1;   // a2m_gemm_pipe_override: -1 default (pipelined), 0 gemm_tile, 1 pipelined
 
 struct PlanRule {
   int M, N, K, tile, splits;
@@ -366,8 +363,7 @@ static const PlanRule kTunedPlans[] = {
                                  // boxes, seven of ten rounds lower)
 };
 static const PlanRule* tuned_plan(int M, int N, int K, int prec) {
-  static const int on = env_int("A2M_GEMM_TUNED", 1);
-  if (!on || prec != 0) return nullptr;
+  if (prec != 0) return nullptr;
   for (const PlanRule& r : kTunedPlans)
     if (r.M == M && r.N == N && r.K == K) return &r;
   return nullptr;
@@ -375,21 +371,13 @@ static const PlanRule* tuned_plan(int M, int N, int K, int prec) {
 
 // bf16 (prec 1) throughput per CU by resident blocks, flop / us: staging- and latency-bound
 // rather than MFMA-bound (16x the f32 MFMA rate), so it grows with the blocks a CU holds far more
-// than the f32 tile's.  A2M_GEMM_BF16_THR="t1,t2,t3,t4[,t128_1,t128_2]" (kflop / us, experiments)
+// than the f32 tile's (kflop / us per CU by resident blocks: 64x64 at 1..4, 128x128 at 1 / 2)
 static double bf16_thr(int tile, int c) {
-  static const std::vector<double> t = [] {
-    // fitted in the replayed bf16 bench step (r05 sweeps, two interleaved rounds each: 1.658 ms
-    // against 1.831 ms with round 4's 4 x the f32 table, {1360, 1712, 1740, 1760, 1856, 2000}e3,
-    // at {530, 750, 900, 1060, 1500, 2000}e3; refitted with the bf16 pipelined tile, whose 64x64
-    // launches run faster: 1.416-1.422 ms against 1.447-1.449)
-    std::vector<double> v = {600e3, 850e3, 1000e3, 1150e3, 1500e3, 2000e3};
-    if (const char* e = std::getenv("A2M_GEMM_BF16_THR")) {
-      double x[6];
-      const int n = std::sscanf(e, "%lf,%lf,%lf,%lf,%lf,%lf", &x[0], &x[1], &x[2], &x[3], &x[4], &x[5]);
-      for (int i = 0; i < n; ++i) v[i] = x[i] * 1e3;
-    }
-    return v;
-  }();
+  // fitted in the replayed bf16 bench step (r05 sweeps, two interleaved rounds each: 1.658 ms
+  // against 1.831 ms with round 4's 4 x the f32 table, {1360, 1712, 1740, 1760, 1856, 2000}e3,
+  // at {530, 750, 900, 1060, 1500, 2000}e3; refitted with the bf16 pipelined tile, whose 64x64
+  // launches run faster: 1.416-1.422 ms against 1.447-1.449)
+  static constexpr double t[6] = {600e3, 850e3, 1000e3, 1150e3, 1500e3, 2000e3};
   return tile == 128 ? t[4 + (c > 1)] : t[std::min(std::max(c, 1), 4) - 1];
 }
 
@@ -409,26 +397,21 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   double thr = prec == 2 ? (tile == 128 ? x6_thr128[c - 1] : x6_thr64[c - 1])
                          : (tile == 128 ? thr128[c - 1] : thr64[c - 1]);
   if (gathered && tile == 64) thr *= 0.84;
-  // channels-last conv rows (mode 6) at the 64x64 tile, percent of the dense fit
-  // (A2M_GEMM_MODE6_THR).  With the two-group tile (KS = 2) these launches ran ~13 % below the
-  // fit (512x4096x2304: 64/1 109 us vs the fit's 95, tools/enc_plan_sweep.py) and 87 moved them
-  // to the 128x128 tile; on the one-group tile, the default for mode 6 since, the fit's own
-  // choices are the fastest measured (encoder 300.0 us; 87: 303.2 us; tools/enc_plan_ab.py)
-  static const double rows6 = env_int("A2M_GEMM_MODE6_THR", 100) / 100.0;
-  if (conv_rows && tile == 64 && prec == 0) thr *= rows6;
+  // (channels-last conv rows, mode 6, run at the dense fit on the one-group 64x64 tile: a 0.87
+  // factor measured slower, encoder 303.2 vs 300.0 us, tools/enc_plan_ab.py, round 3)
   if (prec == 1) thr = bf16_thr(tile, c) * (gathered && tile == 64 ? 0.84 : 1.0);
   const double block_flops = 2.0 * tile * tile * (double)kchunk;
   const double fixed = prec == 2 ? (tile == 128 ? 15.0 : 2.0)
                                  : (tile == 128 ? (gathered ? 16.0 : 10.0) : 3.0);
   double t = per_cu * block_flops / thr + cdiv(per_cu, occ) * fixed + 4.0;
-  // A2M_GEMM_SPLIT_COST (percent, experiments): scales the reduce term
-  static const double red_scale = env_int("A2M_GEMM_SPLIT_COST", 100) / 100.0;
+  // (the reduce term scaled by 0.6 / 1.5 / 2 measured slower in-step, round 2: it is right as fitted)
+  constexpr double red_scale = 1.0;
   // channels-last conv rows (the encoder): the reduce priced at A2M_GEMM_SPLIT_COST_ROWS
   // (default 200 %), so its launches take fewer splits (conv2: 3 instead of 4).  With every
   // launch's reduce at 200 % the encoder measured 0.2906-0.2937 vs 0.2951-0.2971 ms but the step
   // neutral to slightly slower (three rounds); on the encoder's launches only: in-step
   // path_frac 0.480-0.484 vs 0.473-0.476, step 2.718-2.727 vs 2.721-2.737 ms (four rounds, r04s)
-  static const double red_scale_rows = env_int("A2M_GEMM_SPLIT_COST_ROWS", 200) / 100.0;
+  constexpr double red_scale_rows = 2.0;
   if (splits > 1)
     t += (conv_rows ? red_scale_rows : red_scale) * ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0);
   return t;
@@ -436,10 +419,8 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
 
 static Plan plan_for(int M, int N, int K, int batch, bool gathered, int prec, int kquant = 1,
                      bool conv_rows = false, bool pipe64 = false) {
-  static const int env_tile = env_int("A2M_GEMM_TILE", 0);
-  static const int env_split = env_int("A2M_GEMM_SPLIT", 0);
-  const int force_tile = g_override_tile ? g_override_tile : env_tile;
-  const int force_split = g_override_split ? g_override_split : env_split;
+  const int force_tile = g_override_tile;     // a2m_gemm_plan_override (tuning sweeps)
+  const int force_split = g_override_split;
   const int BK = gemm_bk(prec);
   const int KQ = BK * kquant;   // split boundaries on whole k-tile groups (mode 5: all taps of a chunk)
   static const int cand_splits[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256};
@@ -599,12 +580,10 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   const int kquant = mb == 5 ? B.tapconv : 1;
   // gathered: row-vector staging (modes 2 / 3) or gathers; k-contiguous conv rows (mode 6) load
   // like dense rows
-  static const int ks2 = env_int("A2M_GEMM_KS2", 1);
-  // software-pipelined one-wave-per-SIMD tile (gemm_pipe.h; A2M_GEMM_PIPE=0 restores gemm_tile):
-  // fp32 64x64, dense weights x dense rows / channels-last rows / halo tap conv, every element
-  // offset below 2^29 floats (raw buffer loads)
-  static const int pipe_env = env_int("A2M_GEMM_PIPE", 1);
-  const int pipe_on = g_pipe_override >= 0 ? g_pipe_override : pipe_env;
+  // software-pipelined one-wave-per-SIMD tile (gemm_pipe.h; a2m_gemm_pipe_override(0) restores
+  // gemm_tile): fp32 64x64, dense weights x dense rows / channels-last rows / halo tap conv, every
+  // element offset below 2^29 floats (raw buffer loads)
+  const int pipe_on = g_pipe_override >= 0 ? g_pipe_override : 1;
   auto below = [](int64_t v) { return v >= 0 && v < ((int64_t)1 << 29); };
   bool pipe_ext = below((int64_t)(M - 1) * A.sr0 + K);
   if (mb == 0) pipe_ext = pipe_ext && below((int64_t)(N - 1) * B.sr0 + K);
@@ -623,35 +602,29 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     return g.K1 == 1 && g.K2 % 4 == 0 && g.bk2 == 1 && g.sw == 1 && g.divh == 1 && g.divw == 1 &&
            g.sr0 >= 0 && g.sk0 >= 0 && below(rmax);
   };
-  static const int pipe4_env = env_int("A2M_GEMM_PIPE4", 1);
   // ... and B as stride-2 runs (a stride-2 conv's input: gemm_tile gathers it, mode 1)
   const bool runs_s2 = mb == 1 && B.K1 == 1 && B.K2 % 4 == 0 && B.bk2 == 2 && B.sw == 1 && B.divh == 1 &&
                        B.divw == 1 && B.sr0 >= 0 && B.sk0 >= 0 &&
                        below((int64_t)((N - 1) / (B.R1 * B.R2)) * B.sr0 + (int64_t)std::max(0, B.Lh - 1) * std::abs(B.sh) +
                              B.Lw + (int64_t)(K / B.K2) * B.sk0);
-  const bool m4_ok = pipe4_env && ma == 4 && runs4(A, M) && ((mb == 4 && runs4(B, N)) || runs_s2);
+  const bool m4_ok = ma == 4 && runs4(A, M) && ((mb == 4 && runs4(B, N)) || runs_s2);
   // A as a plain [K][M] operand (mode 3: rows at unit stride, loaded 4 at a time) with B dense or
   // plain mode 3 (the weight gradients of the linears / graph layers)
-  static const int pipe_a3_env = env_int("A2M_GEMM_PIPE_A3", 1);
   const bool plainA3 = ma == 3 && A.K1 == 1 && A.K2 == 1 && A.R1 == 1 && A.R2 == 1 && A.sr0 == 1 && A.ch == 0 &&
                        A.cw == 0 && A.divh == 1 && A.divw == 1 && M % 4 == 0 && A.sk0 >= 0 &&
                        below((int64_t)(M - 1) + (int64_t)K * A.sk0);
-  const bool pipe_a3 = pipe_a3_env && plainA3 &&
+  const bool pipe_a3 = plainA3 &&
                        ((mb == 0 && below((int64_t)(N - 1) * B.sr0 + K)) ||
                         (rows3 && below((int64_t)((N - 1) / B.R2) * B.sr0 + B.R2 + (int64_t)K * B.sk0)));
   // the operand modes the fp32 pipelined tile takes (at a 64-row tile)
   const bool tap5 = mb == 5 && B.tapconv >= 1 && B.tapconv <= 3 && B.R2 % 4 == 0 && 64 % B.R2 == 0;
   const bool pipe_modes = (ma == 0 && (mb == 0 || mb == 6 || rows3 || tap5) && pipe_ext) || m4_ok || pipe_a3;
-  // A2M_GEMM_PIPE64: 0 off, 1 fp32 launches only, 2 (default) also bf16's training modes (mode-4 /
-  // plain mode-3 A: bf16 B=32 training kernel time 43.0 -> 41.7 ms a step, r05_p)
-  static const int pipe64_env = env_int("A2M_GEMM_PIPE64", 2);
+  // launches the pipelined tile takes are planned on 64x64 tiles: fp32 every such launch, bf16 its
+  // training modes (mode-4 / plain mode-3 A: bf16 B=32 training kernel time 43.0 -> 41.7 ms a step,
+  // r05_p; the bf16 planner table was refitted on the inference launches with its pipelined tile)
   const Plan p = launch_plan(M, N, K, batch, ma == 2 || ma == 3 || mb == 2 || (mb >= 3 && mb != 6), prec,
                              kquant, mb == 6, force_split,
-                             pipe64_env && pipe_on &&
-                                 ((prec == 0 && pipe_modes) ||
-                                  // bf16: the training modes only (its planner table was refitted on the
-                                  // inference launches with the bf16 pipelined tile in place)
-                                  (prec == 1 && pipe64_env >= 2 && (m4_ok || pipe_a3))));
+                             pipe_on && ((prec == 0 && pipe_modes) || (prec == 1 && (m4_ok || pipe_a3))));
   // A2M_GEMM_HALO=0: mode 5 re-stores the window shifted for every tap (the round-3 loader)
   static const int halo_on = env_int("A2M_GEMM_HALO", 1);
   a.B.halo = halo_on && mb == 5 && prec == 0 && p.bm == 64 && B.tapconv == 3 &&
@@ -660,17 +633,15 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   a.kchunk = p.kchunk;
   a.partial = nullptr;
   a.xcd_group = gemm_xcd_group();
-  static const int stage_m = env_int("A2M_GEMM_MCONTIG", 1);
   // fused resample (E.interp_T): the tile always writes raw slabs (also at one split) and the
   // reduce kernel runs epilogue + resample
   const bool interp = E.interp_T > 0;
   A2M_CHECK_ARG(!interp || (batch == 1 && E.interp_H > 0 && N % E.interp_H == 0 &&
                             (size_t)E.interp_H * sizeof(float) <= 32768),
                 "gemm: fused resample needs batch 1, N a multiple of H = %d <= 8192", E.interp_H);
-  a.mcontig = stage_m && E.som == 1 && M > 1 && !interp;
+  a.mcontig = E.som == 1 && M > 1 && !interp;
   // float4 output rows (pipelined tile): n contiguous within 4-aligned groups of one n2 run, every
   // other stride and base 16-byte aligned; split-K slabs ([M][N]) whenever N % 4 == 0
-  static const int vec4_on = env_int("A2M_GEMM_VEC4", 1);
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   const bool slab_out = p.splits > 1 || interp;
   // the innermost index that varies with n: n2 (N2 > 1), else n1 (N1 > 1), else n0
@@ -679,7 +650,7 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
   const int in_len = in_lvl == 2 ? E.N2 : (in_lvl == 1 ? E.N1 : 4);
   const bool outer4 = (in_lvl == 0 || E.so0 % 4 == 0) && (in_lvl != 2 || E.N1 == 1 || E.so1 % 4 == 0) &&
                       E.som % 4 == 0 && E.bstride % 4 == 0;
-  a.vec4 = vec4_on && !a.mcontig && N % 4 == 0 &&
+  a.vec4 = !a.mcontig && N % 4 == 0 &&
            (slab_out || (in_stride == 1 && in_len % 4 == 0 && outer4 && al16(E.out) &&
                          (!E.res1 || al16(E.res1)) && (!E.res2 || al16(E.res2))));
   const bool pipe_m4 = m4_ok && p.kchunk % 32 == 0;
@@ -740,9 +711,9 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     else if (p.bm == 128) launch_tile<128, 128, 32, 0>(a, ma, mb, batch, stream);
     // two wave groups per 64x64 tile pay off for dense operands (measured -9 % on the decoder
     // convs after im2col); with gathered operands (modes 1-4) they measured slower end to end
-    // (A2M_GEMM_KS2=2 also for channels-last conv rows, mode 6: the encoder measured 305.8 us
-    // with it against 303.2 without, tools/enc_plan_ab.py, four interleaved rounds)
-    else if (ks2 && ma == 0 && (mb == 0 || (ks2 == 2 && mb == 6))) launch_tile<64, 64, 32, 0, 2>(a, ma, mb, batch, stream);
+    // (also for channels-last conv rows, mode 6, the encoder measured 305.8 us against 303.2
+    // without, tools/enc_plan_ab.py, four interleaved rounds)
+    else if (ma == 0 && mb == 0) launch_tile<64, 64, 32, 0, 2>(a, ma, mb, batch, stream);
     else launch_tile<64, 64, 32, 0>(a, ma, mb, batch, stream);
   }
   A2M_LAUNCH_CHECK();
@@ -750,16 +721,14 @@ int gemm(const Gather& A, const Gather& B, const Epilogue& E, int M, int N, int 
     const int H = E.interp_H, nb = N / H;
     // whole (m, b) rows per block: ~2,048 outputs, the rows' H values staged in LDS
     const int RB = std::max(1, std::min(2048 / std::max(E.interp_T, 1), 8192 / H));
-    static const int wide_on = env_int("A2M_GEMM_WIDE_REDUCE", 1);
-    const int wide = wide_on && (N & 3) == 0 && p.splits >= 2 * RW_LANES && (int64_t)M * N / 4 <= 65536;
+    const int wide = (N & 3) == 0 && p.splits >= 2 * RW_LANES && (int64_t)M * N / 4 <= 65536;
     hipLaunchKernelGGL(splitk_reduce_interp_kernel, dim3((unsigned)cdiv((int64_t)M * nb, RB)), dim3(256),
                        (size_t)RB * H * sizeof(float), stream, a, nb, RB, wide);
     A2M_LAUNCH_CHECK();
   } else if (p.splits > 1) {
     const int inner = a.mcontig ? M : N;
     const int64_t total = (int64_t)M * N * batch / ((inner & 3) == 0 ? 4 : 1);
-    static const int wide_on = env_int("A2M_GEMM_WIDE_REDUCE", 1);
-    if (wide_on && (inner & 3) == 0 && p.splits >= 2 * RW_LANES && total <= 65536) {
+    if ((inner & 3) == 0 && p.splits >= 2 * RW_LANES && total <= 65536) {
       hipLaunchKernelGGL(splitk_reduce_wide_kernel, dim3((unsigned)cdiv(total, RW_COLS)),
                          dim3(RW_LANES * RW_COLS), 0, stream, a, batch);
     } else {

@@ -842,9 +842,8 @@ extern "C" int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, con
   GraphStack S{};
   S.nlayers = nlayers;
   S.slope = slope;
-  // bf16 operand mode: the layer products on the bf16 MFMA (A2M_STACK_BF16=0: the fp32 stack)
-  static const int stack_bf16 = std::getenv("A2M_STACK_BF16") ? std::atoi(std::getenv("A2M_STACK_BF16")) : 1;
-  S.bf16 = stack_bf16 && a2m_get_gemm_precision() == 1;
+  // bf16 operand mode: the layer products on the bf16 MFMA
+  S.bf16 = a2m_get_gemm_precision() == 1;
   for (int L = 0; L < nlayers; ++L) {
     A2M_CHECK_ARG(kinds[L] == 0 || kinds[L] == 1, "graph_stack: layer %d kind %d", L, kinds[L]);
     const bool has_w = w0[L] && (kinds[L] == 0 || w1[L]);

@@ -645,10 +645,9 @@ int a2m_logmel_f32(const float* wave, int64_t n_clips, int64_t clip_stride, int6
   A2M_CHECK_ARG(fft_len <= 4096, "logmel: fft_len %d > 4096", fft_len);
   const size_t lds = sizeof(float) * (2 * (size_t)fft_len + fft_len / 2 + 1 + 3);
   A2M_CHECK_ARG(lds <= 160 * 1024, "logmel: fft_len %d too large for LDS", fft_len);
-  static const bool generic_only = std::getenv("A2M_LOGMEL_GENERIC") != nullptr;
   // register-FFT path (its mel rows sit in LDS when each lane's fit in LM_ROWS float4s, as
   // for the build configuration, and are read from L2 otherwise)
-  if (fft_len == 2048 && n_mels <= 128 && !generic_only) {
+  if (fft_len == 2048 && n_mels <= 128) {
     auto kern = window == 2048 ? logmel2048_kernel<true> : logmel2048_kernel<false>;
     const int64_t total = n_clips * nf;
     hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(total, LM_WAVES)), dim3(64 * LM_WAVES), 0,

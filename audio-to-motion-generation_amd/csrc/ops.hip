@@ -488,11 +488,8 @@ int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t,
                 "conv1d: tensor too large for 32-bit offsets");
   Gather A = dense_rk(w, Ci * ks);
   Gather Bg{};
-  static const int im2col_on = std::getenv("A2M_CONV_IM2COL") ? std::atoi(std::getenv("A2M_CONV_IM2COL")) : 1;
   const int64_t K = (int64_t)Ci * ks, N = (int64_t)B * Tout;
-  static const int im2col_min_co = std::getenv("A2M_CONV_IM2COL_MINCO") ? std::atoi(std::getenv("A2M_CONV_IM2COL_MINCO")) : 128;
-  static const int im2col_1x1 = std::getenv("A2M_CONV_IM2COL_1X1") ? std::atoi(std::getenv("A2M_CONV_IM2COL_1X1")) : 0;
-  if (im2col_on && (ks > 1 || im2col_1x1) && ks <= 8 && stride <= 2 && Co >= im2col_min_co && xs_t == 1 && K % 4 == 0 &&
+  if (ks > 1 && ks <= 8 && stride <= 2 && Co >= 128 && xs_t == 1 && K % 4 == 0 &&
       N * K < (1LL << 31)) {
     // explicit im2col into the workspace head, then a dense x dense GEMM
     const size_t col_bytes = ((size_t)(N * K) * sizeof(float) + 255) & ~size_t(255);
@@ -503,17 +500,11 @@ int a2m_conv1d_fwd_f32(const float* x, int64_t xs_b, int64_t xs_c, int64_t xs_t,
     }
     float* col = static_cast<float*>(ws);
     hipStream_t st = as_stream(stream);
-    static const int cc_env = std::getenv("A2M_I2C_C") ? std::atoi(std::getenv("A2M_I2C_C")) : 16;
-    static const int xcd_env = std::getenv("A2M_I2C_XCD") ? std::atoi(std::getenv("A2M_I2C_XCD")) : 1;
-    const int cc = cc_env == 32 ? 32 : 16;   // 16 and 32 measured alike (tools/ab_i2c.sh)
-    const int n_rows = B * (int)cdiv(Tout, I2C_T), n_ct = (int)cdiv(Ci, cc);
-    const unsigned blocks = xcd_env ? (unsigned)(8 * n_ct * cdiv(n_rows, 8)) : (unsigned)(n_rows * n_ct);
-    if (cc == 16)
-      hipLaunchKernelGGL(im2col1d_kernel<16>, dim3(blocks), dim3(256), 0, st, x, xs_b, xs_c, Ci, Tin,
-                         Tout, ks, stride, pad, n_rows, n_ct, xcd_env, col);
-    else
-      hipLaunchKernelGGL(im2col1d_kernel<32>, dim3(blocks), dim3(256), 0, st, x, xs_b, xs_c, Ci, Tin,
-                         Tout, ks, stride, pad, n_rows, n_ct, xcd_env, col);
+    // 16 channels a block, blocks grouped per XCD (32 channels measured alike, tools/ab_i2c.sh)
+    const int n_rows = B * (int)cdiv(Tout, I2C_T), n_ct = (int)cdiv(Ci, 16);
+    const unsigned blocks = (unsigned)(8 * n_ct * cdiv(n_rows, 8));
+    hipLaunchKernelGGL(im2col1d_kernel<16>, dim3(blocks), dim3(256), 0, st, x, xs_b, xs_c, Ci, Tin,
+                       Tout, ks, stride, pad, n_rows, n_ct, 1, col);
     A2M_LAUNCH_CHECK();
     Bg = dense_rk(col, (int)K);
     Epilogue E = epi_bn(y, bias, bn_w, bn_b, bn_rm, bn_rv, bn_eps, act, slope);
@@ -847,13 +838,12 @@ int a2m_conv2d_fwd_f32(const float* x, int32_t B, int32_t Ci, int32_t H, int32_t
                 "conv2d: too large");
   const int Wn = w_hi - w_lo;
   Gather A = dense_rk(w, Ci * kh * kw);
-  static const int im2col2d_on = std::getenv("A2M_CONV2D_IM2COL") ? std::atoi(std::getenv("A2M_CONV2D_IM2COL")) : 1;
   const int64_t K = (int64_t)Ci * kh * kw, N = (int64_t)B * Hout * Wn;
   // explicit im2col into the workspace head, then a dense x dense GEMM, where the GEMM's gain
   // over the gathered (mode-2) operand outweighs writing the [N][K] matrix: measured on the
   // encoder, K >= 2048 (conv2 / conv3 / conv4: 26 / 22 / 18 us of im2col for 32 / 29 / 32 us
   // of GEMM time saved); conv1 (K = 1024, 92 MB of columns at B = 64) loses.
-  if (im2col2d_on && Co >= 128 && K >= 2048 && K % 4 == 0 && N * K < (1LL << 31)) {
+  if (Co >= 128 && K >= 2048 && K % 4 == 0 && N * K < (1LL << 31)) {
     const size_t col_bytes = ((size_t)(N * K) * sizeof(float) + 255) & ~size_t(255);
     const size_t need = col_bytes + gemm_ws_bytes(Co, (int)N, (int)K, 1);
     if (!ws || ws_bytes < need) {
@@ -1293,8 +1283,7 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
   const int64_t qs_b = (int64_t)Cqkv * T;
   // q, k, v as ONE 1x1 convolution with the stacked weights: qkv[b][0:Cq | Cq:2Cq | 2Cq:][t]
   int rc;
-  static const int btc_ok = std::getenv("A2M_ATTN_BTC") ? std::atoi(std::getenv("A2M_ATTN_BTC")) : 1;
-  if (btc_ok && C >= 1024 && T <= TR_MAXT) {
+  if (C >= 1024 && T <= TR_MAXT) {
     // wide channels (the UNet's SelfAttention(2048)): x is first copied to [B*T][C] so the
     // projection GEMM reads both operands as dense k-contiguous rows instead of gathering x's
     // t-runs (mode 3): 255 -> ~220 us for the up_attention projection at T = 32, for a copy of
@@ -1320,10 +1309,9 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
                             ws_bytes, stream);
   }
   if (rc) return rc;
-  static const int fused_ok = std::getenv("A2M_ATTN_FUSED") ? std::atoi(std::getenv("A2M_ATTN_FUSED")) : 1;
-  if (fused_ok && attn_core_fits(C, T))
+  if (attn_core_fits(C, T))
     return attn_core(qkv, qs_b, B, C, T, gamma, x, x_bs, res, y, attn, st);
-  if (fused_ok && attn_core_wide_fits(C, T))   // the UNet's / D's SelfAttention(2048), T <= 32
+  if (attn_core_wide_fits(C, T))   // the UNet's / D's SelfAttention(2048), T <= 32
     return attn_core_wide(qkv, qs_b, B, C, T, gamma, x, x_bs, res, y, attn, st);
   // scores[b][i][j] = sum_c q[b][c][i] k[b][c][j]
   Gather Aq = dense_kr(qkv, T, qs_b);

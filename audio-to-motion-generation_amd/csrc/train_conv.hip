@@ -90,9 +90,8 @@ int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
   float* packed = static_cast<float*>(ws);
   // 1-D, stride 1, 3 taps, pad 1, clips that tile the 64-row block: the tap conv (A2M_DGRAD_TAP=0:
   // the phase GEMM below for every conv)
-  static const int tap_on = std::getenv("A2M_DGRAD_TAP") ? std::atoi(std::getenv("A2M_DGRAD_TAP")) : 1;
   const int chunk = gemm_k_tile();
-  if (tap_on && H == 1 && kh == 1 && pad_h == 0 && stride_h == 1 && stride_w == 1 && kw == 3 && pad_w == 1 &&
+  if (H == 1 && kh == 1 && pad_h == 0 && stride_h == 1 && stride_w == 1 && kw == 3 && pad_w == 1 &&
       Wo == W && W % 4 == 0 && 64 % W == 0 && Co % chunk == 0 &&
       (reinterpret_cast<uintptr_t>(dy) % 16) == 0 && ((int64_t)Co * W) % 4 == 0) {
     hipLaunchKernelGGL(dgrad_tap_pack_kernel, dim3((unsigned)std::min<int64_t>(cdiv((int64_t)Co * kw, 256), 64), (unsigned)Ci),
@@ -116,7 +115,7 @@ int a2m_conv2d_dgrad_f32(const float* dy, int32_t B, int32_t Co, int32_t Ho, int
   // 1-D, stride s > 1 with s * Wo == W: dX is the ConvTranspose1d of dY with W read as its
   // [in = Co][out = Ci][k] weight -- per output phase a tap conv of dY (the eval ConvTranspose's
   // tap-chunked pack and phases), clips of Wo rows that tile the 64-row block
-  if (tap_on && H == 1 && kh == 1 && pad_h == 0 && stride_h == 1 && stride_w > 1 && stride_w * Wo == W &&
+  if (H == 1 && kh == 1 && pad_h == 0 && stride_h == 1 && stride_w > 1 && stride_w * Wo == W &&
       Wo % 4 == 0 && 64 % Wo == 0 && Co % chunk == 0 && (reinterpret_cast<uintptr_t>(dy) % 16) == 0) {
     bool shifts_ok = true;
     for (int r = 0; r < stride_w; ++r) {

@@ -16,12 +16,6 @@ namespace a2m {
 // activation is 1,024 workgroups instead of 256 at one latency-bound round trip per element)
 constexpr int kSlice = 1024;
 
-// A2M_BN_CHAN=0: every BatchNorm on the sliced kernels (the round-5 path; A/B and tests)
-static bool chan_path_off() {
-  static const bool off = std::getenv("A2M_BN_CHAN") && std::atoi(std::getenv("A2M_BN_CHAN")) == 0;
-  return off;
-}
-
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
   uint64_t z = seed + idx * 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -475,7 +469,7 @@ static bool bn_chan_fwd(const BNArgs& a, float eps, float momentum, float* rmean
                         float* rstd_out, const float* gamma, const float* beta, int act, float slope, float* y,
                         int64_t ys_b, int64_t ys_c, hipStream_t st) {
   const int64_t N = (int64_t)a.B * a.L;
-  if (N > kChanMax || chan_path_off()) return false;
+  if (N > kChanMax) return false;
 #define A2M_CHAN_FWD(T, E) hipLaunchKernelGGL((bn_train_chan_kernel<T, E>), dim3(a.C), dim3(T), 0, st, a, eps, \
                                               momentum, rmean, rvar, mean_out, rstd_out, gamma, beta, act, slope, y, \
                                               ys_b, ys_c)
@@ -494,7 +488,7 @@ static bool bn_chan_fwd(const BNArgs& a, float eps, float momentum, float* rmean
 
 static bool bn_chan_bwd(const BNBwdArgs& a, float* dgamma, float* dbeta, float* dx, float* dbias, hipStream_t st) {
   const int64_t N = (int64_t)a.f.B * a.f.L;
-  if (N > kChanMax || chan_path_off()) return false;
+  if (N > kChanMax) return false;
 #define A2M_CHAN_BWD(T, E) hipLaunchKernelGGL((bn_bwd_chan_kernel<T, E>), dim3(a.f.C), dim3(T), 0, st, a, dgamma, \
                                               dbeta, dx, dbias)
   if (N <= 256) A2M_CHAN_BWD(256, 1);

@@ -548,7 +548,7 @@ int a2m_gemm_timing_begin(void);
  * (0 = the planner's choice); workspace sizing follows.  Process-global, not for production. */
 int a2m_gemm_plan_override(int32_t tile, int32_t splits);
 /* Test / tuning hook: which 64x64 tile kernel eligible launches take -- 1 the software-pipelined
- * tile (gemm_pipe.h / gemm_pipe_bf16.h), 0 gemm_tile, -1 the A2M_GEMM_PIPE environment default
+ * tile (gemm_pipe.h / gemm_pipe_bf16.h), 0 gemm_tile, -1 the default
  * (1).  Both give bitwise-equal results; process-global, not for production. */
 int a2m_gemm_pipe_override(int32_t mode);
 /* Operand precision of every GEMM-engine launch (convs, linears, attention products and their

@@ -14,7 +14,8 @@ run c2_fp32 --no-cpu-baseline
 run c2_bf16 --no-cpu-baseline --dtype bf16
 run c5_bf16_b32 --no-cpu-baseline --dtype bf16 --batch 32
 run c4_t480_b8 --no-cpu-baseline --frames 480 --batch 8
-run c3_train_fp32 --mode train --steps 20 --warmup 3
-run c5_train_bf16_b32 --mode train --steps 20 --warmup 3 --batch 32 --dtype bf16
-run c3_train_bf16 --mode train --steps 20 --warmup 3 --dtype bf16
+run c3_train_fp32 --mode train --steps 20 --warmup 5
+run c3_train_fp32_b8 --mode train --steps 20 --warmup 5 --batch 8
+run c5_train_bf16_b32 --mode train --steps 20 --warmup 5 --batch 32 --dtype bf16
+run c3_train_bf16 --mode train --steps 20 --warmup 5 --dtype bf16
 exit 0
