@@ -265,13 +265,12 @@ def test_channel_attention_train(B, C, T):
 @pytest.mark.parametrize('kind,J,lo,norm_res,Fr', [(0, 10, 0, True, 7), (0, 42, 10, True, 7), (1, 42, 10, True, 7),
                                                    (1, 10, 0, True, 7), (0, 42, 10, False, 7),
                                                    (0, 42, 10, True, 29), (1, 10, 0, True, 29)])
-def test_graph_layer_train(kind, J, lo, norm_res, Fr, save_pre, monkeypatch):
+def test_graph_layer_train(kind, J, lo, norm_res, Fr, save_pre):
     """Both backward paths: the forward's saved pre-LayerNorm output (the weight gradients as
     Z (x) x, Z the aggregation adjoint of dout) and the in-kernel recompute (dout (x) Y)."""
     from a2m import autograd as AG
     from a2m import skeleton as S
     from oracle import model as OM
-    monkeypatch.setattr(AG, '_GRAPH_SAVE_PRE', save_pre)
     ei = S.edge_index(lo, J)
     ptr, idx = [t.to(DEV) for t in S.in_neighbour_csr(ei, J)]
     edges = OM.expand_edges(ei, J, Fr)
@@ -287,7 +286,8 @@ def test_graph_layer_train(kind, J, lo, norm_res, Fr, save_pre, monkeypatch):
     dev_p = [p.clone().to(DEV).requires_grad_(True) if p is not None else None for p in allp]
     cpu_p = [p.clone().requires_grad_(True) if p is not None else None for p in allp]
     xd, xc = _leaf(x)
-    yd = AG._GraphLayer.apply(xd, *dev_p, (J, kind, ptr, idx, norm_res, True))
+    # the topology's last entry: keep the pre-LayerNorm copy for the backward (False: recompute)
+    yd = AG._GraphLayer.apply(xd, *dev_p, (J, kind, ptr, idx, norm_res, save_pre))
     w0, w1, a_s, a_d, b, lw, lb = cpu_p
     if kind == 0:
         g = OM._gat_fn(xc, edges, w0, a_s, a_d, b, 4)
