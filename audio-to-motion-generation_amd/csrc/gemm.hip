@@ -288,6 +288,11 @@ struct Plan {
   int bm, bk, splits, kchunk;
 };
 
+// fixed cost of a split-K reduce launch in the planner's model (us)
+#ifndef A2M_RED_FIXED_US
+#define A2M_RED_FIXED_US 3.0
+#endif
+
 // Tile / split-K choice by a cost model fitted to measured sweeps of the engine on MI355X
 // (tools/gemm_tune.py; DESIGN.md "GEMM planner").  For each candidate (tile, splits):
 //   blocks = tiles * splits, per_cu = ceil(blocks / 256) (the busiest CU), c = min(per_cu,
@@ -413,7 +418,8 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   // path_frac 0.480-0.484 vs 0.473-0.476, step 2.718-2.727 vs 2.721-2.737 ms (four rounds, r04s)
   constexpr double red_scale_rows = 2.0;
   if (splits > 1)
-    t += (conv_rows ? red_scale_rows : red_scale) * ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + 3.0);
+    t += (conv_rows ? red_scale_rows : red_scale) *
+         ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + A2M_RED_FIXED_US);
   return t;
 }
 

@@ -53,21 +53,23 @@ __global__ __launch_bounds__(256) void pose_loss_partial_kernel(const float* gen
   __shared__ float red[4];
   const int b = blockIdx.x;
   float* pb = part + (int64_t)b * kPart;
-  // bone lengths averaged over time (one thread per bone and pose); without a real pose the
-  // bone loss is 0 and the generated lengths are not needed (the eval / inference path)
-  for (int i = threadIdx.x; real != nullptr && i < 2 * kBones; i += blockDim.x) {
+  // bone lengths averaged over time, one wave per (bone, pose) series with its lanes along t and
+  // a wave sum (one thread walking all T frames per series was latency-bound); without a real
+  // pose the bone loss is 0 and the generated lengths are not needed (the eval / inference path)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = wave; real != nullptr && i < 2 * kBones; i += (int)(blockDim.x >> 6)) {
     const bool is_real = i >= kBones;
     const int jb = (i % kBones) + 1, pj = kParents[jb];
     const float* base = is_real ? real + b * rs_b : gen + b * gs_b;
     const int64_t st = is_real ? rs_t : gs_t;
     float s = 0.f;
-#pragma unroll 8
-    for (int t = 0; t < T; ++t) {
+    for (int t = lane; t < T; t += 64) {
       const float* p = base + t * st;
       const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
       s += sqrtf(dx * dx + dy * dy);
     }
-    pb[i] = s / (float)T;
+    s = wave64_sum(s);
+    if (lane == 0) pb[i] = s / (float)T;
   }
   float hs = 0.f, bs = 0.f;
   for (int i = threadIdx.x; i < T * 35; i += blockDim.x) {

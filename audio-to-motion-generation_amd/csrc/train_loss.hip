@@ -24,7 +24,7 @@ __constant__ int kHT[30][3] = {
 __constant__ int kBT[5][3] = {{0, 1, 2}, {1, 2, 3}, {0, 4, 5}, {4, 5, 6}, {0, 7, 8}};
 
 constexpr float kPi = 3.14159265358979f;
-constexpr int kTC = 32;  // time steps per LDS chunk in the pose-loss backward
+constexpr int kTC = 16;  // time steps per workgroup in the pose-loss backward
 
 __device__ __forceinline__ double bsum(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -52,12 +52,15 @@ __device__ __forceinline__ float4 angle_grad(const float* p, int a, int j, int c
   return make_float4(gcr * vy + gdt * vx, -gcr * vx + gdt * vy, -gcr * uy + gdt * ux, gcr * ux + gdt * uy);
 }
 
-// One workgroup per clip, kTC time steps per pass.  Phase 1: every bone's and every angle
-// triple's adjoint, each written by one thread into its own LDS slot; phase 2: one thread per
-// (time step, joint) adds the slots that touch its joint in a fixed order (its own bone, its
-// children's bones ascending, the hand triples ascending, the body triples ascending).  No
-// atomics: the gradient is bitwise reproducible (the LDS float atomics used before summed in
-// thread-timing order and moved the G-step's gradients by ~1 ulp run to run).
+// One workgroup per (clip, kTC time steps): the clip's mean bone lengths (over all T, as in the
+// forward) are recomputed by each of its workgroups, then phase 1 writes every bone's and every
+// angle triple's adjoint into its own LDS slot, and phase 2 has one thread per (time step, joint)
+// add the slots that touch its joint in a fixed order -- its own bone, its children's bones
+// ascending, then the triples ascending (middle, first, last joint roles) -- from a per-joint
+// adjacency list the workgroup builds once.  No atomics: the gradient is bitwise reproducible.
+// (Round 6: one workgroup per clip scanning all 86 bones / triples per output element took
+// ~150 us a call at B = 8 / 32, latency-bound on a handful of CUs.)
+constexpr int kAdjMax = 16;   // entries per joint (the hand roots: 5 child bones + 6 triples)
 __global__ __launch_bounds__(256) void pose_loss_bwd_kernel(const float* gen, int64_t gs_b,
                                                             int64_t gs_t, const float* real,
                                                             int64_t rs_b, int64_t rs_t, int B, int T,
@@ -66,78 +69,95 @@ __global__ __launch_bounds__(256) void pose_loss_bwd_kernel(const float* gen, in
   __shared__ float lg[51], lr[51], coef[51];
   __shared__ float2 bone_g[kTC][51];    // (s dx, s dy) of bone k (joint k+1 from its parent)
   __shared__ float4 tri_g[kTC][35];     // angle adjoints: 30 hand triples, then 5 body triples
-  const int b = blockIdx.x;
+  __shared__ short adj[52][kAdjMax];    // per joint: 0x1000 | k own bone k, 0x2000 | k a child's
+  __shared__ unsigned char nadj[52];    //   bone k, 0x3000 | q << 2 | role  triple q (role 0/1/2)
+  const int b = blockIdx.x, t0 = blockIdx.y * kTC;
+  const int nt = min(kTC, T - t0);
+  if (threadIdx.x < 52) {
+    const int jn = threadIdx.x;
+    int n = 0;
+    if (jn >= 1) adj[jn][n++] = (short)(0x1000 | (jn - 1));
+    for (int c = 1; c < 52; ++c)
+      if (kPar[c] == jn) adj[jn][n++] = (short)(0x2000 | (c - 1));
+    for (int q = 0; q < 35; ++q) {
+      const int* tr = q < 30 ? kHT[q] : kBT[q - 30];
+      const int off = q < 30 ? 10 : 0;   // the hand triples index joints from 10 (p + 20)
+      if (tr[1] + off == jn) adj[jn][n++] = (short)(0x3000 | (q << 2) | 1);
+      if (tr[0] + off == jn) adj[jn][n++] = (short)(0x3000 | (q << 2) | 0);
+      if (tr[2] + off == jn) adj[jn][n++] = (short)(0x3000 | (q << 2) | 2);
+    }
+    nadj[jn] = (unsigned char)n;
+  }
   const float gbone = real ? grad_out[0] : 0.f, gang = grad_out[1];
-  // mean bone lengths over time (as in the forward)
-  for (int i = threadIdx.x; i < 102; i += blockDim.x) {
+  // mean bone lengths over time (as in the forward: one wave per series, lanes along t); only
+  // the bone loss needs them, and it exists only with a real pose
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = wave; real != nullptr && i < 102; i += (int)(blockDim.x >> 6)) {
     const bool isr = i >= 51;
-    if (isr && !real) continue;
     const int jb = (i % 51) + 1, pj = kPar[jb];
     const float* base = isr ? real + b * rs_b : gen + b * gs_b;
     const int64_t st = isr ? rs_t : gs_t;
     float s = 0.f;
-    for (int t = 0; t < T; ++t) {
+    for (int t = lane; t < T; t += 64) {
       const float* p = base + t * st;
       const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
       s += sqrtf(dx * dx + dy * dy);
     }
-    (isr ? lr : lg)[i % 51] = s / (float)T;
+    s = wave64_sum(s);
+    if (lane == 0) (isr ? lr : lg)[i % 51] = s / (float)T;
   }
   __syncthreads();
   for (int k = threadIdx.x; k < 51; k += blockDim.x)
     coef[k] = real ? gbone * 2.f * (lg[k] - lr[k]) / (float)(B * 51) / (float)T : 0.f;
   __syncthreads();
   const float gh = gang * hand_w / (float)(B * T * 30), gb = gang * body_w / (float)(B * T * 5);
-  for (int t0 = 0; t0 < T; t0 += kTC) {
-    const int nt = min(kTC, T - t0);
-    for (int i = threadIdx.x; i < nt * 51; i += blockDim.x) {  // bones
-      const int tt = i / 51, k = i % 51, jb = k + 1, pj = kPar[jb];
-      const float* p = gen + b * gs_b + (t0 + tt) * gs_t;
-      const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
-      const float n = sqrtf(dx * dx + dy * dy);
-      const float s = (n == 0.f || coef[k] == 0.f) ? 0.f : coef[k] / n;
-      bone_g[tt][k] = make_float2(s * dx, s * dy);
+  for (int i = threadIdx.x; i < nt * 51; i += blockDim.x) {  // bones
+    const int tt = i / 51, k = i % 51, jb = k + 1, pj = kPar[jb];
+    const float* p = gen + b * gs_b + (t0 + tt) * gs_t;
+    const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
+    const float n = sqrtf(dx * dx + dy * dy);
+    const float s = (n == 0.f || coef[k] == 0.f) ? 0.f : coef[k] / n;
+    bone_g[tt][k] = make_float2(s * dx, s * dy);
+  }
+  for (int i = threadIdx.x; i < nt * 35; i += blockDim.x) {  // angle triples
+    const int tt = i / 35, q = i % 35;
+    const float* p = gen + b * gs_b + (t0 + tt) * gs_t;
+    if (q < 30) {
+      const int* tr = kHT[q];
+      const float* ph = p + 20;
+      const float ux = ph[2 * tr[1]] - ph[2 * tr[0]], uy = ph[2 * tr[1] + 1] - ph[2 * tr[0] + 1];
+      const float vx = ph[2 * tr[2]] - ph[2 * tr[1]], vy = ph[2 * tr[2] + 1] - ph[2 * tr[1] + 1];
+      const float ang = atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
+      const float g = (ang < 0.f ? -gh : 0.f) + (ang > kPi ? gh : 0.f);
+      tri_g[tt][q] = angle_grad(ph, tr[0], tr[1], tr[2], g);
+    } else {
+      const int* tr = kBT[q - 30];
+      const float ux = p[2 * tr[1]] - p[2 * tr[0]], uy = p[2 * tr[1] + 1] - p[2 * tr[0] + 1];
+      const float vx = p[2 * tr[2]] - p[2 * tr[1]], vy = p[2 * tr[2] + 1] - p[2 * tr[1] + 1];
+      const float ang = atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
+      const float g = (ang < -0.5f * kPi ? -gb : 0.f) + (ang > kPi ? gb : 0.f);
+      tri_g[tt][q] = angle_grad(p, tr[0], tr[1], tr[2], g);
     }
-    for (int i = threadIdx.x; i < nt * 35; i += blockDim.x) {  // angle triples
-      const int tt = i / 35, q = i % 35;
-      const float* p = gen + b * gs_b + (t0 + tt) * gs_t;
-      if (q < 30) {
-        const int* tr = kHT[q];
-        const float* ph = p + 20;
-        const float ux = ph[2 * tr[1]] - ph[2 * tr[0]], uy = ph[2 * tr[1] + 1] - ph[2 * tr[0] + 1];
-        const float vx = ph[2 * tr[2]] - ph[2 * tr[1]], vy = ph[2 * tr[2] + 1] - ph[2 * tr[1] + 1];
-        const float ang = atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
-        const float g = (ang < 0.f ? -gh : 0.f) + (ang > kPi ? gh : 0.f);
-        tri_g[tt][q] = angle_grad(ph, tr[0], tr[1], tr[2], g);
-      } else {
-        const int* tr = kBT[q - 30];
-        const float ux = p[2 * tr[1]] - p[2 * tr[0]], uy = p[2 * tr[1] + 1] - p[2 * tr[0] + 1];
-        const float vx = p[2 * tr[2]] - p[2 * tr[1]], vy = p[2 * tr[2] + 1] - p[2 * tr[1] + 1];
-        const float ang = atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
-        const float g = (ang < -0.5f * kPi ? -gb : 0.f) + (ang > kPi ? gb : 0.f);
-        tri_g[tt][q] = angle_grad(p, tr[0], tr[1], tr[2], g);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nt * 52; i += blockDim.x) {
+    const int tt = i / 52, jn = i % 52;
+    float sx = 0.f, sy = 0.f;
+    for (int e = 0; e < nadj[jn]; ++e) {
+      const int code = adj[jn][e], kind = code >> 12, idx = code & 0xfff;
+      if (kind == 1) { sx += bone_g[tt][idx].x; sy += bone_g[tt][idx].y; }
+      else if (kind == 2) { sx -= bone_g[tt][idx].x; sy -= bone_g[tt][idx].y; }
+      else {
+        const float4 v = tri_g[tt][idx >> 2];
+        const int role = idx & 3;
+        if (role == 1) { sx += v.x - v.z; sy += v.y - v.w; }
+        else if (role == 0) { sx -= v.x; sy -= v.y; }
+        else { sx += v.z; sy += v.w; }
       }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nt * 52; i += blockDim.x) {
-      const int tt = i / 52, j = i % 52;
-      float sx = 0.f, sy = 0.f;
-      if (j >= 1) { sx += bone_g[tt][j - 1].x; sy += bone_g[tt][j - 1].y; }
-      for (int c = 1; c < 52; ++c)
-        if (kPar[c] == j) { sx -= bone_g[tt][c - 1].x; sy -= bone_g[tt][c - 1].y; }
-      for (int q = 0; q < 35; ++q) {
-        const int* tr = q < 30 ? kHT[q] : kBT[q - 30];
-        const int off = q < 30 ? 10 : 0;   // the hand triples index joints from 10 (p + 20)
-        const float4 v = tri_g[tt][q];
-        if (tr[1] + off == j) { sx += v.x - v.z; sy += v.y - v.w; }
-        if (tr[0] + off == j) { sx -= v.x; sy -= v.y; }
-        if (tr[2] + off == j) { sx += v.z; sy += v.w; }
-      }
-      float* d = dgen + ((int64_t)b * T + t0 + tt) * 104 + 2 * j;
-      d[0] += sx;
-      d[1] += sy;
-    }
-    __syncthreads();
+    float* d = dgen + ((int64_t)b * T + t0 + tt) * 104 + 2 * jn;
+    d[0] += sx;
+    d[1] += sy;
   }
 }
 
@@ -158,21 +178,28 @@ __global__ __launch_bounds__(256) void motion_terms_kernel(const float* fake, co
       const int t = i / Fd, f = i % Fd;
       l1 += fabsf(m(fp, t, f) - m(rp, t, f));
     }
-  // norms of acceleration (T-2) and jerk (T-3)
-  for (int t = threadIdx.x; t < T; t += blockDim.x) {
+  // norms of acceleration (T-2) and jerk (T-3): four lanes per time step (a DPP quad), each
+  // summing every fourth feature, so the block's 256 threads all take part (one thread per t
+  // walking all Fd features was the kernel's latency-bound half)
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + (threadIdx.x >> 2), q = threadIdx.x & 3;
     float sa = 0.f, sj = 0.f;
     if (t < T - 2)
-      for (int f = 0; f < Fd; ++f) {
+      for (int f = q; f < Fd; f += 4) {
         const float a = m(fp, t + 1, f) - m(fp, t, f);
         sa += a * a;
       }
     if (t < T - 3)
-      for (int f = 0; f < Fd; ++f) {
+      for (int f = q; f < Fd; f += 4) {
         const float j = (m(fp, t + 2, f) - m(fp, t + 1, f)) - (m(fp, t + 1, f) - m(fp, t, f));
         sj += j * j;
       }
-    nacc[t] = sqrtf(sa);
-    njerk[t] = sqrtf(sj);
+    sa = quad_sum(sa);
+    sj = quad_sum(sj);
+    if (q == 0 && t < T) {
+      nacc[t] = sqrtf(sa);
+      njerk[t] = sqrtf(sj);
+    }
   }
   __syncthreads();
   double sa = 0.0, sj = 0.0;
@@ -396,7 +423,8 @@ int a2m_pose_losses_w_bwd_f32(const float* gen, int64_t gs_b, int64_t gs_t, cons
                               size_t ws_bytes, void* stream) {
   (void)ws; (void)ws_bytes;
   A2M_CHECK_ARG(gen && grad_out && dgen && B > 0 && T > 0, "pose_losses_bwd: bad args");
-  hipLaunchKernelGGL(pose_loss_bwd_kernel, dim3(B), dim3(256), 0, as_stream(stream), gen, gs_b, gs_t,
+  hipLaunchKernelGGL(pose_loss_bwd_kernel, dim3(B, (unsigned)cdiv(T, kTC)), dim3(256), 0, as_stream(stream), gen,
+                     gs_b, gs_t,
                      real, rs_b, rs_t, B, T, hand_w, body_w, grad_out, dgen);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
