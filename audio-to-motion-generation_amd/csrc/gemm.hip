@@ -292,6 +292,9 @@ struct Plan {
 #ifndef A2M_RED_FIXED_US
 #define A2M_RED_FIXED_US 3.0
 #endif
+#ifndef A2M_RED_FIXED_US_BF16
+#define A2M_RED_FIXED_US_BF16 6.0
+#endif
 
 // Tile / split-K choice by a cost model fitted to measured sweeps of the engine on MI355X
 // (tools/gemm_tune.py; DESIGN.md "GEMM planner").  For each candidate (tile, splits):
@@ -419,7 +422,7 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   constexpr double red_scale_rows = 2.0;
   if (splits > 1)
     t += (conv_rows ? red_scale_rows : red_scale) *
-         ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + A2M_RED_FIXED_US);
+         ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + (prec == 1 ? A2M_RED_FIXED_US_BF16 : A2M_RED_FIXED_US));
   return t;
 }
 
