@@ -3,8 +3,8 @@
 //   angle = 0.7 * mean relu(-a) + relu(a - pi)  over 30 hand triples (:350-392)
 //         + 0.3 * mean relu(-pi/2 - a) + relu(a - pi) over 5 body triples (:394-447)
 //   a = atan2(cross(u, v), dot(u, v)), u = p[j] - p[p], v = p[c] - p[j]
-// Two deterministic passes: per-clip partial sums (one workgroup per clip), then a single
-// workgroup reduction in a fixed order.
+// Two deterministic passes: per-(clip, 16-frame chunk) partial sums, then a single workgroup
+// reduction in a fixed order.
 #include "a2m_internal.h"
 
 namespace a2m {
@@ -46,41 +46,49 @@ __device__ __forceinline__ float signed_angle(const float* p, int a, int j, int 
   return atan2f(ux * vy - uy * vx, ux * vx + uy * vy);
 }
 
+// One workgroup per (clip, 16-frame chunk): the chunk's poses are staged in LDS with coalesced
+// loads, then the 35 joint angles of each frame and the 2 x 51 bone-length partial sums read LDS.
+// (One workgroup per clip walking all T * 35 angles was latency-bound: 15 us at B = 64, T = 64.)
+constexpr int kTCh = 16;
+
 __global__ __launch_bounds__(256) void pose_loss_partial_kernel(const float* gen, int64_t gs_b,
                                                                 int64_t gs_t, const float* real,
                                                                 int64_t rs_b, int64_t rs_t, int T,
                                                                 float* part) {
   __shared__ float red[4];
-  const int b = blockIdx.x;
-  float* pb = part + (int64_t)b * kPart;
-  // bone lengths averaged over time, one wave per (bone, pose) series with its lanes along t and
-  // a wave sum (one thread walking all T frames per series was latency-bound); without a real
-  // pose the bone loss is 0 and the generated lengths are not needed (the eval / inference path)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = wave; real != nullptr && i < 2 * kBones; i += (int)(blockDim.x >> 6)) {
-    const bool is_real = i >= kBones;
+  __shared__ float sg[kTCh][104];
+  __shared__ float sr[kTCh][104];
+  const int b = blockIdx.x, c = blockIdx.y, nch = gridDim.y;
+  const int t0 = c * kTCh, tn = min(kTCh, T - t0);
+  float* pb = part + ((int64_t)b * nch + c) * kPart;
+  for (int i = threadIdx.x; i < tn * 104; i += blockDim.x) {
+    const int t = i / 104, f = i % 104;
+    sg[t][f] = gen[b * gs_b + (int64_t)(t0 + t) * gs_t + f];
+    if (real != nullptr) sr[t][f] = real[b * rs_b + (int64_t)(t0 + t) * rs_t + f];
+  }
+  __syncthreads();
+  // bone-length sums over the chunk's frames, one thread per (bone, pose) series in frame order;
+  // without a real pose the bone loss is 0 and the generated lengths are not needed (inference)
+  if (real != nullptr && threadIdx.x < 2 * kBones) {
+    const int i = threadIdx.x;
     const int jb = (i % kBones) + 1, pj = kParents[jb];
-    const float* base = is_real ? real + b * rs_b : gen + b * gs_b;
-    const int64_t st = is_real ? rs_t : gs_t;
     float s = 0.f;
-    for (int t = lane; t < T; t += 64) {
-      const float* p = base + t * st;
+    for (int t = 0; t < tn; ++t) {
+      const float* p = i >= kBones ? sr[t] : sg[t];
       const float dx = p[2 * jb] - p[2 * pj], dy = p[2 * jb + 1] - p[2 * pj + 1];
       s += sqrtf(dx * dx + dy * dy);
     }
-    s = wave64_sum(s);
-    if (lane == 0) pb[i] = s / (float)T;
+    pb[i] = s;
   }
   float hs = 0.f, bs = 0.f;
-  for (int i = threadIdx.x; i < T * 35; i += blockDim.x) {
+  for (int i = threadIdx.x; i < tn * 35; i += blockDim.x) {
     const int t = i / 35, q = i % 35;
-    const float* p = gen + b * gs_b + t * gs_t;
     if (q < 30) {
-      const float a = signed_angle(p + 20, kHandTriples[q][0], kHandTriples[q][1], kHandTriples[q][2]);
+      const float a = signed_angle(sg[t] + 20, kHandTriples[q][0], kHandTriples[q][1], kHandTriples[q][2]);
       hs += fmaxf(0.f - a, 0.f) + fmaxf(a - 3.14159265358979f, 0.f);
     } else {
       const int r = q - 30;
-      const float a = signed_angle(p, kBodyTriples[r][0], kBodyTriples[r][1], kBodyTriples[r][2]);
+      const float a = signed_angle(sg[t], kBodyTriples[r][0], kBodyTriples[r][1], kBodyTriples[r][2]);
       bs += fmaxf(-1.57079632679490f - a, 0.f) + fmaxf(a - 3.14159265358979f, 0.f);
     }
   }
@@ -92,20 +100,26 @@ __global__ __launch_bounds__(256) void pose_loss_partial_kernel(const float* gen
   }
 }
 
-__global__ __launch_bounds__(256) void pose_loss_final_kernel(const float* part, int B, int T,
-                                                              int has_real, float hand_w,
+// Fixed-order reduction of the (clip, chunk) partials: bone means per clip = chunk sums / T.
+__global__ __launch_bounds__(256) void pose_loss_final_kernel(const float* part, int B, int nch,
+                                                              int T, int has_real, float hand_w,
                                                               float body_w, float* out) {
   __shared__ float red[4];
   float bone = 0.f, hs = 0.f, bs = 0.f;
   for (int i = threadIdx.x; has_real && i < B * kBones; i += blockDim.x) {
-    const float* pb = part + (int64_t)(i / kBones) * kPart;
+    const float* pb = part + (int64_t)(i / kBones) * nch * kPart;
     const int k = i % kBones;
-    const float d = pb[k] - pb[kBones + k];
+    float g = 0.f, r = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      g += pb[c * kPart + k];
+      r += pb[c * kPart + kBones + k];
+    }
+    const float d = g / (float)T - r / (float)T;
     bone += d * d;
   }
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    hs += part[(int64_t)b * kPart + 2 * kBones];
-    bs += part[(int64_t)b * kPart + 2 * kBones + 1];
+  for (int i = threadIdx.x; i < B * nch; i += blockDim.x) {
+    hs += part[(int64_t)i * kPart + 2 * kBones];
+    bs += part[(int64_t)i * kPart + 2 * kBones + 1];
   }
   const float Bn = block_sum(bone, red);
   const float Hs = block_sum(hs, red);
@@ -125,17 +139,18 @@ extern "C" int a2m_pose_losses_w_f32(const float* gen, int64_t gs_b, int64_t gs_
                                      float body_w, float* out, void* ws, size_t ws_bytes,
                                      void* stream) {
   A2M_CHECK_ARG(gen && out && B > 0 && T > 0, "pose_losses: bad args");
-  const size_t need = sizeof(float) * (size_t)B * kPart;
+  const int nch = (T + kTCh - 1) / kTCh;
+  const size_t need = sizeof(float) * (size_t)B * nch * kPart;
   if (!ws || ws_bytes < need) {
     set_error("pose_losses: workspace too small (%zu < %zu)", ws_bytes, need);
     return A2M_EWS;
   }
   float* part = static_cast<float*>(ws);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(pose_loss_partial_kernel, dim3(B), dim3(256), 0, st, gen, gs_b, gs_t, real,
-                     rs_b, rs_t, T, part);
+  hipLaunchKernelGGL(pose_loss_partial_kernel, dim3(B, nch), dim3(256), 0, st, gen, gs_b, gs_t,
+                     real, rs_b, rs_t, T, part);
   A2M_LAUNCH_CHECK();
-  hipLaunchKernelGGL(pose_loss_final_kernel, dim3(1), dim3(256), 0, st, part, B, T,
+  hipLaunchKernelGGL(pose_loss_final_kernel, dim3(1), dim3(256), 0, st, part, B, nch, T,
                      real != nullptr ? 1 : 0, hand_w, body_w, out);
   A2M_LAUNCH_CHECK();
   return A2M_OK;

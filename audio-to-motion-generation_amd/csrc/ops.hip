@@ -164,6 +164,94 @@ __global__ __launch_bounds__(256) void channel_att_weights_kernel(const float* x
   }
 }
 
+// The same with the scale fused, for C = 256, Cr = 32 and T = 64 (the model's shape): one
+// workgroup per clip keeps the clip's x (64 KB) in registers -- wave w, step k holds rows
+// 64w + 4k + (lane >> 4), 16 lanes a row, so every load and store instruction covers 1 KB of
+// contiguous rows -- and stores y = x * att from registers without a second pass over x.  The
+// MLP weights are loaded at the start alongside x (the layer-by-layer weight loads of the generic
+// kernel were its latency chain): layer 1 by (r, eighth of C) threads and an 8-lane sum, layer 2
+// one thread per channel.  Every x element is read before any y element of its clip is written
+// (the barriers between), so y may alias x.
+#ifndef A2M_CA_FUSED
+#define A2M_CA_FUSED 1
+#endif
+__global__ __launch_bounds__(256) void channel_att_fused256_kernel(const float* x, const float* w1,
+                                                                   const float* b1, const float* w2,
+                                                                   const float* b2, float* att,
+                                                                   float* y) {
+  constexpr int C = 256, Cr = 32, T = 64, NK = 16;
+  __shared__ __attribute__((aligned(16))) float pavg[C];
+  __shared__ __attribute__((aligned(16))) float pmax[C];
+  __shared__ float hid[2 * Cr];
+  __shared__ float satt[C];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6, q = lane & 15, sub = lane >> 4;
+  const int r = tid >> 3, part = tid & 7;
+  float4 w1v[8], w2v[8], xv[NK];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    w1v[k] = reinterpret_cast<const float4*>(w1 + r * C)[part + 8 * k];
+    w2v[k] = reinterpret_cast<const float4*>(w2 + tid * Cr)[k];
+  }
+  const float bias1 = b1[r], bias2 = b2[tid];
+  const float4* xb = reinterpret_cast<const float4*>(x + (int64_t)b * C * T);
+#pragma unroll
+  for (int k = 0; k < NK; ++k) xv[k] = xb[(64 * w + 4 * k + sub) * (T / 4) + q];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    float s = xv[k].x + xv[k].y + xv[k].z + xv[k].w;
+    float m = fmaxf(fmaxf(xv[k].x, xv[k].y), fmaxf(xv[k].z, xv[k].w));
+    s = row16_sum(s);
+    m = row16_max(m);
+    if (q == 0) {
+      pavg[64 * w + 4 * k + sub] = s / (float)T;
+      pmax[64 * w + 4 * k + sub] = m;
+    }
+  }
+  __syncthreads();
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float4 pa = reinterpret_cast<const float4*>(pavg)[part + 8 * k];
+    const float4 pm = reinterpret_cast<const float4*>(pmax)[part + 8 * k];
+    a0 += w1v[k].x * pa.x + w1v[k].y * pa.y + w1v[k].z * pa.z + w1v[k].w * pa.w;
+    a1 += w1v[k].x * pm.x + w1v[k].y * pm.y + w1v[k].z * pm.z + w1v[k].w * pm.w;
+  }
+  // sum over the 8 lanes of r (lanes 8r'..8r'+7 of the wave): xor 1, 2 in the quad, then xor 4
+  a0 = quad_sum(a0);
+  a1 = quad_sum(a1);
+  a0 += dpp_f<DPP_HALF_MIRROR>(a0);
+  a1 += dpp_f<DPP_HALF_MIRROR>(a1);
+  if (part == 0) {
+    a0 += bias1;
+    a1 += bias1;
+    hid[r] = a0 > 0.f ? a0 : 0.f;
+    hid[Cr + r] = a1 > 0.f ? a1 : 0.f;
+  }
+  __syncthreads();
+  float o0 = bias2, o1 = bias2;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    o0 += w2v[k].x * hid[4 * k] + w2v[k].y * hid[4 * k + 1] + w2v[k].z * hid[4 * k + 2] +
+          w2v[k].w * hid[4 * k + 3];
+    o1 += w2v[k].x * hid[Cr + 4 * k] + w2v[k].y * hid[Cr + 4 * k + 1] +
+          w2v[k].z * hid[Cr + 4 * k + 2] + w2v[k].w * hid[Cr + 4 * k + 3];
+  }
+  const float a = 1.f / (1.f + expf(-o0)) + 1.f / (1.f + expf(-o1));
+  att[(int64_t)b * C + tid] = a;
+  satt[tid] = a;
+  __syncthreads();
+  float4* yb = reinterpret_cast<float4*>(y + (int64_t)b * C * T);
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int row = 64 * w + 4 * k + sub;
+    const float ar = satt[row];
+    float4 v = xv[k];
+    v.x *= ar; v.y *= ar; v.z *= ar; v.w *= ar;
+    yb[row * (T / 4) + q] = v;
+  }
+}
+
 // y[b][c][t] = x[b][c][t] * att[b][c], float4 along T when T % 4 == 0.
 __global__ void channel_scale_kernel(const float* x, const float* att, int T, int64_t n, float* y) {
   if ((T & 3) == 0) {
@@ -1400,6 +1488,14 @@ int a2m_channel_attention_fwd_f32(const float* x, int32_t B, int32_t C, int32_t 
   const size_t lds = sizeof(float) * (2 * (size_t)C + 2 * Cr);
   A2M_CHECK_ARG(lds <= 64 * 1024, "channel_attention: C too large");
   hipStream_t st = as_stream(stream);
+  const bool al16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+                      reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2)) & 15) == 0;
+  if (A2M_CA_FUSED && C == 256 && Cr == 32 && T == 64 && al16) {
+    hipLaunchKernelGGL(channel_att_fused256_kernel, dim3(B), dim3(256), 0, st, x, w1, b1, w2, b2,
+                       att_out, y);
+    A2M_LAUNCH_CHECK();
+    return A2M_OK;
+  }
   hipLaunchKernelGGL(channel_att_weights_kernel, dim3(B), dim3(256), lds, st, x, C, T, w1, b1, Cr,
                      w2, b2, att_out);
   A2M_LAUNCH_CHECK();

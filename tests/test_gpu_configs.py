@@ -60,6 +60,7 @@ def _dp_worker(rank, world, port, outdir, q):
             dist.init_process_group('gloo', rank=rank, world_size=world)
         t = golden('train_step_b16t64.npz')
         f64 = golden('train_step_b16t64_f64.npz')
+        sens = golden('train_step_b16t64_f64_sens.npz')
         B = t['audio'].shape[0] // world
         audio = torch.from_numpy(t['audio'][rank * B:(rank + 1) * B]).to(dev)
         pose = torch.from_numpy(t['real_pose'][rank * B:(rank + 1) * B]).to(dev)
@@ -77,10 +78,10 @@ def _dp_worker(rank, world, port, outdir, q):
         g_loss = tr.g_step(audio, pose, valid)
         for p in d.parameters():
             p.requires_grad_(True)
-        eg = _grad_errors(g, t, f64, 'gG')
+        eg = _grad_errors(g, t, f64, sens, 'gG')
         np.save(os.path.join(outdir, f'gG_{world}_{rank}.npy'), tr.opt_G.flat_grad.cpu().numpy())
         d_loss = tr.d_step(audio, AG.pos_to_motion(pose), valid, fake)
-        ed = _grad_errors(d, t, f64, 'gD')
+        ed = _grad_errors(d, t, f64, sens, 'gD')
         np.save(os.path.join(outdir, f'gD_{world}_{rank}.npy'), tr.opt_D.flat_grad.cpu().numpy())
         pair = torch.stack([g_loss.reshape(()), d_loss.reshape(())]).double()
         tr._allreduce_(pair)

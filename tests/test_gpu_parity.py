@@ -324,6 +324,20 @@ def test_channel_attention_layernorm_mean_repeat():
     ref = OM.channel_attention(OM.Ctx(sd), 'c', x)
     d = [sd[k].to(DEV) for k in ('c.fc.0.weight', 'c.fc.0.bias', 'c.fc.2.weight', 'c.fc.2.bias')]
     assert rel_err(F.channel_attention(x.to(DEV), *d).cpu(), ref) < TOL
+    # the fused (C, T) = (256, 64) kernel in place (y aliasing x), with its weights vector
+    xi = x.to(DEV).clone()
+    att = torch.empty(3, 256, device=DEV)
+    F.channel_attention(xi, *d, out=xi, att=att)
+    assert rel_err(xi.cpu(), ref) < TOL
+    ra = ref / x
+    assert rel_err(att.cpu(), ra[:, :, 0]) < 1e-5
+    # the generic two-kernel path (other shapes)
+    x2 = _rand(2, 128, 40, seed=68)
+    sd2 = {'c.fc.0.weight': _rand(16, 128, seed=69, scale=0.08), 'c.fc.0.bias': _rand(16, seed=70, scale=0.1),
+           'c.fc.2.weight': _rand(128, 16, seed=71, scale=0.2), 'c.fc.2.bias': _rand(128, seed=72, scale=0.1)}
+    ref2 = OM.channel_attention(OM.Ctx(sd2), 'c', x2)
+    d2 = [sd2[k].to(DEV) for k in ('c.fc.0.weight', 'c.fc.0.bias', 'c.fc.2.weight', 'c.fc.2.bias')]
+    assert rel_err(F.channel_attention(x2.to(DEV), *d2).cpu(), ref2) < TOL
     rows = _rand(3 * 64, 256, seed=65)
     w, b = _rand(256, seed=66).abs() + .5, _rand(256, seed=67)
     ref = torch.nn.functional.layer_norm(rows, (256,), w, b).view(3, 64, 256).permute(0, 2, 1)

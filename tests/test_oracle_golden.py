@@ -199,3 +199,39 @@ def test_bf16_autocast_oracle_agrees_with_reference():
     # fp32 losses of the same step: the oracle and the reference agree to fp32 rounding
     assert abs(orc['g_loss_fp32'] - ref['g_loss_fp32']) < 1e-4 * abs(ref['g_loss_fp32'])
     assert abs(orc['d_loss_fp32'] - ref['d_loss_fp32']) < 1e-4 * abs(ref['d_loss_fp32'])
+
+
+@pytest.mark.parametrize('fixture', ['train_step_b16t64', 'train_step_b2t64'])
+def test_f64_sensitivity_fixture(fixture):
+    """oracle/make_f64_sensitivity.py's per-parameter change of the exact gradient under a 1e-7
+    relative input perturbation (fp32's rounding scale): one entry per sampled parameter, over
+    the parameters no larger than the reference's own fp32 error (median below 10x it: at B = 2
+    the G-step's median is 1.6e-3 against the reference's 1.1e-3), and setting the GPU gradient
+    bound (tests/test_gpu_train.py _SENS_MULT) on at most 2 % of the parameters (3 of 260 in each
+    G-step) -- at B = 2 the leaky-ReLU kink of body_gcn5's attention logits (a sensitivity 80x
+    the reference's error there)."""
+    from test_gpu_train import _CANCEL_FLOOR, _CANCELLING, _SENS_MULT, STEP_CASES
+    case = STEP_CASES['b16' if 'b16' in fixture else 'b2']
+    t = golden(fixture + '.npz')
+    f64 = golden(fixture + '_f64.npz')
+    s = golden(fixture + '_f64_sens.npz')
+    assert float(s['rel_noise']) == 1e-7
+    for prefix in ('gG', 'gD'):
+        sens = s[f'{prefix}_sens']
+        assert sens.shape == (len(t[f'{prefix}_names']),) and np.all(np.isfinite(sens)) and np.all(sens >= 0)
+        rs, rr = [], []
+        for i, n in enumerate(t[f'{prefix}_names']):
+            ok = t[f'{prefix}_idx'][i] >= 0
+            exact = f64[f'{prefix}_val'][i][ok]
+            scale = max(np.sqrt(t[f'{prefix}_sumsq'][i] / max(ok.sum(), 1)), np.abs(exact).max(), 1e-12)
+            rs.append(sens[i] / scale)
+            rr.append(np.abs(t[f'{prefix}_val'][i][ok] - exact).max() / scale)
+        assert np.median(rs) < 10.0 * np.median(rr), (prefix, np.median(rs), np.median(rr))
+        floor = [max(case['floor'], _CANCEL_FLOOR) if str(n).endswith(_CANCELLING) else case['floor']
+                 for n in t[f'{prefix}_names']]
+        binds = [str(n) for n, a, b, f in zip(t[f'{prefix}_names'], rs, rr, floor)
+                 if _SENS_MULT * a > case['ratio'] * max(b, f)]
+        assert len(binds) <= 0.02 * len(rs), binds
+        if fixture == 'train_step_b2t64' and prefix == 'gG':
+            i = list(t['gG_names']).index('body_gcn5.att_dst')
+            assert rs[i] > 0.02 and rs[i] > 30 * rr[i], (rs[i], rr[i])
