@@ -9,7 +9,7 @@ import sys
 if len(sys.argv) > 2 and sys.argv[1] == '--summarise':
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
     for line in open(sys.argv[2]):
-        m = re.match(r'a2m gemm-time (.*) tile ([\d.]+) us reduce ([\d.]+) us', line)
+        m = re.match(r'a2m gemm-time (.*) tile ([\d.]+) us (?:\(all-XCD span [\d.]+\) )?reduce ([\d.]+) us', line)
         if m:
             a = agg[m.group(1)]
             a[0] += 1
