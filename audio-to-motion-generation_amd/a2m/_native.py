@@ -130,6 +130,7 @@ SIGNATURES = {
     'a2m_gemm_plan_override': (ctypes.c_int, [I32, I32]),
     'a2m_gemm_pipe_override': (ctypes.c_int, [I32]),
     'a2m_set_gemm_precision': (ctypes.c_int, [I32]),
+    'a2m_set_attn_eval_chunk': (ctypes.c_int, [I32]),
     'a2m_get_gemm_precision': (I32, []),
     'a2m_gemm_timing_end': (ctypes.c_int, [ctypes.POINTER(I64), ctypes.POINTER(F64), ctypes.POINTER(F64),
                                            ctypes.POINTER(F64), ctypes.POINTER(I64)]),

@@ -166,7 +166,15 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
 constexpr int QP = 36;        // Q^T / K^T pitch (32 columns): conflict-free b128 rows
 constexpr int FK = 32;        // projection k-tile (channels)
 constexpr int FKP = FK + 4;   // staged tile pitch
-constexpr int FCOLS = 128;    // projection output columns: Q 32 | K 32 | V 64
+// V channels per workgroup at C % 128 == 0.  128 computes a C = 256 clip's Q / K twice instead of
+// four times: the kernel's time drops 358.5 -> 305.8 us a step, but the step got 0.5-0.7 % slower
+// (fp32 2.520 vs 2.503 ms, bf16 1.439 vs 1.432, three interleaved pairs,
+// profiles/r06_j_attn_chunk_ab.txt): half the workgroups, each longer, on the decoder's critical
+// path.  64 stays the default; 128 is reachable through a2m_set_attn_eval_chunk (tests).
+#ifndef A2M_ATTN_NV
+#define A2M_ATTN_NV 64
+#endif
+static int g_attn_nv = A2M_ATTN_NV;   // a2m_set_attn_eval_chunk (test hook)
 
 // bf16 operand mode (precision 1): the projection's products on v_mfma_f32_32x32x16_bf16 --
 // each lane's 8 staged k of a 16-k half rounded to bf16 in registers (the fp32 fragment layout is
@@ -185,8 +193,14 @@ __device__ __forceinline__ bf16x8 attn_pack8(const float (&v)[8]) {
   return __builtin_bit_cast(bf16x8, u4{u[0], u[1], u[2], u[3]});
 }
 
-template <bool BF16>
-__global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
+// NV = V channels per workgroup (64 or 128): the projection has FC = 64 + NV columns (Q 32 | K 32 |
+// V NV), FC / 32 column tiles by 2 t tiles = one 32 x 32 tile per wave (8 waves at NV = 64, 12 at
+// 128).  At NV = 128 a C = 256 clip's Q and K are computed twice instead of four times (the
+// projection 1.33x the non-redundant 5C/4 rows instead of 1.6x); every output element sees the
+// same operations in the same order at either NV, so the two are bitwise equal (NV = 64 is the
+// default, A2M_ATTN_NV below).
+template <bool BF16, int NV>
+__global__ __launch_bounds__(NV == 64 ? 512 : 768, NV == 64 ? 2 : 1) void attn_fused_eval_kernel(
     const float* __restrict__ x, int64_t x_bs, int C, int T, const float* __restrict__ wqkv,
     const float* __restrict__ bqkv, const float* __restrict__ gamma, const float* __restrict__ res,
     float* __restrict__ y, int B, int64_t x_gs, int64_t res_gs, int64_t y_gs) {
@@ -199,27 +213,31 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
     bqkv += (int64_t)g * (C / 4 + C);
     gamma += g;
   }
-  constexpr int XT = AT * FKP, WTL = FCOLS * FKP, STG = XT + WTL;  // eight waves
+  constexpr int FC = 64 + NV, NCT = FC / 32, NT = 64 * 2 * NCT;
+  constexpr int XT = AT * FKP, WTL = FC * FKP, STG = XT + WTL;
   // stages (2 x (x tile + w tile)) early; Q^T, K^T, V, scores overlay them afterwards
   __shared__ __attribute__((aligned(16))) float lds[2 * STG];
   float* qs = lds;                     // [i][c'] pitch QP
   float* ks = qs + AT * QP;            // [j][c']
   float* vs = ks + AT * QP;            // [c][j]  pitch AP
-  float* ss = vs + ACH * AP;           // [i][j]  pitch AP
-  static_assert(2 * AT * QP + 2 * ACH * AP <= 2 * STG, "overlay must fit the stages");
-  const int b = blockIdx.y % B, c0 = blockIdx.x * ACH;
+  float* ss = vs + NV * AP;            // [i][j]  pitch AP
+  static_assert(2 * AT * QP + (NV + AT) * AP <= 2 * STG, "overlay must fit the stages");
+  static_assert(FC * 8 == 2 * NT, "two float4 of weight rows per thread");
+  const int b = blockIdx.y % B, c0 = blockIdx.x * NV;
   const int Cq = C / 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
-  // projection: eight waves, wave (pt, pc) = (wave >> 2, wave & 3) owns t rows 32 pt.. and
-  // columns 32 pc.. (one accumulator; two waves per SIMD hide each other's LDS and barrier
-  // waits); attention steps: waves 0-3 as (wt, wc) = (wave >> 1, wave & 1)
-  const int pt = wave >> 2, pc = wave & 3;
-  const int wt = (wave & 3) >> 1, wc = wave & 1;
+  // projection: wave (pt, pc) = (wave / NCT, wave % NCT) owns t rows 32 pt.. and columns 32 pc..
+  // (one accumulator; two or three waves per SIMD hide each other's LDS and barrier waits);
+  // attention steps: the score product on waves 0-3 as (wt, wc) = (wave >> 1, wave & 1), PV on
+  // waves 4.. as (channel tile, query tile) = ((wave - 4) >> 1, (wave - 4) & 1)
+  const int pt = wave / NCT, pc = wave % NCT;
+  const int wt = wave < 4 ? wave >> 1 : (wave - 4) >> 1, wc = wave & 1;
   const float* xb = x + (int64_t)b * x_bs;
 
   // Staging maps.  x tile [t][c] from x[c][t]: thread -> (c = tid % 32, t quad = tid / 32), one
-  // float4 per thread, transposed writes conflict-free (32 lanes = 32 consecutive c).
+  // float4 per thread of the first 512, transposed writes conflict-free (32 lanes = 32
+  // consecutive c).
   // w tile [col][c]: stacked rows Q 0..Cq-1 -> cols 0.., K Cq.. -> 32.., V 2Cq + c0.. -> 64..;
   // two float4 per thread along c.  All loads are raw buffer loads (rows past Cq / t past T read
   // 0), so the k-step below is branch-free and its operand work is placed between the MFMAs
@@ -227,14 +245,15 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   // MFMAs, one barrier, the next fragments read behind the second half's first MFMAs).
   const __amdgpu_buffer_rsrc_t xrs = pipe_rsrc(xb), wrs = pipe_rsrc(wqkv);
   const int xc = tid & 31, xq = tid >> 5;
+  const bool xst = xq < AT / 4;   // this thread stages a piece of the x tile
   uint32_t xoff = 4 * xq < T ? (uint32_t)(xc * T + 4 * xq) * 4u : kPipeOOB;   // advanced 32 channels a tile
   uint32_t woff[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int col = (tid + u * 512) >> 3;
+    const int col = (tid + u * NT) >> 3;
     const int wrow = col < 32 ? (col < Cq ? col : -1)
                               : col < 64 ? (col - 32 < Cq ? Cq + col - 32 : -1) : 2 * Cq + c0 + col - 64;
-    woff[u] = wrow >= 0 ? (uint32_t)(wrow * C + ((tid + u * 512) & 7) * 4) * 4u : kPipeOOB;
+    woff[u] = wrow >= 0 ? (uint32_t)(wrow * C + ((tid + u * NT) & 7) * 4) * 4u : kPipeOOB;
   }
   struct Regs { float4 x, w[2]; };
   Regs rg[2];
@@ -250,11 +269,12 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   };
   auto store_piece = [&](float* st, const Regs& r, int piece) {   // 0-1: x halves, 2-3: w rows
     if (piece < 2) {
+      if (!xst) return;
       float* xs = st + (4 * xq + 2 * piece) * FKP + xc;
       xs[0] = piece == 0 ? r.x.x : r.x.z;
       xs[FKP] = piece == 0 ? r.x.y : r.x.w;
     } else {
-      const int e = tid + (piece - 2) * 512;
+      const int e = tid + (piece - 2) * NT;
       *reinterpret_cast<float4*>(st + XT + (e >> 3) * FKP + (e & 7) * 4) = r.w[piece - 2];
     }
   };
@@ -332,7 +352,7 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   }
   __syncthreads();
 
-  // waves 4-7 (PV + epilogue) fetch their x / residual values now, while waves 0-3 run the
+  // waves 4.. (PV + epilogue) fetch their x / residual values now, while waves 0-3 run the
   // score product and the softmax, instead of after their PV MFMAs
   float xv[16], rv[16];
   if (wave >= 4 && wc * 32 + li < T) {
@@ -404,7 +424,7 @@ __global__ __launch_bounds__(512, 2) void attn_fused_eval_kernel(
   }
   __syncthreads();
 
-  // out[c][i] = sum_j V[c][j] A[i][j]: waves 4-7, wave (wt, wc) owns channels 32 wt.., queries 32 wc..
+  // out[c][i] = sum_j V[c][j] A[i][j]: waves 4.., wave (wt, wc) owns channels 32 wt.., queries 32 wc..
   if (wave < 4) return;
 #pragma unroll
   for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
@@ -639,13 +659,24 @@ int attn_core_wide(const float* qkv, int64_t qs_b, int B, int C, int T, const fl
 int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const float* wqkv,
                     const float* bqkv, const float* gamma, const float* res, float* y,
                     hipStream_t st, int G, int64_t x_gs, int64_t res_gs, int64_t y_gs) {
-  dim3 grid((unsigned)cdiv(C, ACH), (unsigned)(B * G));
-  if (a2m_get_gemm_precision() == 1)
-    hipLaunchKernelGGL(attn_fused_eval_kernel<true>, grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
-                       res, y, B, x_gs, res_gs, y_gs);
-  else
-    hipLaunchKernelGGL(attn_fused_eval_kernel<false>, grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
-                       res, y, B, x_gs, res_gs, y_gs);
+  const bool bf16 = a2m_get_gemm_precision() == 1;
+  if (g_attn_nv == 128 && C % 128 == 0) {
+    dim3 grid((unsigned)(C / 128), (unsigned)(B * G));
+    if (bf16)
+      hipLaunchKernelGGL((attn_fused_eval_kernel<true, 128>), grid, dim3(768), 0, st, x, x_bs, C, T, wqkv, bqkv,
+                         gamma, res, y, B, x_gs, res_gs, y_gs);
+    else
+      hipLaunchKernelGGL((attn_fused_eval_kernel<false, 128>), grid, dim3(768), 0, st, x, x_bs, C, T, wqkv, bqkv,
+                         gamma, res, y, B, x_gs, res_gs, y_gs);
+  } else {
+    dim3 grid((unsigned)cdiv(C, 64), (unsigned)(B * G));
+    if (bf16)
+      hipLaunchKernelGGL((attn_fused_eval_kernel<true, 64>), grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv,
+                         gamma, res, y, B, x_gs, res_gs, y_gs);
+    else
+      hipLaunchKernelGGL((attn_fused_eval_kernel<false, 64>), grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv,
+                         gamma, res, y, B, x_gs, res_gs, y_gs);
+  }
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }
@@ -663,3 +694,12 @@ int attn_core(const float* qkv, int64_t qs_b, int B, int C, int T, const float* 
 }
 
 }  // namespace a2m
+
+extern "C" int a2m_set_attn_eval_chunk(int32_t nv) {
+  if (nv != 64 && nv != 128) {
+    a2m::set_error("set_attn_eval_chunk: %d (64 or 128)", (int)nv);
+    return A2M_EINVAL;
+  }
+  a2m::g_attn_nv = nv;
+  return A2M_OK;
+}

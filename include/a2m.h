@@ -551,6 +551,12 @@ int a2m_gemm_plan_override(int32_t tile, int32_t splits);
  * tile (gemm_pipe.h / gemm_pipe_bf16.h), 0 gemm_tile, -1 the default
  * (1).  Both give bitwise-equal results; process-global, not for production. */
 int a2m_gemm_pipe_override(int32_t mode);
+/* Test hook: V channels per workgroup of the fused eval SelfAttention at C % 128 == 0 -- 64
+ * (default: eight waves, Q / K computed by each of the C / 64 chunks) or 128 (twelve waves, Q / K
+ * once per two 64-channel chunks: less kernel time, but measured 0.5-0.7 % slower a step).  Both
+ * give bitwise-equal results; A2M_EINVAL for any other value.  Process-global, not for
+ * production. */
+int a2m_set_attn_eval_chunk(int32_t nv);
 /* Operand precision of every GEMM-engine launch (convs, linears, attention products and their
  * backward) issued after the call: 0 = fp32 (default; the parity configuration), 1 = bf16
  * operands with fp32 accumulation (BASELINE configs[4], torch.autocast(bfloat16)-equivalent:

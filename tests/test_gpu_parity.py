@@ -244,6 +244,26 @@ def test_self_attention(B, C, T):
                                 d['a.key_conv.weight'], d['a.key_conv.bias'], d['a.value_conv.weight'],
                                 d['a.value_conv.bias'], d['a.gamma'], res=res.to(DEV), save=save)
         assert 'qkv' in save and rel_err(out.cpu(), out2.cpu()) < 2e-6
+    if N.lib.a2m_self_attention_eval_fits(C, T) and C % 128 == 0:
+        # the fused kernel's V chunks of 64 channels (the default) and of 128 (Q / K once per two
+        # 64-channel chunks): the same operations per output element, so bitwise equal, fp32 and
+        # bf16 operand modes
+        outs = {}
+        try:
+            for prec in (0, 1):
+                N.check(N.lib.a2m_set_gemm_precision(prec))
+                for nv in (64, 128):
+                    N.check(N.lib.a2m_set_attn_eval_chunk(nv))
+                    outs[prec, nv] = F.self_attention(
+                        x.to(DEV), d['a.query_conv.weight'], d['a.query_conv.bias'], d['a.key_conv.weight'],
+                        d['a.key_conv.bias'], d['a.value_conv.weight'], d['a.value_conv.bias'], d['a.gamma'],
+                        res=res.to(DEV)).cpu()
+        finally:
+            N.lib.a2m_set_attn_eval_chunk(64)
+            N.lib.a2m_set_gemm_precision(0)
+        assert torch.equal(outs[0, 64], outs[0, 128]) and torch.equal(outs[1, 64], outs[1, 128])
+        assert torch.equal(outs[0, 64], out.cpu())
+        assert N.lib.a2m_set_attn_eval_chunk(96) == N.A2M_EINVAL
     save = {}
     F.self_attention(x.to(DEV), d['a.query_conv.weight'], d['a.query_conv.bias'], d['a.key_conv.weight'],
                      d['a.key_conv.bias'], d['a.value_conv.weight'], d['a.value_conv.bias'], d['a.gamma'],
