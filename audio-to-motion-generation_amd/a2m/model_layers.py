@@ -193,11 +193,12 @@ class ConvTranspose1D(nn.Module):
                          act=F.ACT_RELU, out=out, cache=self._pack)
 
 
-_ENC_NHWC = __import__('os').environ.get('A2M_ENC_NHWC', '1') != '0'
-_ENC_NHWC_ALL = __import__('os').environ.get('A2M_ENC_NHWC_ALL', '1') != '0'
+# module flags (measured-slower alternatives stay reachable from tests by flipping them)
+_ENC_NHWC = True       # channels-last encoder chain
+_ENC_NHWC_ALL = True   # ... for every layer whose Ci is 1 or a multiple of 64
 # the last conv + time resample as one GEMM whose reduce writes the resampled output
-# (a2m_conv2d_nhwc_interp_fwd_f32); A2M_ENC_FUSED_INTERP=0 restores conv + interp_time
-_ENC_FUSED_INTERP = __import__('os').environ.get('A2M_ENC_FUSED_INTERP', '1') != '0'
+# (a2m_conv2d_nhwc_interp_fwd_f32); False restores conv + interp_time
+_ENC_FUSED_INTERP = True
 
 
 class AudioEncoder(nn.Module):
@@ -277,7 +278,7 @@ class AudioEncoder(nn.Module):
         """Channels-last for every layer the GEMM engine can read as contiguous channel runs:
         conv0 (Ci = 1, its direct kernel) and every layer with Ci a multiple of the k-tile
         (loader mode 6: each k-tile is one tap's channel slice), so no layer needs an im2col
-        matrix (A2M_ENC_NHWC_ALL=0 restores the round-2 split: channels-last only below K =
+        matrix (_ENC_NHWC_ALL = False restores the round-2 split: channels-last only below K =
         2048, im2col + dense GEMM above)."""
         w = self.conv[i].conv.weight
         Ci, kw = w.shape[1], w.shape[3]

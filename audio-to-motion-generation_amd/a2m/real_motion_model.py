@@ -147,7 +147,7 @@ class SelfAttention_G(_GraphTopology):
     # Eval can run each shared layer for both branches as ONE grouped launch (batch = 2
     # problems with their own weights): twice the workgroups per launch, half the launches.
     # Per launch that is faster (two 256->256 k3 convs 62 -> 48 us, two attentions 40 -> 33 us),
-    # but the step measured slower than two concurrent branch streams (A2M_GROUPED_DEC 0 / 1 /
+    # but the step measured slower than two concurrent branch streams (_GROUPED 0 / 1 /
     # 2: 2.787 / 2.824 / 2.851 ms, three interleaved 200-step runs each): the chip is already
     # full at B = 64, and the grouped schedule leaves the latency-bound hand graph stack with
     # less concurrent work beside it.  Off by default; tests/test_gpu_grouped.py keeps it exact.
@@ -313,7 +313,7 @@ class SelfAttention_G(_GraphTopology):
 _BRANCH_STREAMS = os.environ.get('A2M_BRANCH_STREAMS', '1') != '0'
 # body + hand decoder layers as grouped launches: 0 off, 1 decoder_pre grouped (the rest per
 # branch on two streams), 2 decoder_pre and decoder_post grouped
-_GROUPED = int(os.environ.get('A2M_GROUPED_DEC', '0'))
+_GROUPED = 0
 
 
 def N_tap_chunk():
@@ -326,7 +326,7 @@ def _group_sources(m):
         n = m.norm
         return (m.conv.weight, m.conv.bias, n.weight, n.bias, n.running_mean, n.running_var)
     return m.weights()   # SelfAttention
-_FUSED_STACK = os.environ.get('A2M_GRAPH_STACK', '1') != '0'   # one launch for the 5 graph layers
+_FUSED_STACK = True   # one launch for the 5 graph layers
 _SIDE_STREAMS = {}
 
 
