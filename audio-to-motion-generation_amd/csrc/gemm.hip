@@ -306,8 +306,8 @@ struct Plan {
 // operand (modes 2/3: transposed LDS staging) costs the 64x64 tile ~16 % of throughput and
 // the 128x128 tile ~6 us more per round of blocks.  The model is
 // deterministic in (M, N, K, batch, gathered), so a shape always gets the same plan and the
-// same (bitwise-reproducible) split order.  A2M_GEMM_TILE=64|128, A2M_GEMM_SPLIT=n,
-// a2m_gemm_plan_override and A2M_GEMM_XCD=g override (experiments).
+// same (bitwise-reproducible) split order.  a2m_gemm_plan_override and A2M_GEMM_PLAN_RULES
+// (per-shape "M,N,K:tile:splits;...") override it (experiments).
 // Operand precision of the engine: 0 = fp32 (v_mfma_f32_32x32x2_f32, BK 32; the default and
 // the parity configuration), 1 = bf16 (operands rounded to bf16 in LDS, fp32 accumulation,
 // BK 64; a2m_set_gemm_precision, configs[4]), 2 = bf16x6 (fp32 operands split exactly into

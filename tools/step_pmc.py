@@ -6,7 +6,7 @@ read the output (replay_filter.py) keep only the dispatches after the marker, i.
 replayed steps: no first-call repacks, no eager-step copies.
 
     rocprofv3 --pmc FETCH_SIZE -d DIR -- python tools/step_pmc.py [R] [--dtype bf16]
-        [--engine-json F] [--stamps F] [--sync]
+        [--engine-json F] [--stamps F] [--sync] [--batch B]
 --stamps also records the engine launches' own span stamps in every replay (a device sync after
 each replay), so the kernel trace and the stamps describe the same dispatches
 (tools/stamp_vs_trace.py).
@@ -39,6 +39,11 @@ def main():
     # with it (engine 2628 us/step against 2345 us with a sync per replay, the stamps' 2265 us of
     # spans + 2.2 us per launch); unprofiled, synced and free-running replays take the same time
     # (tools/branch_probe.py: 2.672 vs 2.661 ms)
+    B = 64
+    if '--batch' in argv:
+        i = argv.index('--batch')
+        B = int(argv[i + 1])
+        del argv[i:i + 2]
     sync = '--sync' in argv
     args = [a for a in argv if not a.startswith('--') and a != 'bf16']
     reps = int(args[0]) if args else 3
@@ -46,7 +51,7 @@ def main():
     import a2m
     a2m.set_gemm_precision('bf16' if '--dtype' in sys.argv and 'bf16' in sys.argv else 'fp32')
     from a2m.real_motion_model import SelfAttention_G
-    B, T = 64, 64
+    T = 64
     torch.manual_seed(1234)
     g = SelfAttention_G(time_steps=T, p=0.2)
     for m in g.modules():
