@@ -49,6 +49,9 @@ SIGNATURES = {
     'a2m_graph_att_proj_f32': (ctypes.c_int, [P, P, P, P, P]),
     'a2m_graph_stack_fwd_f32': (ctypes.c_int, [P, I32, I32, P, P, I32, P, P, P, P, P, P, P, F32,
                                                P, P]),
+    'a2m_graph_stack_fwd_ex_f32': (ctypes.c_int, [P, I32, I32, P, P, I32, P, P, P, P, P, P, P, P, P,
+                                                  F32, P, P]),
+    'a2m_to_bf16_f32': (ctypes.c_int, [P, P, I64, P]),
     'a2m_conv1d_tap_pack_f32': (ctypes.c_int, [P, I32, I32, I32, I32, P, P]),
     'a2m_conv1d_tap_fwd_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, P, I32, P, I32, I32, I32,
                                               P, P, P, P, F32, I32, F32, P, I64, I64, I64, P, SZ, P]),

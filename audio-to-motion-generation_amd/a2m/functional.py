@@ -522,9 +522,29 @@ def graph_att_proj(w0, att_src, att_dst, cache=None):
     return U
 
 
-def graph_stack(x, J, nbr_ptr, nbr_idx, layers, slope=0.2, out=None):
-    """Fused eval stack of graph layers (a2m_graph_stack_fwd_f32).  x: [F*J, 64] contiguous;
-    layers: list of (kind, w0, w1, U, bias, ln_w, ln_b) with U from graph_att_proj for GAT."""
+def to_bf16(x, out=None):
+    """bf16 (RNE) copy of a contiguous fp32 tensor (a2m_to_bf16_f32)."""
+    _check_dev(x, out)
+    assert x.is_contiguous() and x.dtype == torch.float32
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    N.check(N.lib.a2m_to_bf16_f32(_p(x), _p(out), x.numel(), _stream()))
+    return out
+
+
+def graph_weights_bf16(w0, w1, cache):
+    """bf16 copies of a graph layer's weights for the bf16 operand mode's fused stack, cached in
+    `cache` per weight version (w1 may be None: GAT)."""
+    key = _wkey((w0, w1))
+    if cache.get('key') != key:
+        cache.update(key=key, h0=to_bf16(w0.detach()), h1=None if w1 is None else to_bf16(w1.detach()))
+    return cache['h0'], cache['h1']
+
+
+def graph_stack(x, J, nbr_ptr, nbr_idx, layers, slope=0.2, out=None, wh=None):
+    """Fused eval stack of graph layers (a2m_graph_stack_fwd_ex_f32).  x: [F*J, 64] contiguous;
+    layers: list of (kind, w0, w1, U, bias, ln_w, ln_b) with U from graph_att_proj for GAT;
+    wh: optional per-layer (w0, w1) bf16 copies (graph_weights_bf16) for the bf16 operand mode."""
     _check_dev(x, out)
     assert x.is_contiguous() and x.shape[1] == 64 and x.shape[0] % J == 0 and 0 < len(layers) <= 8
     F = x.shape[0] // J
@@ -533,9 +553,11 @@ def graph_stack(x, J, nbr_ptr, nbr_idx, layers, slope=0.2, out=None):
     n = len(layers)
     ptrs = lambda i: (ctypes.c_void_p * n)(*[_p(L[i]) for L in layers])  # noqa: E731
     kinds = (ctypes.c_int32 * n)(*[L[0] for L in layers])
-    N.check(N.lib.a2m_graph_stack_fwd_f32(_p(x), F, J, _p(nbr_ptr), _p(nbr_idx), n, kinds,
-                                          ptrs(1), ptrs(2), ptrs(3), ptrs(4), ptrs(5), ptrs(6),
-                                          slope, _p(out), _stream()))
+    hp = [None, None] if wh is None else \
+        [(ctypes.c_void_p * n)(*[_p(h[i]) for h in wh]) for i in (0, 1)]
+    N.check(N.lib.a2m_graph_stack_fwd_ex_f32(_p(x), F, J, _p(nbr_ptr), _p(nbr_idx), n, kinds,
+                                             ptrs(1), ptrs(2), ptrs(3), ptrs(4), ptrs(5), ptrs(6),
+                                             hp[0], hp[1], slope, _p(out), _stream()))
     return out
 
 

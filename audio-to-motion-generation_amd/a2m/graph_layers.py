@@ -26,6 +26,7 @@ class GATConv(nn.Module):
         self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
         self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
         self._U = {}   # attention projections for the fused eval stack (functional.graph_att_proj)
+        self._Wh = {}  # bf16 weight copies for the bf16 mode's fused stack (functional.graph_weights_bf16)
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -51,3 +52,4 @@ class GraphConv(nn.Module):
         assert aggr == 'add'
         self.lin_rel = nn.Linear(in_channels, out_channels, bias=bias)
         self.lin_root = nn.Linear(in_channels, out_channels, bias=False)
+        self._Wh = {}  # bf16 weight copies for the bf16 mode's fused stack (functional.graph_weights_bf16)

@@ -105,7 +105,8 @@ class SelfAttention_G(_GraphTopology):
         ptr, idx = self.topology(part)
         lns = getattr(self, f'{part}_layer_norms')
         if _FUSED_STACK:
-            layers = []
+            layers, wh = [], []
+            bf16 = F.N.lib.a2m_get_gemm_precision() == 1
             for L in range(5):
                 g = getattr(self, f'{part}_gcn{L + 1}')
                 if L % 2 == 0:
@@ -114,7 +115,9 @@ class SelfAttention_G(_GraphTopology):
                 else:
                     layers.append((1, g.lin_rel.weight, g.lin_root.weight, None, g.lin_rel.bias,
                                    lns[L].weight, lns[L].bias))
-            a = F.graph_stack(a, nj, ptr, idx, layers, out=b)
+                if bf16 and _STACK_BF16_WEIGHTS:
+                    wh.append(F.graph_weights_bf16(layers[-1][1], layers[-1][2], g._Wh))
+            a = F.graph_stack(a, nj, ptr, idx, layers, out=b, wh=wh or None)
         else:
             for L in range(5):
                 g = getattr(self, f'{part}_gcn{L + 1}')
@@ -327,6 +330,8 @@ def _group_sources(m):
         return (m.conv.weight, m.conv.bias, n.weight, n.bias, n.running_mean, n.running_var)
     return m.weights()   # SelfAttention
 _FUSED_STACK = True   # one launch for the 5 graph layers
+# bf16 operand mode: the stack's layer weights as cached bf16 copies (bitwise the same result)
+_STACK_BF16_WEIGHTS = True
 _SIDE_STREAMS = {}
 
 

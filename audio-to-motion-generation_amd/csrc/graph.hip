@@ -321,6 +321,10 @@ struct GraphStack {
   const float* bias[GMAXL];
   const float* ln_w[GMAXL];
   const float* ln_b[GMAXL];
+  // bf16 mode: the layer weights as bf16 copies in the fp32 weights' [row][64] layout (made once
+  // per weight version, a2m_to_bf16_f32); null: rounded from the fp32 weights in the k loop
+  const __bf16* w0h[GMAXL];
+  const __bf16* w1h[GMAXL];
   float slope;
   int bf16;   // 1: layer products with bf16 operands (precision 1)
 };
@@ -468,8 +472,9 @@ __device__ __forceinline__ sbf16x8 stack_pack8(const float (&v)[8]) {
 
 template <int DL, bool GAT>
 __device__ __forceinline__ void stack_layer_kh(const float* xs, const float (*al)[GMAXN], const int (&id)[GMAXDEG],
-                                               int node, int d0, const float* W0, const float* W1, int li,
-                                               int lh, floatx16 (&acc)[2]) {
+                                               int node, int d0, const float* W0, const float* W1,
+                                               const __bf16* H0, const __bf16* H1, int li, int lh,
+                                               floatx16 (&acc)[2]) {
   constexpr int NS = GAT ? GHEADS : 1;
   constexpr int NSEG = GAT ? GHEADS : 2;
   float wq[NS][DL];
@@ -505,12 +510,19 @@ __device__ __forceinline__ void stack_layer_kh(const float* xs, const float (*al
       const float* W = GAT ? W0 + h * GF * GF : (h == 0 ? W0 : W1);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const float* wr = W + (t * 32 + li) * GF + off;
-        const float4 b0 = *reinterpret_cast<const float4*>(wr);
-        const float4 b1 = *reinterpret_cast<const float4*>(wr + 4);
-        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-        if (STACK_TEPI) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(stack_pack8(bv), af, acc[t], 0, 0, 0);
-        else acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, stack_pack8(bv), acc[t], 0, 0, 0);
+        sbf16x8 wb;
+        if (H0) {   // the cached bf16 copy: one 16-byte load, no rounding in the loop
+          const __bf16* H = GAT ? H0 + h * GF * GF : (h == 0 ? H0 : H1);
+          wb = *reinterpret_cast<const sbf16x8*>(H + (t * 32 + li) * GF + off);
+        } else {
+          const float* wr = W + (t * 32 + li) * GF + off;
+          const float4 b0 = *reinterpret_cast<const float4*>(wr);
+          const float4 b1 = *reinterpret_cast<const float4*>(wr + 4);
+          const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+          wb = stack_pack8(bv);
+        }
+        if (STACK_TEPI) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, af, acc[t], 0, 0, 0);
+        else acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, wb, acc[t], 0, 0, 0);
       }
     }
   }
@@ -519,16 +531,17 @@ __device__ __forceinline__ void stack_layer_kh(const float* xs, const float (*al
 template <bool GAT>
 __device__ __forceinline__ void stack_layer_dispatch_h(int dl, const float* xs, const float (*al)[GMAXN],
                                                        const int (&id)[GMAXDEG], int node, int d0, const float* W0,
-                                                       const float* W1, int li, int lh, floatx16 (&acc)[2]) {
+                                                       const float* W1, const __bf16* H0, const __bf16* H1, int li,
+                                                       int lh, floatx16 (&acc)[2]) {
   switch (dl) {
-    case 1: stack_layer_kh<1, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 2: stack_layer_kh<2, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 3: stack_layer_kh<3, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 4: stack_layer_kh<4, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 5: stack_layer_kh<5, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 6: stack_layer_kh<6, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    case 7: stack_layer_kh<7, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
-    default: stack_layer_kh<8, GAT>(xs, al, id, node, d0, W0, W1, li, lh, acc); break;
+    case 1: stack_layer_kh<1, GAT>(xs, al, id, node, d0, W0, W1, H0, H1, li, lh, acc); break;
+    case 2: stack_layer_kh<2, GAT>(xs, al, id, node, d0, W0, W1, H0, H1, li, lh, acc); break;
+    case 3: stack_layer_kh<3, GAT>(xs, al, id, node, d0, W0, W1, H0, H1, li, lh, acc); break;
+    case 4: stack_layer_kh<4, GAT>(xs, al, id, node, d0, W0, W1, H0, H1, li, lh, acc); break;
+    case 5: stack_layer_kh<5, GAT>(xs, al, id, node, d0, W0, W1, H0, H1, li, lh, acc); break;
+    case 6: stack_layer_kh<6, GAT>(xs, al, id, node, d0, W0, W1, H0, H1, li, lh, acc); break;
+    case 7: stack_layer_kh<7, GAT>(xs, al, id, node, d0, W0, W1, H0, H1, li, lh, acc); break;
+    default: stack_layer_kh<8, GAT>(xs, al, id, node, d0, W0, W1, H0, H1, li, lh, acc); break;
   }
 }
 
@@ -676,8 +689,9 @@ __global__ __launch_bounds__(256, BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU)
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
     dl = __builtin_amdgcn_readfirstlane(dl);
     if constexpr (BF16) {
-      if (gat) stack_layer_dispatch_h<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
-      else stack_layer_dispatch_h<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
+      if (gat) stack_layer_dispatch_h<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], S.w0h[L], S.w1h[L], li, lh, acc);
+      else stack_layer_dispatch_h<false>(max(dl, 1), xs, al, idg, node, d0, S.w0[L], S.w1[L], S.w0h[L], S.w1h[L],
+                                         li, lh, acc);
     } else if (gat) {
       stack_layer_dispatch<true>(dl, xs, al, idg, node, d0, S.w0[L], S.w1[L], li, lh, acc);
     } else {
@@ -827,12 +841,57 @@ extern "C" int a2m_graph_att_proj_f32(const float* w0, const float* att_src, con
   return A2M_OK;
 }
 
+// RNE fp32 -> bf16 with the k loop's conversion (stack_pack8), so a cached copy holds exactly the
+// values the loop would round to
+__global__ void to_bf16_kernel(const float* __restrict__ x, __bf16* __restrict__ y, int64_t n) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+  for (int64_t i = 2 * (blockIdx.x * (int64_t)blockDim.x + threadIdx.x); i < n;
+       i += 2 * (int64_t)gridDim.x * blockDim.x) {
+    if (i + 1 < n) {
+      *reinterpret_cast<h2*>(y + i) = __builtin_convertvector((f2{x[i], x[i + 1]}), h2);
+    } else {
+      y[i] = __builtin_convertvector((f2{x[i], 0.f}), h2)[0];
+    }
+  }
+}
+
+extern "C" int a2m_to_bf16_f32(const float* x, void* y, int64_t n, void* stream) {
+  A2M_CHECK_ARG(x && y && n >= 0, "to_bf16: bad args");
+  A2M_CHECK_ARG((reinterpret_cast<uintptr_t>(y) & 3) == 0, "to_bf16: y not 4-byte aligned");
+  if (n == 0) return A2M_OK;
+  const int blocks = (int)std::min<int64_t>(cdiv(cdiv(n, 2), 256), 1024);
+  hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x,
+                     static_cast<__bf16*>(y), n);
+  A2M_LAUNCH_CHECK();
+  return A2M_OK;
+}
+
+extern "C" int a2m_graph_stack_fwd_ex_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
+                                          const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
+                                          const float* const* w0, const float* const* w1,
+                                          const float* const* U, const float* const* bias,
+                                          const float* const* ln_w, const float* const* ln_b,
+                                          const void* const* w0h, const void* const* w1h, float slope,
+                                          float* y, void* stream);
+
 extern "C" int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
                                        const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
                                        const float* const* w0, const float* const* w1,
                                        const float* const* U, const float* const* bias,
                                        const float* const* ln_w, const float* const* ln_b,
                                        float slope, float* y, void* stream) {
+  return a2m_graph_stack_fwd_ex_f32(x, F, J, nbr_ptr, nbr_idx, nlayers, kinds, w0, w1, U, bias, ln_w, ln_b,
+                                    nullptr, nullptr, slope, y, stream);
+}
+
+extern "C" int a2m_graph_stack_fwd_ex_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
+                                          const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
+                                          const float* const* w0, const float* const* w1,
+                                          const float* const* U, const float* const* bias,
+                                          const float* const* ln_w, const float* const* ln_b,
+                                          const void* const* w0h, const void* const* w1h, float slope,
+                                          float* y, void* stream) {
   A2M_CHECK_ARG(w0 && w1, "graph_stack: null pointer");
   A2M_CHECK_ARG(x && y && nbr_ptr && nbr_idx && kinds && U && bias && ln_w && ln_b,
                 "graph_stack: null pointer");
@@ -853,6 +912,13 @@ extern "C" int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, con
     S.w0[L] = w0[L]; S.w1[L] = w1[L];
     S.U[L] = U[L];
     S.bias[L] = bias[L]; S.ln_w[L] = ln_w[L]; S.ln_b[L] = ln_b[L];
+    // the cached bf16 copies count only when every weight of the layer has one (16-byte aligned)
+    const void* h0 = w0h ? w0h[L] : nullptr;
+    const void* h1 = w1h && kinds[L] == 1 ? w1h[L] : nullptr;
+    const bool cached = S.bf16 && h0 && (kinds[L] == 0 || h1) &&
+                        ((reinterpret_cast<uintptr_t>(h0) | reinterpret_cast<uintptr_t>(h1)) & 15) == 0;
+    S.w0h[L] = cached ? static_cast<const __bf16*>(h0) : nullptr;
+    S.w1h[L] = cached ? static_cast<const __bf16*>(h1) : nullptr;
   }
   if (F == 0) return A2M_OK;
   const int fpb = GMAXN / J;

@@ -273,6 +273,21 @@ int a2m_graph_stack_fwd_f32(const float* x, int32_t F, int32_t J, const int32_t*
                             const float* const* w0, const float* const* w1, const float* const* U,
                             const float* const* bias, const float* const* ln_w,
                             const float* const* ln_b, float slope, float* y, void* stream);
+/* The same with bf16 copies of the layer weights for the bf16 operand mode (precision 1):
+ * w0h[l] / w1h[l] are device buffers holding w0[l] / w1[l] rounded to bf16 (a2m_to_bf16_f32, same
+ * [row][64] layout, 16-byte aligned), made once per weight version, so the layers' k loops load
+ * ready bf16 fragments instead of rounding the fp32 weights each time (the same values: the
+ * result is bitwise that of a2m_graph_stack_fwd_f32).  w0h / w1h (the arrays or a layer's
+ * entries) may be NULL; ignored at precision 0. */
+int a2m_graph_stack_fwd_ex_f32(const float* x, int32_t F, int32_t J, const int32_t* nbr_ptr,
+                               const int32_t* nbr_idx, int32_t nlayers, const int32_t* kinds,
+                               const float* const* w0, const float* const* w1, const float* const* U,
+                               const float* const* bias, const float* const* ln_w,
+                               const float* const* ln_b, const void* const* w0h,
+                               const void* const* w1h, float slope, float* y, void* stream);
+/* y[i] = bf16(x[i]), round to nearest even (the rounding the bf16 operand mode applies), n
+ * elements; y 4-byte aligned, 2 bytes an element. */
+int a2m_to_bf16_f32(const float* x, void* y, int64_t n, void* stream);
 /* ---------------------------------------------------------------- skeleton graph layers
  * One fused GNN step of the body / hand decoders (real_motion_model.py:173-201, 225-253):
  *   y = LeakyReLU(LayerNorm64(L(x))) + x

@@ -483,11 +483,22 @@ def test_graph_stack_bf16_mode(part, J, lo):
             layers.append((1, dv(wr), dv(wo), None, dv(br), dv(lnw), dv(lnb)))
         ref = torch.nn.functional.leaky_relu(torch.nn.functional.layer_norm(g, (64,), lnw, lnb), 0.2) + ref
     out32 = F.graph_stack(dv(x), J, dv(ptr), dv(idx), layers).cpu()
+    # the layer weights' cached bf16 copies (a2m_to_bf16_f32: the same RNE values torch's cast
+    # gives) feed the k loops the values it would round itself: bitwise the same stack output
+    wh = [F.graph_weights_bf16(Lr[1], Lr[2], {}) for Lr in layers]
+    for Lr, (h0, h1) in zip(layers, wh):
+        assert torch.equal(h0.cpu(), Lr[1].cpu().to(torch.bfloat16))
+        assert h1 is None or torch.equal(h1.cpu(), Lr[2].cpu().to(torch.bfloat16))
+    odd = dv(_rand(7, seed=170))
+    assert torch.equal(F.to_bf16(odd).cpu(), odd.cpu().to(torch.bfloat16))
     prev = a2m.set_gemm_precision('bf16')
     try:
         out16 = F.graph_stack(dv(x), J, dv(ptr), dv(idx), layers).cpu()
+        out16h = F.graph_stack(dv(x), J, dv(ptr), dv(idx), layers, wh=wh).cpu()
     finally:
         a2m.set_gemm_precision(prev)
+    assert torch.equal(out16, out16h)
+    assert torch.equal(F.graph_stack(dv(x), J, dv(ptr), dv(idx), layers, wh=wh).cpu(), out32)  # fp32 ignores wh
     e16, e32 = rel_err(out16, ref), rel_err(out32, ref)
     print(f'{part}: bf16 stack vs oracle {e16:.2e}, fp32 stack {e32:.2e}')
     assert e32 < TOL and 1e-6 < e16 < 3e-2, (e16, e32)

@@ -1,7 +1,7 @@
 """Times the fused eval graph stack (a2m_graph_stack_fwd_f32: GAT, GraphConv, GAT, GraphConv,
 GAT) at the bench shapes: hand (J=42) and body (J=10) over B*T = 4096 frames, each alone on the
 chip.
-    python tools/stack_bench.py [hand|body|both] [iters] [bf16]"""
+    python tools/stack_bench.py [hand|body|both] [iters] [bf16 [nowh]]"""
 import os
 import sys
 
@@ -14,7 +14,7 @@ from a2m import skeleton as S  # noqa: E402
 
 dev = torch.device('cuda')
 FR = 4096
-argv = [a for a in sys.argv[1:] if a != 'bf16']
+argv = [a for a in sys.argv[1:] if a not in ('bf16', 'nowh')]
 if 'bf16' in sys.argv[1:]:   # the bf16 operand mode's stack (layer products on the bf16 MFMA)
     import a2m
     a2m.set_gemm_precision('bf16')
@@ -42,12 +42,15 @@ for name, J, lo in (('hand', 42, 10), ('body', 10, 0)):
         else:
             layers.append((1, rnd(64, 64, scale=0.12), rnd(64, 64, scale=0.12), None, rnd(64, scale=0.1), lnw, lnb, {}))
     out = torch.empty_like(x)
+    # bf16 mode: the layer weights' cached bf16 copies, as the model passes them (nowh: without)
+    wh = [F.graph_weights_bf16(Lr[1], Lr[2], {}) for Lr in layers] \
+        if 'bf16' in sys.argv[1:] and 'nowh' not in sys.argv[1:] else None
     for _ in range(3):
-        F.graph_stack(x, J, ptr, idx, layers, out=out)
+        F.graph_stack(x, J, ptr, idx, layers, out=out, wh=wh)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
-        F.graph_stack(x, J, ptr, idx, layers, out=out)
+        F.graph_stack(x, J, ptr, idx, layers, out=out, wh=wh)
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / iters
