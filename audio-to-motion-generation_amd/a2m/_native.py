@@ -91,6 +91,7 @@ SIGNATURES = {
                                                  I32, U64, I32, F32, P, I64, P, P, P, SZ, P]),
     'a2m_self_attention_eval_fits': (I32, [I32, I32]),
     'a2m_self_attention_eval_f32': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, P, I64, P]),
+    'a2m_self_attention_eval_ex_f32': (ctypes.c_int, [P, I64, I32, I32, I32, P, P, P, P, P, I64, P, P]),
     'a2m_self_attention_eval_group_f32': (ctypes.c_int, [P, I64, I64, I32, I32, I32, I32, P, P, P, P, I64,
                                                          P, I64, P]),
     'a2m_conv1d_tap_group_fwd_f32': (ctypes.c_int, [P, I64, I64, I64, I32, I32, I32, I32, P, I64, I32, P,

@@ -414,6 +414,8 @@ _ATTN_EVAL_FUSED = True
 # bf16 operand mode: the fused eval attention with its projection on the bf16 MFMA
 # (False: the engine's bf16 QKV GEMM + the attention core, as in round 4; tests compare the two)
 _ATTN_EVAL_BF16 = True
+# bf16 mode: the fused eval attention stages a cached bf16 copy of its stacked weights
+_ATTN_BF16_WEIGHTS = True
 
 
 def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=None, cache=None):
@@ -432,9 +434,16 @@ def self_attention(x, wq, bq, wk, bk, wv, bv, gamma, res=None, out=None, save=No
     if save is None and _ATTN_EVAL_FUSED and N.lib.a2m_self_attention_eval_fits(C, T) and \
             x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 and \
             N.lib.a2m_get_gemm_precision() in ((0, 1) if _ATTN_EVAL_BF16 else (0,)):
-        # inference: q/k/v projections fused into the attention core, one launch
-        N.check(N.lib.a2m_self_attention_eval_f32(_p(x), x.stride(0), B, C, T, _p(wqkv), _p(bqkv), _p(gamma),
-                                                  _p(res), _p(out), out.stride(0), _stream()))
+        # inference: q/k/v projections fused into the attention core, one launch (bf16 mode: the
+        # stacked weights' bf16 copy, cached per weight version, when the module keeps a cache)
+        wh = None
+        if cache is not None and _ATTN_BF16_WEIGHTS and N.lib.a2m_get_gemm_precision() == 1:
+            key = _wkey((wq, bq, wk, bk, wv, bv))
+            if cache.get('hkey') != key:
+                cache.update(hkey=key, wh=to_bf16(wqkv.contiguous()))
+            wh = cache['wh']
+        N.check(N.lib.a2m_self_attention_eval_ex_f32(_p(x), x.stride(0), B, C, T, _p(wqkv), _p(bqkv), _p(gamma),
+                                                     _p(res), _p(out), out.stride(0), _p(wh), _stream()))
         return out
     qkv = torch.empty(B, C // 4 + C, T, device=x.device, dtype=x.dtype)
     attn = torch.empty(B, T, T, device=x.device, dtype=x.dtype)

@@ -213,8 +213,10 @@ int attn_core(const float* qkv, int64_t qs_b, int B, int C, int T, const float* 
 bool attn_fused_eval_fits(int C, int T);
 // G > 1: G problems with their own weights (wqkv / bqkv / gamma stacked per problem) over
 // x + g*x_gs, res + g*res_gs, y + g*y_gs (grouped decoder branches)
+// wqkv_h (bf16 mode only, may be null): wqkv rounded to bf16 (a2m_to_bf16_f32), staged as is
 int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const float* wqkv,
                     const float* bqkv, const float* gamma, const float* res, float* y,
-                    hipStream_t st, int G = 1, int64_t x_gs = 0, int64_t res_gs = 0, int64_t y_gs = 0);
+                    hipStream_t st, int G = 1, int64_t x_gs = 0, int64_t res_gs = 0, int64_t y_gs = 0,
+                    const void* wqkv_h = nullptr);
 
 }  // namespace a2m

@@ -166,6 +166,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
 constexpr int QP = 36;        // Q^T / K^T pitch (32 columns): conflict-free b128 rows
 constexpr int FK = 32;        // projection k-tile (channels)
 constexpr int FKP = FK + 4;   // staged tile pitch
+constexpr int kHWP = FK + 8;  // bf16 weight tile pitch (halves): conflict-free b128 fragment rows
 // V channels per workgroup at C % 128 == 0.  128 computes a C = 256 clip's Q / K twice instead of
 // four times: the kernel's time drops 358.5 -> 305.8 us a step, but the step got 0.5-0.7 % slower
 // (fp32 2.520 vs 2.503 ms, bf16 1.439 vs 1.432, three interleaved pairs,
@@ -199,17 +200,24 @@ __device__ __forceinline__ bf16x8 attn_pack8(const float (&v)[8]) {
 // projection 1.33x the non-redundant 5C/4 rows instead of 1.6x); every output element sees the
 // same operations in the same order at either NV, so the two are bitwise equal (NV = 64 is the
 // default, A2M_ATTN_NV below).
-template <bool BF16, int NV>
+// WH (bf16 mode): the stacked weights come as a bf16 copy (wqkv_h, made once per weight version)
+// and are staged as bf16 -- one 16-byte load and store per thread a k-tile instead of two, and the
+// fragments read ready for the MFMA instead of rounded at every read; the same values, so bitwise
+// the same result.
+template <bool BF16, int NV, bool WH = false>
 __global__ __launch_bounds__(NV == 64 ? 512 : 768, NV == 64 ? 2 : 1) void attn_fused_eval_kernel(
     const float* __restrict__ x, int64_t x_bs, int C, int T, const float* __restrict__ wqkv,
     const float* __restrict__ bqkv, const float* __restrict__ gamma, const float* __restrict__ res,
-    float* __restrict__ y, int B, int64_t x_gs, int64_t res_gs, int64_t y_gs) {
+    float* __restrict__ y, int B, int64_t x_gs, int64_t res_gs, int64_t y_gs,
+    const __bf16* __restrict__ wqkv_h) {
+  static_assert(BF16 || !WH, "bf16 weights only in bf16 mode");
   {  // grouped launches: blockIdx.y = g * B + b, problem g with its own weights
     const int g = blockIdx.y / B;
     x += g * x_gs;
     y += g * y_gs;
     if (res) res += g * res_gs;
     wqkv += (int64_t)g * (C / 4 + C) * C;
+    if (WH) wqkv_h += (int64_t)g * (C / 4 + C) * C;
     bqkv += (int64_t)g * (C / 4 + C);
     gamma += g;
   }
@@ -243,17 +251,26 @@ __global__ __launch_bounds__(NV == 64 ? 512 : 768, NV == 64 ? 2 : 1) void attn_f
   // 0), so the k-step below is branch-free and its operand work is placed between the MFMAs
   // (pipe_step, gemm_pipe.h: tile i + 1 stored and tile i + 3 loaded behind the first half's
   // MFMAs, one barrier, the next fragments read behind the second half's first MFMAs).
-  const __amdgpu_buffer_rsrc_t xrs = pipe_rsrc(xb), wrs = pipe_rsrc(wqkv);
+  const __amdgpu_buffer_rsrc_t xrs = pipe_rsrc(xb),
+                               wrs = pipe_rsrc(WH ? reinterpret_cast<const float*>(wqkv_h) : wqkv);
   const int xc = tid & 31, xq = tid >> 5;
   const bool xst = xq < AT / 4;   // this thread stages a piece of the x tile
   uint32_t xoff = 4 * xq < T ? (uint32_t)(xc * T + 4 * xq) * 4u : kPipeOOB;   // advanced 32 channels a tile
   uint32_t woff[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int col = (tid + u * NT) >> 3;
+  if constexpr (WH) {   // one 16-byte piece (8 bf16 of k) per thread: row tid / 4, k 8 (tid % 4)
+    const int col = tid >> 2;
     const int wrow = col < 32 ? (col < Cq ? col : -1)
                               : col < 64 ? (col - 32 < Cq ? Cq + col - 32 : -1) : 2 * Cq + c0 + col - 64;
-    woff[u] = wrow >= 0 ? (uint32_t)(wrow * C + ((tid + u * NT) & 7) * 4) * 4u : kPipeOOB;
+    woff[0] = wrow >= 0 && col < FC ? (uint32_t)(wrow * C + (tid & 3) * 8) * 2u : kPipeOOB;
+    woff[1] = kPipeOOB;
+  } else {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int col = (tid + u * NT) >> 3;
+      const int wrow = col < 32 ? (col < Cq ? col : -1)
+                                : col < 64 ? (col - 32 < Cq ? Cq + col - 32 : -1) : 2 * Cq + c0 + col - 64;
+      woff[u] = wrow >= 0 ? (uint32_t)(wrow * C + ((tid + u * NT) & 7) * 4) * 4u : kPipeOOB;
+    }
   }
   struct Regs { float4 x, w[2]; };
   Regs rg[2];
@@ -264,6 +281,7 @@ __global__ __launch_bounds__(NV == 64 ? 512 : 768, NV == 64 ? 2 : 1) void attn_f
   auto load_piece = [&](Regs& r, int piece) {   // piece 0: x, 1-2: w rows
     const bool ok = cnext < C;
     if (piece == 0) { r.x = pipe_load(xrs, ok ? xoff : kPipeOOB); xoff += 4u * FK * T; }
+    else if (WH) { if (piece == 1) { r.w[0] = pipe_load(wrs, ok ? woff[0] : kPipeOOB); woff[0] += 2u * FK; } }
     else { r.w[piece - 1] = pipe_load(wrs, ok ? woff[piece - 1] : kPipeOOB); woff[piece - 1] += 4u * FK; }
     if (piece == 2) cnext += FK;
   };
@@ -273,6 +291,9 @@ __global__ __launch_bounds__(NV == 64 ? 512 : 768, NV == 64 ? 2 : 1) void attn_f
       float* xs = st + (4 * xq + 2 * piece) * FKP + xc;
       xs[0] = piece == 0 ? r.x.x : r.x.z;
       xs[FKP] = piece == 0 ? r.x.y : r.x.w;
+    } else if (WH) {   // the bf16 w tile: [col][k] rows of kHWP halves
+      if (piece == 2 && tid < 4 * FC)
+        *reinterpret_cast<float4*>(reinterpret_cast<__bf16*>(st + XT) + (tid >> 2) * kHWP + (tid & 3) * 8) = r.w[0];
     } else {
       const int e = tid + (piece - 2) * NT;
       *reinterpret_cast<float4*>(st + XT + (e >> 3) * FKP + (e & 7) * 4) = r.w[piece - 2];
@@ -284,14 +305,20 @@ __global__ __launch_bounds__(NV == 64 ? 512 : 768, NV == 64 ? 2 : 1) void attn_f
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const int nk = C / FK;   // even (C in {128, 256})
   const int arow = (pt * 32 + li) * FKP + lh * 8, brow = XT + (pc * 32 + li) * FKP + lh * 8;
+  const int bhrow = (pc * 32 + li) * kHWP + lh * 8;   // WH: in halves from the w tile's start
+  auto hfrag = [&](const float* stage, int k) {
+    return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(stage + XT) + bhrow + k);
+  };
   float fa0[8], fb0[8];
+  bf16x8 hb0;
   for (int pc2 = 0; pc2 < 3; ++pc2) load_piece(rg[0], pc2);   // tile 0
   for (int pc2 = 0; pc2 < 3; ++pc2) load_piece(rg[1], pc2);   // tile 1
   for (int pc2 = 0; pc2 < 4; ++pc2) store_piece(lds, rg[0], pc2);
   for (int pc2 = 0; pc2 < 3; ++pc2) load_piece(rg[0], pc2);   // tile 2
   __syncthreads();
   pipe_frag(lds + arow, fa0);
-  pipe_frag(lds + brow, fb0);
+  if constexpr (WH) hb0 = hfrag(lds, 0);
+  else pipe_frag(lds + brow, fb0);
   // step i: tile i in stage i & 1; stores tile i + 1 from set (i + 1) & 1, then loads tile
   // i + 3 into that set (tiles past nk read channels past C: harmless, never stored as used)
   auto step = [&](auto par, int i) {
@@ -303,18 +330,21 @@ __global__ __launch_bounds__(NV == 64 ? 512 : 768, NV == 64 ? 2 : 1) void attn_f
       // the first half's MFMA, tile i + 1's stores and tile i + 3's loads, the barrier, the second
       // half's MFMA, tile i + 1's first-half fragments
       float fa1[8], fb1[8];
+      bf16x8 hb1;
       pipe_frag(cur + arow + 16, fa1);
-      pipe_frag(cur + brow + 16, fb1);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(attn_pack8(fa0), attn_pack8(fb0), acc, 0, 0, 0);
+      if constexpr (WH) hb1 = hfrag(cur, 16);
+      else pipe_frag(cur + brow + 16, fb1);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(attn_pack8(fa0), WH ? hb0 : attn_pack8(fb0), acc, 0, 0, 0);
 #pragma unroll
       for (int s = 0; s < 4; ++s) store_piece(nxt, rg[Q], s);
 #pragma unroll
       for (int s = 0; s < 3; ++s) load_piece(rg[Q], s);
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(attn_pack8(fa1), attn_pack8(fb1), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(attn_pack8(fa1), WH ? hb1 : attn_pack8(fb1), acc, 0, 0, 0);
       pipe_frag(nxt + arow, fa0);
-      pipe_frag(nxt + brow, fb0);
+      if constexpr (WH) hb0 = hfrag(nxt, 0);
+      else pipe_frag(nxt + brow, fb0);
     } else {
       pipe_step(acc, fa0, fb0, cur + arow, cur + brow, nxt + arow, nxt + brow, [&](int s) {
         if (s < 4) store_piece(nxt, rg[Q], s);
@@ -656,27 +686,36 @@ int attn_core_wide(const float* qkv, int64_t qs_b, int B, int C, int T, const fl
   return A2M_OK;
 }
 
+template <int NV>
+static void attn_fused_eval_launch(bool bf16, bool wh, dim3 grid, hipStream_t st, const float* x, int64_t x_bs,
+                                   int C, int T, const float* wqkv, const float* bqkv, const float* gamma,
+                                   const float* res, float* y, int B, int64_t x_gs, int64_t res_gs,
+                                   int64_t y_gs, const __bf16* wqkv_h) {
+  const dim3 blk(NV == 64 ? 512 : 768);
+  if (bf16 && wh)
+    hipLaunchKernelGGL((attn_fused_eval_kernel<true, NV, true>), grid, blk, 0, st, x, x_bs, C, T, wqkv, bqkv,
+                       gamma, res, y, B, x_gs, res_gs, y_gs, wqkv_h);
+  else if (bf16)
+    hipLaunchKernelGGL((attn_fused_eval_kernel<true, NV>), grid, blk, 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
+                       res, y, B, x_gs, res_gs, y_gs, wqkv_h);
+  else
+    hipLaunchKernelGGL((attn_fused_eval_kernel<false, NV>), grid, blk, 0, st, x, x_bs, C, T, wqkv, bqkv, gamma,
+                       res, y, B, x_gs, res_gs, y_gs, wqkv_h);
+}
+
 int attn_fused_eval(const float* x, int64_t x_bs, int B, int C, int T, const float* wqkv,
                     const float* bqkv, const float* gamma, const float* res, float* y,
-                    hipStream_t st, int G, int64_t x_gs, int64_t res_gs, int64_t y_gs) {
+                    hipStream_t st, int G, int64_t x_gs, int64_t res_gs, int64_t y_gs, const void* wqkv_h) {
   const bool bf16 = a2m_get_gemm_precision() == 1;
-  if (g_attn_nv == 128 && C % 128 == 0) {
-    dim3 grid((unsigned)(C / 128), (unsigned)(B * G));
-    if (bf16)
-      hipLaunchKernelGGL((attn_fused_eval_kernel<true, 128>), grid, dim3(768), 0, st, x, x_bs, C, T, wqkv, bqkv,
-                         gamma, res, y, B, x_gs, res_gs, y_gs);
-    else
-      hipLaunchKernelGGL((attn_fused_eval_kernel<false, 128>), grid, dim3(768), 0, st, x, x_bs, C, T, wqkv, bqkv,
-                         gamma, res, y, B, x_gs, res_gs, y_gs);
-  } else {
-    dim3 grid((unsigned)cdiv(C, 64), (unsigned)(B * G));
-    if (bf16)
-      hipLaunchKernelGGL((attn_fused_eval_kernel<true, 64>), grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv,
-                         gamma, res, y, B, x_gs, res_gs, y_gs);
-    else
-      hipLaunchKernelGGL((attn_fused_eval_kernel<false, 64>), grid, dim3(512), 0, st, x, x_bs, C, T, wqkv, bqkv,
-                         gamma, res, y, B, x_gs, res_gs, y_gs);
-  }
+  // the bf16 copy counts when 16-byte aligned (rows of C halves are then 16-byte aligned too)
+  const bool wh = wqkv_h != nullptr && (reinterpret_cast<uintptr_t>(wqkv_h) & 15) == 0;
+  const __bf16* h = static_cast<const __bf16*>(wqkv_h);
+  if (g_attn_nv == 128 && C % 128 == 0)
+    attn_fused_eval_launch<128>(bf16, wh, dim3((unsigned)(C / 128), (unsigned)(B * G)), st, x, x_bs, C, T, wqkv,
+                                bqkv, gamma, res, y, B, x_gs, res_gs, y_gs, h);
+  else
+    attn_fused_eval_launch<64>(bf16, wh, dim3((unsigned)cdiv(C, 64), (unsigned)(B * G)), st, x, x_bs, C, T, wqkv,
+                               bqkv, gamma, res, y, B, x_gs, res_gs, y_gs, h);
   A2M_LAUNCH_CHECK();
   return A2M_OK;
 }

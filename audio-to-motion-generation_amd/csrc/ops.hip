@@ -1457,6 +1457,18 @@ int a2m_self_attention_eval_f32(const float* x, int64_t x_bs, int32_t B, int32_t
   return attn_fused_eval(x, x_bs, B, C, T, wqkv, bqkv, gamma, res, y, as_stream(stream));
 }
 
+int a2m_self_attention_eval_ex_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
+                                   const float* wqkv, const float* bqkv, const float* gamma,
+                                   const float* res, float* y, int64_t y_bs, const void* wqkv_h,
+                                   void* stream) {
+  A2M_CHECK_ARG(x && wqkv && bqkv && gamma && y && B > 0, "self_attention_eval: null pointer");
+  A2M_CHECK_ARG(attn_fused_eval_fits(C, T), "self_attention_eval: C=%d T=%d not supported (C in {128, 256}, T <= 64, T %% 4 == 0)", C, T);
+  A2M_CHECK_ARG(x_bs == y_bs && x_bs % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+                "self_attention_eval: x / y layout (batch stride %lld)", (long long)x_bs);
+  A2M_CHECK_ARG(fits32((int64_t)B * x_bs), "self_attention_eval: too large");
+  return attn_fused_eval(x, x_bs, B, C, T, wqkv, bqkv, gamma, res, y, as_stream(stream), 1, 0, 0, 0, wqkv_h);
+}
+
 int a2m_self_attention_fwd_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
                                const float* wq, const float* bq, const float* wk, const float* bk,
                                const float* wv, const float* bv, const float* gamma,

@@ -229,6 +229,14 @@ int32_t a2m_self_attention_eval_fits(int32_t C, int32_t T);
 int a2m_self_attention_eval_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
                                 const float* wqkv, const float* bqkv, const float* gamma,
                                 const float* res, float* y, int64_t y_bs, void* stream);
+/* The same with wqkv_h, wqkv rounded to bf16 (a2m_to_bf16_f32, 16-byte aligned; made once per
+ * weight version), for the bf16 operand mode: the projection stages the ready bf16 weights
+ * instead of rounding the fp32 ones in every workgroup -- bitwise the same result.  wqkv_h may
+ * be NULL; ignored at precision 0. */
+int a2m_self_attention_eval_ex_f32(const float* x, int64_t x_bs, int32_t B, int32_t C, int32_t T,
+                                   const float* wqkv, const float* bqkv, const float* gamma,
+                                   const float* res, float* y, int64_t y_bs, const void* wqkv_h,
+                                   void* stream);
 
 /* G such problems in one launch (grid G*B): problem g has its own wqkv + g*(C/4 + C)*C,
  * bqkv + g*(C/4 + C), gamma + g, and reads x + g*x_gs (batch stride x_bs, also y's), res +

@@ -248,19 +248,24 @@ def test_self_attention(B, C, T):
         # the fused kernel's V chunks of 64 channels (the default) and of 128 (Q / K once per two
         # 64-channel chunks): the same operations per output element, so bitwise equal, fp32 and
         # bf16 operand modes
+        # In bf16 mode also with the module cache, i.e. the stacked weights' cached bf16 copy
+        # staged as is (a2m_self_attention_eval_ex_f32): the values the kernel would round to.
         outs = {}
         try:
             for prec in (0, 1):
                 N.check(N.lib.a2m_set_gemm_precision(prec))
                 for nv in (64, 128):
                     N.check(N.lib.a2m_set_attn_eval_chunk(nv))
-                    outs[prec, nv] = F.self_attention(
-                        x.to(DEV), d['a.query_conv.weight'], d['a.query_conv.bias'], d['a.key_conv.weight'],
-                        d['a.key_conv.bias'], d['a.value_conv.weight'], d['a.value_conv.bias'], d['a.gamma'],
-                        res=res.to(DEV)).cpu()
+                    for cached in ((False, True) if prec == 1 else (False,)):
+                        outs[prec, nv, cached] = F.self_attention(
+                            x.to(DEV), d['a.query_conv.weight'], d['a.query_conv.bias'], d['a.key_conv.weight'],
+                            d['a.key_conv.bias'], d['a.value_conv.weight'], d['a.value_conv.bias'], d['a.gamma'],
+                            res=res.to(DEV), cache={} if cached else None).cpu()
         finally:
             N.lib.a2m_set_attn_eval_chunk(64)
             N.lib.a2m_set_gemm_precision(0)
+        outs = {k[:2] if not k[2] else k: v for k, v in outs.items()}
+        assert torch.equal(outs[1, 64], outs[1, 64, True]) and torch.equal(outs[1, 128], outs[1, 128, True])
         assert torch.equal(outs[0, 64], outs[0, 128]) and torch.equal(outs[1, 64], outs[1, 128])
         assert torch.equal(outs[0, 64], out.cpu())
         assert N.lib.a2m_set_attn_eval_chunk(96) == N.A2M_EINVAL
