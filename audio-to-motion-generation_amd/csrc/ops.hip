@@ -1371,11 +1371,17 @@ int a2m_self_attention_packed_fwd_f32(const float* x, int64_t x_bs, int32_t B, i
   const int64_t qs_b = (int64_t)Cqkv * T;
   // q, k, v as ONE 1x1 convolution with the stacked weights: qkv[b][0:Cq | Cq:2Cq | 2Cq:][t]
   int rc;
-  if (C >= 1024 && T <= TR_MAXT) {
-    // wide channels (the UNet's SelfAttention(2048)): x is first copied to [B*T][C] so the
-    // projection GEMM reads both operands as dense k-contiguous rows instead of gathering x's
-    // t-runs (mode 3): 255 -> ~220 us for the up_attention projection at T = 32, for a copy of
-    // a few microseconds.  Same k order, so the same result bit for bit.
+#ifndef A2M_WIDE_BTC
+#define A2M_WIDE_BTC 2   // 0 never, 1 always, 2 in the bf16 operand mode only
+#endif
+  if ((A2M_WIDE_BTC == 1 || (A2M_WIDE_BTC == 2 && a2m_get_gemm_precision() != 0)) && C >= 1024 &&
+      T <= TR_MAXT) {
+    // wide channels (the UNet's SelfAttention(2048)) in bf16 mode: x is first copied to [B*T][C]
+    // so the projection GEMM reads both operands as dense k-contiguous rows instead of gathering
+    // x's t-runs (mode 3).  Round 6, with the pipelined tiles: the bf16 step 1.293 vs 1.494 ms
+    // without the copy, the fp32 step 2.257 vs 2.242 ms (the fp32 pipelined tile gathers the
+    // t-runs well), so fp32 skips it (profiles/r06_q_wide_btc_ab.txt).  Same k order either way,
+    // so the same result bit for bit.
     const size_t xt_bytes = (((size_t)B * T * C * sizeof(float)) + 255) & ~size_t(255);
     const size_t need = xt_bytes + gemm_ws_bytes(Cqkv, B * T, C, 1);
     if (!ws || ws_bytes < need) {
