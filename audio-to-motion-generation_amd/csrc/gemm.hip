@@ -352,30 +352,11 @@ static const PlanRule* plan_rule(int M, int N, int K) {
   return nullptr;
 }
 
-// Plans tuned in the replayed bench step (fp32; A2M_GEMM_TUNED=0 turns the table off): the
-// UNet's large tap-chunked convs, where the planner's isolated fit prefers 128x128 tiles with 4
-// or 8 splits but the step runs faster on 64x64 tiles with 2 (r04: in-step sweeps with
-// A2M_GEMM_PLAN_RULES, three rounds each, 2.698-2.707 vs 2.716 ms for the first entry;
-// DESIGN.md 6 Round 4)
-static const PlanRule kTunedPlans[] = {
-    {1024, 2048, 6144, 64, 2},   // UNet up conv, T 32
-    {512, 4096, 3072, 64, 2},    // UNet up conv, T 64
-    {512, 2048, 1024, 64, 2},
-    // round 5, with the pipelined 64x64 tile (two interleaved rounds each, r05 plan sweep): the
-    // UNet's last two 128x128 launches move to it
-    {1024, 1024, 4096, 64, 2},   // down conv (im2col) + convT phase: 2.347-2.355 vs 2.379 ms
-    {2048, 1024, 3072, 64, 1},   // conv1d k3 at T 16 (halo pipe): 2.342-2.344 vs 2.379 ms
-    {1024, 1024, 2048, 64, 1},   // convT phase (2 taps): 2.335-2.348 vs 2.342-2.370 ms (weak)
-    {256, 4096, 2688, 64, 1},    // hand graph-stack output projection: 1 split instead of 2 (weaker
-                                 // evidence: mean 2.694 vs 2.705 ms and 2.719 vs 2.753 ms on two noisy
-                                 // boxes, seven of ten rounds lower)
-};
-static const PlanRule* tuned_plan(int M, int N, int K, int prec) {
-  if (prec != 0) return nullptr;
-  for (const PlanRule& r : kTunedPlans)
-    if (r.M == M && r.N == N && r.K == K) return &r;
-  return nullptr;
-}
+// (Rounds 4-5 kept a table of seven fp32 plans tuned in the replayed bench step -- 64x64 tiles
+// with 2 splits on the UNet's large tap convs, 1 split on the hand stack's proj_out.  With the
+// round-6 kernels the planner's own choices measured faster: 2.245 vs 2.228 ms and 2.473 vs
+// 2.448 ms, three interleaved rounds on each of two boxes, training neutral
+// (profiles/r06_r_tuned_plans_ab.txt); the table is gone.)
 
 // bf16 (prec 1) throughput per CU by resident blocks, flop / us: staging- and latency-bound
 // rather than MFMA-bound (16x the f32 MFMA rate), so it grows with the blocks a CU holds far more
@@ -468,8 +449,8 @@ static size_t split_ws_bytes(const Plan& p, int M, int N, int batch) {
   return (size_t)p.splits * batch * M * (size_t)N * sizeof(float);
 }
 
-// the plan gemm() launches: the planner's, unless a tuned-table entry or an A2M_GEMM_PLAN_RULES
-// rule fixes the tile / split count for the shape
+// the plan gemm() launches: the planner's, unless an A2M_GEMM_PLAN_RULES rule fixes the tile /
+// split count for the shape
 static Plan launch_plan(int M, int N, int K, int batch, bool gathered, int prec, int kquant, bool rows6,
                         int force_split, bool pipe64 = false) {
   Plan p = plan_for(M, N, K, batch, gathered, prec, kquant, rows6, pipe64);
@@ -477,9 +458,7 @@ static Plan launch_plan(int M, int N, int K, int batch, bool gathered, int prec,
     p.kchunk = (int)(cdiv(cdiv(K, force_split), p.bk * kquant) * p.bk * kquant);
     p.splits = (int)cdiv(K, p.kchunk);
   }
-  const PlanRule* rule = plan_rule(M, N, K);
-  if (!rule && force_split <= 0 && g_override_split == 0 && g_override_tile == 0) rule = tuned_plan(M, N, K, prec);
-  if (const PlanRule* r = rule) {
+  if (const PlanRule* r = plan_rule(M, N, K)) {
     if (r->tile) p.bm = r->tile;
     if (r->splits > 0) {
       p.kchunk = (int)(cdiv(cdiv(K, r->splits), p.bk * kquant) * p.bk * kquant);
