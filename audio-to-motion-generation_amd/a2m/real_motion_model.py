@@ -277,9 +277,11 @@ class SelfAttention_G(_GraphTopology):
             main = torch.cuda.current_stream(audio.device)
             side = _side_stream(audio.device)
             side.wait_stream(main)
+            first, second = (('hand', self.body_feats), ('body', 0)) if _HAND_ON_SIDE else \
+                (('body', 0), ('hand', self.body_feats))
             with torch.cuda.stream(side):
-                self._branch('hand', feats, out, self.body_feats)
-            self._branch('body', feats, out, 0)
+                self._branch(first[0], feats, out, first[1])
+            self._branch(second[0], feats, out, second[1])
             main.wait_stream(side)
         else:
             self._branch('body', feats, out, 0)
@@ -314,6 +316,8 @@ class SelfAttention_G(_GraphTopology):
 
 
 _BRANCH_STREAMS = os.environ.get('A2M_BRANCH_STREAMS', '1') != '0'
+# the hand branch (the longer one) forked onto the side stream and issued first; False: the body
+_HAND_ON_SIDE = True
 # body + hand decoder layers as grouped launches: 0 off, 1 decoder_pre grouped (the rest per
 # branch on two streams), 2 decoder_pre and decoder_post grouped
 _GROUPED = 0
