@@ -400,7 +400,10 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   // launch's reduce at 200 % the encoder measured 0.2906-0.2937 vs 0.2951-0.2971 ms but the step
   // neutral to slightly slower (three rounds); on the encoder's launches only: in-step
   // path_frac 0.480-0.484 vs 0.473-0.476, step 2.718-2.727 vs 2.721-2.737 ms (four rounds, r04s)
-  constexpr double red_scale_rows = 2.0;
+#ifndef A2M_RED_SCALE_ROWS
+#define A2M_RED_SCALE_ROWS 2.0
+#endif
+  constexpr double red_scale_rows = A2M_RED_SCALE_ROWS;
   if (splits > 1)
     t += (conv_rows ? red_scale_rows : red_scale) *
          ((splits + 1.0) * M * N * (double)batch * 4.0 / 3.5e6 + (prec == 1 ? A2M_RED_FIXED_US_BF16 : A2M_RED_FIXED_US));
