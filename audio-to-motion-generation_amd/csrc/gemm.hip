@@ -385,7 +385,14 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   const int c = (int)std::min<int64_t>(per_cu, occ);
   double thr = prec == 2 ? (tile == 128 ? x6_thr128[c - 1] : x6_thr64[c - 1])
                          : (tile == 128 ? thr128[c - 1] : thr64[c - 1]);
-  if (gathered && tile == 64) thr *= 0.84;
+#ifndef A2M_THR64_SCALE
+#define A2M_THR64_SCALE 1.0   // diagnostic: the 64x64 tile's fitted throughput scaled
+#endif
+#ifndef A2M_GATHER_F
+#define A2M_GATHER_F 0.84
+#endif
+  if (prec == 0 && tile == 64) thr *= A2M_THR64_SCALE;
+  if (gathered && tile == 64) thr *= A2M_GATHER_F;
   // (channels-last conv rows, mode 6, run at the dense fit on the one-group 64x64 tile: a 0.87
   // factor measured slower, encoder 303.2 vs 300.0 us, tools/enc_plan_ab.py, round 3)
   if (prec == 1) thr = bf16_thr(tile, c) * (gathered && tile == 64 ? 0.84 : 1.0);
