@@ -395,7 +395,10 @@ static double plan_cost_us(int M, int N, int K, int batch, bool gathered, int ti
   if (gathered && tile == 64) thr *= A2M_GATHER_F;
   // (channels-last conv rows, mode 6, run at the dense fit on the one-group 64x64 tile: a 0.87
   // factor measured slower, encoder 303.2 vs 300.0 us, tools/enc_plan_ab.py, round 3)
-  if (prec == 1) thr = bf16_thr(tile, c) * (gathered && tile == 64 ? 0.84 : 1.0);
+#ifndef A2M_BF16_THR128_SCALE
+#define A2M_BF16_THR128_SCALE 1.0   // diagnostic: the bf16 128x128 tile's fitted throughput scaled
+#endif
+  if (prec == 1) thr = bf16_thr(tile, c) * (gathered && tile == 64 ? 0.84 : 1.0) * (tile == 128 ? A2M_BF16_THR128_SCALE : 1.0);
   const double block_flops = 2.0 * tile * tile * (double)kchunk;
   const double fixed = prec == 2 ? (tile == 128 ? 15.0 : 2.0)
                                  : (tile == 128 ? (gathered ? 16.0 : 10.0) : 3.0);
