@@ -561,8 +561,13 @@ __device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, co
   }
 }
 
-#ifndef STACK_WG_PER_CU_BF16   // three workgroups per CU as the fp32 stack (hand 228.7 us alone
-#define STACK_WG_PER_CU_BF16 3   // against 250 us at two, where its registers need no spills)
+// bf16 stack: two workgroups per CU (256 VGPRs, no spills).  Three (168 VGPRs, 114 spilled) won
+// while every wave rounded its fp32 weights in the k loop (hand 228.7 vs 250 us alone); with the
+// cached bf16 weights two is faster in the step -- hand 164 vs 159 us alone but body 53 vs 58.5 us,
+// and the other branch's kernels fit beside it: bf16 B = 64 1.354 -> 1.346 ms, B = 32 0.977 ->
+// 0.959 ms (profiles/r06_v_stack_wg_ab.txt)
+#ifndef STACK_WG_PER_CU_BF16
+#define STACK_WG_PER_CU_BF16 2
 #endif
 template <bool BF16>
 __global__ __launch_bounds__(256, BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU) void graph_stack_kernel(
