@@ -81,7 +81,10 @@ __global__ __launch_bounds__(512) void graph_att_proj_kernel(const float* __rest
 // neighbours' 8-float k-slices from the LDS node tile and issues the MFMAs.  LayerNorm(64),
 // LeakyReLU and the residual run on the accumulators (row reductions = 32-lane shuffles).
 // LDS = node tile + logits + lists (~40 KB): several workgroups per CU hide the HBM latency.
-__global__ __launch_bounds__(256, 3) void graph_layer_kernel(
+#ifndef GL_WG_PER_CU
+#define GL_WG_PER_CU 3
+#endif
+__global__ __launch_bounds__(256, GL_WG_PER_CU) void graph_layer_kernel(
     const float* __restrict__ x, int F, int J, int kind, int norm_res, const int* __restrict__ nbr_ptr,
     const int* __restrict__ nbr_idx, const float* __restrict__ w0, const float* __restrict__ w1,
     const float* __restrict__ att_src, const float* __restrict__ att_dst,
