@@ -572,8 +572,11 @@ __device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, co
 #ifndef STACK_WG_PER_CU_BF16
 #define STACK_WG_PER_CU_BF16 2
 #endif
-template <bool BF16>
-__global__ __launch_bounds__(256, BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU) void graph_stack_kernel(
+#ifndef STACK_WG_PER_CU_BF16_WIDE   // diagnostic: the bf16 stack's occupancy for J > 32 (the hand)
+#define STACK_WG_PER_CU_BF16_WIDE STACK_WG_PER_CU_BF16
+#endif
+template <bool BF16, int WG = (BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU)>
+__global__ __launch_bounds__(256, WG) void graph_stack_kernel(
     const float* __restrict__ x, int F, int J, const int* __restrict__ nbr_ptr,
     const int* __restrict__ nbr_idx, GraphStack S, float* __restrict__ y) {
   __shared__ __attribute__((aligned(16))) float xs[GMAXN * ZP];        // node-indexed tile
@@ -930,7 +933,10 @@ extern "C" int a2m_graph_stack_fwd_ex_f32(const float* x, int32_t F, int32_t J, 
   }
   if (F == 0) return A2M_OK;
   const int fpb = GMAXN / J;
-  if (S.bf16)
+  if (S.bf16 && J > 32 && STACK_WG_PER_CU_BF16_WIDE != STACK_WG_PER_CU_BF16)
+    hipLaunchKernelGGL((graph_stack_kernel<true, STACK_WG_PER_CU_BF16_WIDE>), dim3((unsigned)cdiv(F, fpb)), dim3(256),
+                       0, as_stream(stream), x, F, J, nbr_ptr, nbr_idx, S, y);
+  else if (S.bf16)
     hipLaunchKernelGGL(graph_stack_kernel<true>, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
                        x, F, J, nbr_ptr, nbr_idx, S, y);
   else
