@@ -575,6 +575,9 @@ __device__ __forceinline__ void stack_layer_dispatch(int dl, const float* xs, co
 #ifndef STACK_WG_PER_CU_BF16_WIDE   // diagnostic: the bf16 stack's occupancy for J > 32 (the hand)
 #define STACK_WG_PER_CU_BF16_WIDE STACK_WG_PER_CU_BF16
 #endif
+#ifndef STACK_WG_PER_CU_WIDE        // diagnostic: the fp32 stack's occupancy for J > 32 (the hand)
+#define STACK_WG_PER_CU_WIDE STACK_WG_PER_CU
+#endif
 template <bool BF16, int WG = (BF16 ? STACK_WG_PER_CU_BF16 : STACK_WG_PER_CU)>
 __global__ __launch_bounds__(256, WG) void graph_stack_kernel(
     const float* __restrict__ x, int F, int J, const int* __restrict__ nbr_ptr,
@@ -939,6 +942,9 @@ extern "C" int a2m_graph_stack_fwd_ex_f32(const float* x, int32_t F, int32_t J, 
   else if (S.bf16)
     hipLaunchKernelGGL(graph_stack_kernel<true>, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
                        x, F, J, nbr_ptr, nbr_idx, S, y);
+  else if (J > 32 && STACK_WG_PER_CU_WIDE != STACK_WG_PER_CU)
+    hipLaunchKernelGGL((graph_stack_kernel<false, STACK_WG_PER_CU_WIDE>), dim3((unsigned)cdiv(F, fpb)), dim3(256),
+                       0, as_stream(stream), x, F, J, nbr_ptr, nbr_idx, S, y);
   else
     hipLaunchKernelGGL(graph_stack_kernel<false>, dim3((unsigned)cdiv(F, fpb)), dim3(256), 0, as_stream(stream),
                        x, F, J, nbr_ptr, nbr_idx, S, y);
